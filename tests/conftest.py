@@ -1,0 +1,23 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for sub in ("oracle", "tfhe-gpu_amd"):
+    path = os.path.join(ROOT, sub)
+    if path not in sys.path:
+        sys.path.insert(0, path)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
+    config.addinivalue_line("markers", "slow: CPU test taking more than ~10 s")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import pyoracle
+
+    pyoracle.build()
+    return pyoracle
