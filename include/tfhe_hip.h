@@ -1,0 +1,167 @@
+/*
+ * tfhe_hip.h -- C-ABI of the MI355X-native batched CGGI/GINX bootstrapping engine.
+ *
+ * This is the drop-in boundary.  The reference (eric070021/TFHE-GPU) exposes its
+ * GPU path as seven C++ static members that OpenFHE's unchanged BinFHE code calls
+ * (SURVEY.md 8(b)).  Each of those maps onto one entry point here; the OpenFHE
+ * side binding a maintainer adds (a ~200-line shim translating NativeVector /
+ * NativePoly <-> flat u64) is in INTEGRATION.md.
+ *
+ *   reference symbol                                        entry point
+ *   GPUFFTBootstrap::GPUSetup       bootstrapping.cuh:111   tfhe_setup
+ *   GPUFFTBootstrap::GPUClean       bootstrapping.cuh:116   tfhe_clean
+ *   GPUFFTBootstrap::EvalAcc_CUDA   bootstrapping.cuh:126   tfhe_eval_acc
+ *   GPUFFTBootstrap::MKMSwitch_CUDA bootstrapping.cuh:135   tfhe_mkm_switch
+ *   GPULWEOperation::CiphertextMulMatrix_CUDA lwe-operation.cuh:49  tfhe_ciphertext_mul_matrix
+ *   GPULWEOperation::GPUSetup       lwe-operation.cuh:57    tfhe_lwe_gpu_setup
+ *   GPULWEOperation::GPUClean       lwe-operation.cuh:62    tfhe_lwe_gpu_clean
+ *
+ * Above those, the vector BinFHEContext surface (binfhecontext.cpp:316-347 ->
+ * binfhe-base-scheme.cpp:598-1085) is offered as fused entry points that keep
+ * every chained bootstrap on the device: tfhe_eval_bin_gate, tfhe_eval_func,
+ * tfhe_eval_floor, tfhe_eval_sign, tfhe_eval_decomp.
+ *
+ * Conventions
+ *  - All integers are u64, little-endian, flat row-major arrays in HOST memory
+ *    unless the name ends in _device (then device pointers on the context's
+ *    first device, ordered on the given hipStream_t, passed as void*).
+ *  - LWE ciphertext: [n+1] words, a[0..n-1] then b.
+ *  - RLWE accumulator: [2][N] words, coefficient form.
+ *  - BSK (coefficient form): [n][2][dG2][2][N]: LWE index i, ternary key
+ *    (0: s_i=+1, 1: s_i=-1; rgsw-acc-cggi.cpp:53-77), gadget row (poly + 2*digit,
+ *    rgsw-acc-cggi.cpp:229-238), RLWE poly, coefficient.  The reference keeps the
+ *    RingGSWACCKey in EVALUATION form for OpenFHE's own NTT; the shim converts
+ *    it with SetFormat(COEFFICIENT) exactly as the reference's KeyCopy_FFT does
+ *    (bootstrapping.cu:1112-1137).
+ *  - KSK: [N][baseKS][dKS][n+1], B stored at index n (the reference's device
+ *    layout, bootstrapping.cu:961-975).
+ *  - Errors: every call returns tfhe_status; tfhe_last_error() gives a message.
+ *    The reference exit()s on device faults (bootstrapping.cu:28-37); here the
+ *    caller decides (the shim converts to OPENFHE_THROW).
+ *  - Not re-entrant per context (like the reference's static state); separate
+ *    contexts are independent.
+ */
+#ifndef TFHE_HIP_H
+#define TFHE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFHE_HIP_ABI_VERSION 1
+
+typedef enum tfhe_status {
+    TFHE_OK = 0,
+    TFHE_ERR_INVALID_ARGUMENT = 1,
+    TFHE_ERR_UNSUPPORTED = 2,
+    TFHE_ERR_NOT_SET_UP = 3,
+    TFHE_ERR_DEVICE = 4,
+    TFHE_ERR_OUT_OF_MEMORY = 5,
+    TFHE_ERR_INTERNAL = 6
+} tfhe_status;
+
+/* BINFHE_PARAMSET (binfhe-constants.h:46-90) */
+typedef enum tfhe_paramset {
+    TFHE_TOY = 0, TFHE_MEDIUM, TFHE_STD128_AP, TFHE_STD128_APOPT, TFHE_STD128, TFHE_STD128_OPT, TFHE_STD192,
+    TFHE_STD192_OPT, TFHE_STD256, TFHE_STD256_OPT, TFHE_STD128Q, TFHE_STD128Q_OPT, TFHE_STD192Q,
+    TFHE_STD192Q_OPT, TFHE_STD256Q, TFHE_STD256Q_OPT, TFHE_SIGNED_MOD_TEST
+} tfhe_paramset;
+
+/* BINGATE (binfhe-constants.h:101) */
+typedef enum tfhe_gate {
+    TFHE_OR = 0, TFHE_AND, TFHE_NOR, TFHE_NAND, TFHE_XOR_FAST, TFHE_XNOR_FAST, TFHE_XOR, TFHE_XNOR
+} tfhe_gate;
+
+/* Flat parameter record (the reference's params_CUDA[10], bootstrapping.cu:917-929,
+ * plus the gadget base).  digitsG, dKS and dG2 are derived by tfhe_params_finish. */
+typedef struct tfhe_params {
+    uint32_t n;                /* LWE dimension */
+    uint32_t N;                /* ring dimension (power of two) */
+    uint64_t q;                /* LWE modulus */
+    uint64_t Q;                /* RLWE modulus, prime, Q = 1 mod 2N */
+    uint64_t qKS;              /* key-switching modulus */
+    uint32_t baseKS;           /* key-switching base */
+    uint32_t baseG;            /* gadget base, power of two */
+    uint32_t numDigitsToThrow; /* approximate gadget decomposition */
+    uint32_t digitsG;          /* ceil(log Q / log baseG)           (derived) */
+    uint32_t dKS;              /* ceil(log qKS / log baseKS)        (derived) */
+    uint32_t dG2;              /* 2*(digitsG - numDigitsToThrow)    (derived) */
+} tfhe_params;
+
+typedef struct tfhe_info {
+    int num_devices;           /* devices the context shards over */
+    int word_bits;             /* 32: Q fits the u32 Shoup path; 64 otherwise */
+    uint64_t bsk_device_bytes; /* per device */
+    uint64_t ksk_device_bytes; /* per device */
+    uint64_t bootstraps;       /* blind rotations executed since setup */
+    uint64_t key_image_bytes;  /* size of the exportable device key image */
+} tfhe_info;
+
+typedef struct tfhe_ctx tfhe_ctx;
+
+/* ---- parameters (binfhecontext.cpp:42-181) ---- */
+tfhe_status tfhe_params_from_set(int paramset, tfhe_params* out);
+tfhe_status tfhe_params_from_logq(int paramset, int arb_func, uint32_t logQ, int64_t N, uint32_t baseG,
+                                  uint32_t num_digits_to_throw, tfhe_params* out);
+tfhe_status tfhe_params_finish(tfhe_params* p);
+
+/* ---- reference boundary ---- */
+tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
+                       int num_gpus);
+tfhe_status tfhe_clean(tfhe_ctx* ctx);
+/* a[B][n] mod a_mod; acc[B][2][N] coefficient in/out; acc0 returned transposed
+ * (the callers rely on it: binfhe-base-scheme.cpp:665-671, 1203-1204). */
+tfhe_status tfhe_eval_acc(tfhe_ctx* ctx, size_t B, const uint64_t* a, uint64_t a_mod, uint64_t* acc);
+/* ct_ext[B][N+1] mod Q -> out[B][n+1] mod fmod: ModSwitch(qKS), KeySwitch, ModSwitch(fmod) */
+tfhe_status tfhe_mkm_switch(tfhe_ctx* ctx, size_t B, const uint64_t* ct_ext, uint64_t fmod, uint64_t* out);
+/* out[c] = sum_k matrix[k][c] * ct[k] mod modulus, c < cols: ct[K][n+1], matrix[K][cols], out[cols][n+1] */
+tfhe_status tfhe_ciphertext_mul_matrix(tfhe_ctx* ctx, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
+                                       uint64_t modulus, uint64_t* out);
+tfhe_status tfhe_lwe_gpu_setup(int num_gpus);
+tfhe_status tfhe_lwe_gpu_clean(void);
+
+/* ---- vector BinFHEContext surface, bootstraps chained on device ---- */
+tfhe_status tfhe_eval_bin_gate(tfhe_ctx* ctx, int gate, size_t B, const uint64_t* ct1, const uint64_t* ct2, uint64_t q,
+                               uint64_t* out);
+/* lut: [q] shared (per_ct_lut = 0) or [B][q] (per_ct_lut = 1); out mod q */
+tfhe_status tfhe_eval_func(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t q, const uint64_t* lut, int per_ct_lut,
+                           uint64_t* out);
+tfhe_status tfhe_eval_floor(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t mod, uint32_t roundbits,
+                            uint64_t* out);
+/* ct mod `mod`; out mod q (the LWE modulus) */
+tfhe_status tfhe_eval_sign(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t mod, uint64_t* out);
+/* out[B][max_digits][n+1]; moduli[max_digits]; *num_digits set */
+tfhe_status tfhe_eval_decomp(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t mod, uint32_t max_digits,
+                             uint64_t* out, uint64_t* moduli, uint32_t* num_digits);
+
+/* ---- device-resident variants (inputs/outputs already in HBM of device 0) ---- */
+tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* ctx, int gate, size_t B, const uint64_t* d_ct1,
+                                      const uint64_t* d_ct2, uint64_t q, uint64_t* d_out, void* stream);
+tfhe_status tfhe_eval_acc_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_a, uint64_t a_mod, uint64_t* d_acc,
+                                 void* stream);
+tfhe_status tfhe_mkm_switch_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct_ext, uint64_t fmod, uint64_t* d_out,
+                                   void* stream);
+
+/* ---- key replication for one-process-per-GPU deployments ----
+ * The packed device key image (NTT-domain BSK with Shoup companions, packed
+ * KSK, tables) can be copied device-to-device (e.g. broadcast over RCCL/xGMI by
+ * torch.distributed) and adopted by another process without host conversion. */
+tfhe_status tfhe_export_key_image(tfhe_ctx* ctx, void* d_dst, size_t bytes, void* stream);
+tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, const void* d_src, size_t bytes,
+                                      int device);
+
+/* ---- introspection ---- */
+tfhe_status tfhe_get_info(tfhe_ctx* ctx, tfhe_info* out);
+const char* tfhe_status_string(tfhe_status s);
+const char* tfhe_last_error(void);
+int tfhe_abi_version(void);
+/* host-only self test of the NTT tables and packing (no GPU needed); 0 = pass */
+tfhe_status tfhe_host_selftest(const tfhe_params* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFHE_HIP_H */

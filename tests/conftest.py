@@ -4,7 +4,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for sub in ("oracle", "tfhe-gpu_amd"):
+for sub in ("oracle", "tfhe-gpu_amd", "tests"):
     path = os.path.join(ROOT, sub)
     if path not in sys.path:
         sys.path.insert(0, path)

@@ -1,0 +1,67 @@
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol
+include/tfhe_hip.h declares, its parameter selection agrees with the oracle and
+the reference table, and its host-side number theory self-tests pass.
+No compute call touches a GPU here."""
+import ctypes
+
+import pytest
+
+
+@pytest.fixture(scope="module")
+def capi():
+    import tfhe_amd
+
+    tfhe_amd.build()
+    return tfhe_amd
+
+
+def test_library_exports_every_header_symbol(capi):
+    lib = capi.lib()
+    syms = capi.exported_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert lib.tfhe_abi_version() == 1
+
+
+@pytest.mark.parametrize("name", ["TOY", "MEDIUM", "STD128", "STD128_OPT", "STD192", "STD192_OPT", "STD256",
+                                  "STD128Q", "STD128Q_OPT", "STD192Q", "STD256Q", "SIGNED_MOD_TEST"])
+def test_params_agree_with_oracle(capi, oracle, name):
+    a = capi.params_from_set(name).as_dict()
+    b = oracle.params_from_set(name).as_dict()
+    for k in a:
+        assert a[k] == b[k], (name, k)
+
+
+@pytest.mark.parametrize("arb,logq,thr", [(True, 12, 1), (True, 12, 0), (False, 23, 1), (False, 11, 0),
+                                          (True, 29, 0), (False, 17, 0)])
+def test_logq_params_agree_with_oracle(capi, oracle, arb, logq, thr):
+    a = capi.params_from_logq("STD128", arb, logq, 0, 0, thr).as_dict()
+    b = oracle.params_from_logq("STD128", arb, logq, 0, 0, thr).as_dict()
+    for k in a:
+        assert a[k] == b[k], (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("name", ["TOY", "STD128", "STD192", "STD128Q", "STD256Q"])
+def test_host_selftest(capi, name):
+    capi.host_selftest(capi.params_from_set(name))
+
+
+def test_host_selftest_large_q(capi):
+    capi.host_selftest(capi.params_from_logq("STD128", True, 12, 0, 0, 1))
+    capi.host_selftest(capi.params_from_logq("STD128", False, 23, 0, 0, 1))
+
+
+def test_errors_without_setup(capi):
+    import numpy as np
+
+    lib = capi.lib()
+    a = np.zeros(4, dtype=np.uint64)
+    st = lib.tfhe_eval_acc(None, 1, a, 1024, a)
+    assert st == 3  # TFHE_ERR_NOT_SET_UP
+    assert b"not set up" in lib.tfhe_last_error()
+    assert lib.tfhe_status_string(2) == b"unsupported"
+    bad = capi.params_from_set("STD128")
+    bad.Q = 1000  # not prime / not 1 mod 2N
+    assert lib.tfhe_params_finish(ctypes.byref(bad)) == 1
+    assert lib.tfhe_host_selftest(ctypes.byref(bad)) == 1

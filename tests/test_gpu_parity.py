@@ -1,0 +1,185 @@
+"""GPU parity: the HIP engine, called through the C-ABI, must equal the CPU
+oracle bit for bit on the same inputs, and reproduce the reference's own KAT
+digests (tests/golden/kat_openfhe.json)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import cube_lut, kat_inputs, random_cts
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kat_openfhe.json")
+
+
+@pytest.fixture(scope="module")
+def capi():
+    import tfhe_amd
+
+    return tfhe_amd
+
+
+def make_pair(capi, oracle, op, cp, bsk, ksk):
+    ctx = capi.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    return ctx, orc
+
+
+# ---------------------------------------------------------------- KATs
+@pytest.mark.parametrize("name", ["std128", "std192", "arb12"])
+def test_gpu_reproduces_reference_kat(capi, oracle, name):
+    gold = json.load(open(GOLDEN))["configs"][name]
+    p, bsk, ksk, trials = kat_inputs(oracle, name)
+    cp = capi.params_from_set("STD128") if name == "std128" else (
+        capi.params_from_set("STD192") if name == "std192" else capi.params_from_logq("STD128", True, 12, 0, 0, 1))
+    ctx = capi.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    c1 = np.stack([t[0] for t in trials])
+    c2 = np.stack([t[1] for t in trials])
+    out = ctx.EvalFunc(c1, cube_lut(cp.q)) if name == "arb12" else ctx.EvalBinGate("NAND", c1, c2)
+    for r, g in zip(out, gold["trials"]):
+        assert [int(x) for x in r[:4]] == g["a0_3"]
+        assert int(r[-1]) == g["b"]
+        assert f"{oracle.fnv1a64(r):016x}" == g["fnv"]
+    ctx.GPUClean()
+
+
+# ---------------------------------------------------------------- boundary calls
+@pytest.fixture(scope="module")
+def std128(capi, oracle):
+    op = oracle.params_from_set("STD128")
+    rng = oracle.Rng(7)
+    sk, bsk, ksk = oracle.keygen(op, rng)
+    cp = capi.params_from_set("STD128")
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng)
+    ctx.GPUClean()
+    orc.close()
+
+
+def test_eval_acc_parity(std128):
+    op, ctx, orc = std128["op"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(1)
+    B = 5
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    acc[0, 0, :] = 0  # a sparse test-vector-like accumulator too
+    for amod in (op.q, op.q // 2, 2 * op.N):
+        g = ctx.EvalAcc(a % amod, amod, acc)
+        c = orc.eval_acc(a % amod, amod, acc)
+        assert np.array_equal(g, c), amod
+
+
+def test_mkm_parity(std128):
+    op, ctx, orc = std128["op"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(2)
+    ext = rs.integers(0, op.Q, (33, op.N + 1), dtype=np.uint64)
+    ext[0, :] = 0
+    ext[1, :] = op.Q - 1
+    for fmod in (op.q, 2 * op.q, 1 << 20):
+        assert np.array_equal(ctx.MKMSwitch(ext, fmod), orc.mkm_switch(ext, fmod))
+
+
+# ---------------------------------------------------------------- vector surface
+GATES = ["OR", "AND", "NOR", "NAND", "XOR_FAST", "XNOR_FAST", "XOR", "XNOR"]
+TRUTH = {"AND": lambda x, y: x & y, "OR": lambda x, y: x | y, "NAND": lambda x, y: 1 - (x & y),
+         "NOR": lambda x, y: 1 - (x | y), "XOR": lambda x, y: x ^ y, "XNOR": lambda x, y: 1 - (x ^ y),
+         "XOR_FAST": lambda x, y: x ^ y, "XNOR_FAST": lambda x, y: 1 - (x ^ y)}
+
+
+@pytest.mark.parametrize("gate", GATES)
+def test_gate_parity_and_decrypt(std128, oracle, gate):
+    op, ctx, orc, sk, rng = std128["op"], std128["ctx"], std128["orc"], std128["sk"], std128["rng"]
+    m1 = np.array([0, 0, 1, 1, 1, 0, 1])
+    m2 = np.array([0, 1, 0, 1, 1, 1, 0])
+    c1 = np.stack([oracle.encrypt(op, rng, sk, int(m), 4, op.q) for m in m1])
+    c2 = np.stack([oracle.encrypt(op, rng, sk, int(m), 4, op.q) for m in m2])
+    g = ctx.EvalBinGate(gate, c1, c2)
+    assert np.array_equal(g, orc.eval_bin_gate(gate, c1, c2))
+    got = [oracle.decrypt(op, sk, r, 4, op.q) for r in g]
+    assert got == [TRUTH[gate](int(x), int(y)) for x, y in zip(m1, m2)]
+
+
+def test_gate_random_inputs_parity(std128):
+    op, ctx, orc = std128["op"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(3)
+    c1 = random_cts(rs, 9, op.n, op.q)
+    c2 = random_cts(rs, 9, op.n, op.q)
+    assert np.array_equal(ctx.EvalBinGate("AND", c1, c2), orc.eval_bin_gate("AND", c1, c2))
+
+
+def test_gate_errors(std128, capi):
+    ctx, op = std128["ctx"], std128["op"]
+    c = np.zeros((0, op.n + 1), dtype=np.uint64)
+    with pytest.raises(capi.TfheError):
+        ctx.EvalBinGate("AND", c, c.copy())
+
+
+def test_eval_func_parity_all_lut_kinds(std128, oracle):
+    """negacyclic (1 bootstrap), periodic and arbitrary (2 bootstraps) LUTs,
+    binfhe-base-scheme.cpp:679-789; arbitrary needs q <= N, so q = 512 here."""
+    op, ctx, orc, sk, rng = std128["op"], std128["ctx"], std128["orc"], std128["sk"], std128["rng"]
+    q = 512
+    P = 4
+    iv = q // P
+    arb = np.array([((i // iv) ** 2 % P) * iv for i in range(q)], dtype=np.uint64)
+    half = [(i // iv) * iv + iv // 2 for i in range(q // 2)]
+    neg = np.array(half + [q - v for v in half], dtype=np.uint64)
+    per = np.array([((i // iv) % 2) * iv for i in range(q)], dtype=np.uint64)
+    ms = [0, 1, 2, 3, 1, 2]
+    ct = np.stack([oracle.encrypt(op, rng, sk, m, P, q) for m in ms])
+    for lut in (arb, neg, per):
+        g = ctx.EvalFunc(ct, lut, q=q)
+        assert np.array_equal(g, orc.eval_func(ct, lut, q=q))
+    luts = np.stack([arb if i % 2 else arb[::-1].copy() for i in range(len(ms))])
+    assert np.array_equal(ctx.EvalFunc(ct, luts, q=q), orc.eval_func(ct, luts, q=q))
+
+
+# ---------------------------------------------------------------- large precision
+@pytest.fixture(scope="module")
+def sign23(capi, oracle):
+    """STD128 logQ=23 throw=1 (time-estimate.cpp:162-163): Q = 2^54 - 77823, 64-bit path."""
+    op = oracle.params_from_logq("STD128", False, 23, 0, 0, 1)
+    rng = oracle.Rng(9)
+    sk, bsk, ksk = oracle.keygen(op, rng)
+    cp = capi.params_from_logq("STD128", False, 23, 0, 0, 1)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng)
+    ctx.GPUClean()
+    orc.close()
+
+
+def test_floor_sign_decomp_parity(sign23, oracle):
+    op, ctx, orc, sk, rng = sign23["op"], sign23["ctx"], sign23["orc"], sign23["sk"], sign23["rng"]
+    Qin = 1 << 17
+    p = (op.q // 128 // 2) * (Qin // op.q)
+    ms = [0, p // 2 - 8, p // 2 + 8, p - 1]
+    ct = np.stack([oracle.encrypt(op, rng, sk, m, p, Qin) for m in ms])
+    fl = ctx.EvalFloor(ct, Qin)
+    assert np.array_equal(fl, orc.eval_floor(ct, Qin))
+    sg = ctx.EvalSign(ct, Qin)
+    assert np.array_equal(sg, orc.eval_sign(ct, Qin))
+    assert [oracle.decrypt(op, sk, r, 2, op.q) for r in sg] == [int(m >= p // 2) for m in ms]
+    d_g, mods_g = ctx.EvalDecomp(ct, Qin)
+    d_c, mods_c = orc.eval_decomp(ct, Qin)
+    assert mods_g == mods_c
+    assert np.array_equal(d_g, d_c)
+
+
+# ---------------------------------------------------------------- full size property
+def test_full_batch_nand_decrypts(std128, oracle):
+    """BASELINE config C2 shape (STD128, B=8192): every output decrypts to NAND,
+    and a sample equals the oracle bit for bit."""
+    op, ctx, orc, sk = std128["op"], std128["ctx"], std128["orc"], std128["sk"]
+    rs = np.random.default_rng(4)
+    B = 8192
+    m1 = rs.integers(0, 2, B)
+    m2 = rs.integers(0, 2, B)
+    rng = oracle.Rng(123)
+    c1 = np.stack([oracle.encrypt(op, rng, sk, int(m), 4, op.q) for m in m1])
+    c2 = np.stack([oracle.encrypt(op, rng, sk, int(m), 4, op.q) for m in m2])
+    out = ctx.EvalBinGate("NAND", c1, c2)
+    dec = np.array([oracle.decrypt(op, sk, r, 4, op.q) for r in out])
+    assert np.array_equal(dec, 1 - (m1 & m2))
+    idx = [0, 1, 4095, 8191]
+    assert np.array_equal(out[idx], orc.eval_bin_gate("NAND", c1[idx], c2[idx]))

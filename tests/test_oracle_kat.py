@@ -10,37 +10,9 @@ import os
 
 import numpy as np
 import pytest
+from helpers import cube_lut, kat_inputs
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "kat_openfhe.json")
-
-
-def kat_inputs(po, name):
-    if name == "std128":
-        p = po.params_from_set("STD128")
-    elif name == "std192":
-        p = po.params_from_set("STD192")
-    else:
-        p = po.params_from_logq("STD128", True, 12, 0, 0, 1)
-    rng = po.Rng(1)
-    bsk, ksk = po.kat_keys(p, rng)
-    trials = []
-    for _ in range(3):
-        a1 = po.splitmix(rng, p.n, p.q)
-        b1 = po.splitmix(rng, 1, p.q)
-        a2 = po.splitmix(rng, p.n, p.q)
-        b2 = po.splitmix(rng, 1, p.q)
-        trials.append((np.concatenate([a1, b1]), np.concatenate([a2, b2])))
-    return p, bsk, ksk, trials
-
-
-def cube_lut(q, P=8):
-    """GenerateLUTviaFunction(m^3 mod p, p) (binfhecontext.cpp:280-301, time-estimate.cpp:70-75)."""
-    interval = q // P
-
-    def f(m, p1):
-        return (m * m * m) % p1 if m < p1 else ((m - p1 // 2) ** 3) % p1
-
-    return np.array([f(i // interval, P) * interval for i in range(q)], dtype=np.uint64)
 
 
 @pytest.mark.parametrize("name", ["std128", "std192", "arb12"])

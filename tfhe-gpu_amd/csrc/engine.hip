@@ -1,0 +1,944 @@
+// engine.hip -- tfhe_ctx: key ingest (GPUSetup), device pipelines for every batch
+// operation, multi-GPU sharding, and the extern "C" entry points of tfhe_hip.h.
+//
+// Design (MI355X-first):
+//  * keys live in one per-device "key arena" (tables + NTT-domain BSK with Shoup
+//    companions + packed KSK) so a whole key image is one device-to-device copy
+//    (peer copy over xGMI in-process, RCCL broadcast across processes);
+//  * every bootstrap of a fused op (gate, EvalFunc, EvalFloor, EvalSign,
+//    EvalDecomp) stays in HBM: test vector -> blind rotation -> extraction ->
+//    MKM -> LWE glue, one stream per device, host sees only LWE ciphertexts;
+//  * a batch is split into contiguous shards, one host thread + stream per
+//    device (the reference interleaves SM_count-sized chunks, bootstrapping.cu:1617).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host_math.hpp"
+#include "kernels.hpp"
+#include "tfhe_hip.h"
+
+using namespace tfhe;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+tfhe_status fail(tfhe_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define HCHECK(expr)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return fail(e_ == hipErrorOutOfMemory ? TFHE_ERR_OUT_OF_MEMORY : TFHE_ERR_DEVICE,          \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                            \
+    } while (0)
+
+#define SCHECK(expr)                        \
+    do {                                    \
+        tfhe_status s_ = (expr);            \
+        if (s_ != TFHE_OK) return s_;       \
+    } while (0)
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+int ksk_bits_for(uint64_t qKS) {
+    if (qKS <= (1ull << 16)) return 16;
+    if (qKS <= (1ull << 32)) return 32;
+    return 64;
+}
+
+// Byte offsets of everything inside the key arena; a pure function of the params,
+// so an importing process can locate the sections of a broadcast image.
+struct ArenaLayout {
+    size_t psi, psi_sh, ipsi, ipsi_sh, mono, mono_sh, eidx, bsk, bsk_sh, ksk, total;
+    size_t bsk_words, ksk_words;
+};
+
+ArenaLayout arena_layout(const tfhe_params& p, int word_bits) {
+    ArenaLayout L{};
+    const size_t wb = word_bits / 8, N = p.N;
+    const size_t kb = ksk_bits_for(p.qKS) / 8;
+    L.bsk_words = (size_t)p.n * 2 * p.dG2 * 2 * N;
+    L.ksk_words = (size_t)N * p.baseKS * p.dKS * (p.n + 1);
+    size_t o = 0;
+    L.psi = o; o = align_up(o + N * wb);
+    L.psi_sh = o; o = align_up(o + N * wb);
+    L.ipsi = o; o = align_up(o + N * wb);
+    L.ipsi_sh = o; o = align_up(o + N * wb);
+    L.mono = o; o = align_up(o + 2 * N * wb);
+    L.mono_sh = o; o = align_up(o + 2 * N * wb);
+    L.eidx = o; o = align_up(o + N * 4);
+    L.bsk = o; o = align_up(o + L.bsk_words * wb);
+    L.bsk_sh = o; o = align_up(o + L.bsk_words * wb);
+    L.ksk = o; o = align_up(o + L.ksk_words * kb);
+    L.total = o;
+    return L;
+}
+
+struct Scratch {
+    uint64_t* acc = nullptr;  // [cap][2][N]
+    uint64_t* a = nullptr;    // [cap][n]
+    uint64_t* ext = nullptr;  // [cap][N+1]
+    uint64_t* lwe[6] = {};    // [cap][n+1] each
+    size_t cap = 0;
+};
+
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    unsigned char* arena = nullptr;
+    void* bsk_fast = nullptr;
+    Scratch sc;
+    DevTables tables{};
+};
+
+}  // namespace
+
+struct tfhe_ctx {
+    tfhe_params p{};
+    int word_bits = 64;
+    int ksk_bits = 64;
+    bool use_fast = false;
+    BRParams br{};
+    KSParams ks{};
+    ArenaLayout layout{};
+    std::vector<Device> devs;
+    std::atomic<uint64_t> bootstraps{0};
+    size_t max_chunk = 65536;  // the reference's max_bootstapping_num, bootstrapping.cuh:140
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// setup helpers
+// ---------------------------------------------------------------------------
+tfhe_status init_derived(tfhe_ctx* c) {
+    const tfhe_params& p = c->p;
+    c->word_bits = word_bits_for(p);
+    c->ksk_bits = ksk_bits_for(p.qKS);
+    c->layout = arena_layout(p, c->word_bits);
+    c->br.N = p.N;
+    c->br.logN = ilog2(p.N);
+    c->br.n = p.n;
+    c->br.dG2 = p.dG2;
+    c->br.digits = p.digitsG - p.numDigitsToThrow;
+    c->br.thr = p.numDigitsToThrow;
+    c->br.logG = ilog2(p.baseG);
+    c->br.Q = p.Q;
+    c->br.r1 = c->word_bits == 32 ? (uint64_t)((((u128)1) << 32) / p.Q) : (uint64_t)((((u128)1) << 64) / p.Q);
+    c->ks.N = p.N;
+    c->ks.n = p.n;
+    c->ks.baseKS = p.baseKS;
+    c->ks.dKS = p.dKS;
+    c->ks.Q = p.Q;
+    c->ks.qKS = p.qKS;
+    c->use_fast = fast_path_supported(c->br, c->word_bits);
+    if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
+        return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
+    if (p.baseKS > 256) return fail(TFHE_ERR_UNSUPPORTED, "baseKS > 256 not supported");
+    return TFHE_OK;
+}
+
+template <typename W>
+void fill_words(std::vector<unsigned char>& host, size_t off, const uint64_t* src, size_t count) {
+    W* dst = reinterpret_cast<W*>(host.data() + off);
+    const size_t blk = 1 << 16;
+    parallel_for((count + blk - 1) / blk, [&](size_t b) {
+        for (size_t i = b * blk; i < std::min(count, (b + 1) * blk); ++i) dst[i] = (W)src[i];
+    });
+}
+
+template <typename W>
+void fill_companions(std::vector<unsigned char>& host, size_t off, const uint64_t* src, size_t count, uint64_t Q) {
+    W* dst = reinterpret_cast<W*>(host.data() + off);
+    const int bits = sizeof(W) * 8;
+    const size_t blk = 1 << 14;
+    parallel_for((count + blk - 1) / blk, [&](size_t b) {
+        for (size_t i = b * blk; i < std::min(count, (b + 1) * blk); ++i) dst[i] = (W)shoup_companion(src[i], Q, bits);
+    });
+}
+
+// Build the whole key image on the host (one-time, GPUSetup_core's job in the
+// reference, bootstrapping.cu:874-1083).
+tfhe_status build_host_image(tfhe_ctx* c, const uint64_t* bsk_coeff, const uint64_t* ksk,
+                             std::vector<unsigned char>& img) {
+    const tfhe_params& p = c->p;
+    const ArenaLayout& L = c->layout;
+    img.assign(L.total, 0);
+    NttTables t = make_ntt_tables(p.Q, p.N);
+    std::vector<uint64_t> bsk_ntt(L.bsk_words);
+    bsk_to_ntt_scaled(p, t, bsk_coeff, bsk_ntt.data());
+    auto put = [&](auto tag, size_t off, size_t off_sh, const uint64_t* v, size_t count) {
+        using W = decltype(tag);
+        fill_words<W>(img, off, v, count);
+        if (off_sh != (size_t)-1) fill_companions<W>(img, off_sh, v, count, p.Q);
+    };
+    if (c->word_bits == 32) {
+        put(uint32_t{}, L.psi, L.psi_sh, t.psi_br.data(), p.N);
+        put(uint32_t{}, L.ipsi, L.ipsi_sh, t.ipsi_br.data(), p.N);
+        put(uint32_t{}, L.mono, L.mono_sh, t.mono.data(), 2ull * p.N);
+        put(uint32_t{}, L.bsk, L.bsk_sh, bsk_ntt.data(), L.bsk_words);
+    } else {
+        put(uint64_t{}, L.psi, L.psi_sh, t.psi_br.data(), p.N);
+        put(uint64_t{}, L.ipsi, L.ipsi_sh, t.ipsi_br.data(), p.N);
+        put(uint64_t{}, L.mono, L.mono_sh, t.mono.data(), 2ull * p.N);
+        put(uint64_t{}, L.bsk, L.bsk_sh, bsk_ntt.data(), L.bsk_words);
+    }
+    std::memcpy(img.data() + L.eidx, t.eidx.data(), sizeof(uint32_t) * p.N);
+    // KSK: packed to the narrowest word holding qKS (reference keeps u64, bootstrapping.cu:963)
+    const uint64_t qks = p.qKS;
+    std::atomic<bool> bad{false};
+    const size_t blk = 1 << 16;
+    parallel_for((L.ksk_words + blk - 1) / blk, [&](size_t b) {
+        for (size_t i = b * blk; i < std::min(L.ksk_words, (b + 1) * blk); ++i)
+            if (ksk[i] >= qks) bad = true;
+    });
+    if (bad) return fail(TFHE_ERR_INVALID_ARGUMENT, "KSK entry >= qKS");
+    if (c->ksk_bits == 16) fill_words<uint16_t>(img, L.ksk, ksk, L.ksk_words);
+    else if (c->ksk_bits == 32) fill_words<uint32_t>(img, L.ksk, ksk, L.ksk_words);
+    else fill_words<uint64_t>(img, L.ksk, ksk, L.ksk_words);
+    return TFHE_OK;
+}
+
+void bind_tables(tfhe_ctx* c, Device& d) {
+    const ArenaLayout& L = c->layout;
+    d.tables.psi = d.arena + L.psi;
+    d.tables.psi_sh = d.arena + L.psi_sh;
+    d.tables.ipsi = d.arena + L.ipsi;
+    d.tables.ipsi_sh = d.arena + L.ipsi_sh;
+    d.tables.mono = d.arena + L.mono;
+    d.tables.mono_sh = d.arena + L.mono_sh;
+    d.tables.eidx = reinterpret_cast<const uint32_t*>(d.arena + L.eidx);
+}
+
+tfhe_status finish_device(tfhe_ctx* c, Device& d) {
+    bind_tables(c, d);
+    if (c->use_fast) {
+        HCHECK(hipMalloc(&d.bsk_fast, bsk_fast_bytes(c->br)));
+        HCHECK(launch_pack_bsk_fast(c->br, d.arena + c->layout.bsk, d.arena + c->layout.bsk_sh, d.bsk_fast,
+                                    d.stream));
+        HCHECK(hipStreamSynchronize(d.stream));
+    }
+    return TFHE_OK;
+}
+
+void free_device(Device& d) {
+    if (d.id < 0) return;
+    hipSetDevice(d.id);
+    if (d.stream) hipStreamSynchronize(d.stream);
+    hipFree(d.arena);
+    hipFree(d.bsk_fast);
+    hipFree(d.sc.acc);
+    hipFree(d.sc.a);
+    hipFree(d.sc.ext);
+    for (auto* p : d.sc.lwe) hipFree(p);
+    if (d.stream) hipStreamDestroy(d.stream);
+    d = Device{};
+    d.id = -1;
+}
+
+tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
+    if (B <= d.sc.cap) return TFHE_OK;
+    const tfhe_params& p = c->p;
+    const size_t cap = std::max(B, std::min(c->max_chunk, (size_t)1024));
+    hipFree(d.sc.acc);
+    hipFree(d.sc.a);
+    hipFree(d.sc.ext);
+    for (auto*& q : d.sc.lwe) hipFree(q), q = nullptr;
+    d.sc = Scratch{};
+    HCHECK(hipMalloc(&d.sc.acc, cap * 2 * p.N * sizeof(uint64_t)));
+    HCHECK(hipMalloc(&d.sc.a, cap * p.n * sizeof(uint64_t)));
+    HCHECK(hipMalloc(&d.sc.ext, cap * (p.N + 1) * sizeof(uint64_t)));
+    for (auto*& q : d.sc.lwe) HCHECK(hipMalloc(&q, cap * (p.n + 1) * sizeof(uint64_t)));
+    d.sc.cap = cap;
+    return TFHE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device pipelines (one device, one stream, B <= scratch capacity)
+// ---------------------------------------------------------------------------
+tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B) {
+    if (amod == 0 || (2ull * c->p.N) % amod != 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "a-modulus must divide 2N");
+    const ArenaLayout& L = c->layout;
+    if (c->use_fast) {
+        HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
+    } else {
+        HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
+                                           amod, acc, B, d.stream));
+    }
+    c->bootstraps += B;
+    return TFHE_OK;
+}
+
+tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
+    if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
+    HCHECK(launch_mkm(c->ks, c->ksk_bits, d.arena + c->layout.ksk, ext, fmod, out, B, d.stream));
+    return TFHE_OK;
+}
+
+// BootstrapFunc / BootstrapGate on device: ct[B][n+1] mod tv.ctmod -> out mod fmod
+tfhe_status dev_bootstrap(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
+                          size_t B) {
+    tv.N = c->p.N;
+    tv.n = c->p.n;
+    tv.Q = c->p.Q;
+    tv.Q8 = c->p.Q / 8 + 1;
+    if ((2ull * c->p.N) % tv.ctmod != 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "ciphertext modulus must divide 2N");
+    HCHECK(launch_build_testvector(tv, ct, d.sc.acc, d.sc.a, B, d.stream));
+    SCHECK(dev_blind_rotate(c, d, d.sc.a, tv.ctmod, d.sc.acc, B));
+    HCHECK(launch_extract(c->p.N, c->p.Q, b_add, d.sc.acc, d.sc.ext, B, d.stream));
+    return dev_mkm(c, d, d.sc.ext, tv.fmod, out, B);
+}
+
+uint64_t gate_const(int gate, uint64_t q) {  // rgsw-cryptoparameters.h:130-137
+    static const uint64_t k[] = {5, 7, 1, 3, 5, 1};
+    return k[gate] * (q >> 3);
+}
+
+// vector EvalBinGate, binfhe-base-scheme.cpp:598-677.  Uses lwe[0..2] + lwe[5].
+tfhe_status dev_gate(tfhe_ctx* c, Device& d, int gate, const uint64_t* ct1, const uint64_t* ct2, uint64_t q,
+                     uint64_t* out, size_t B) {
+    const uint32_t n = c->p.n;
+    hipStream_t s = d.stream;
+    if (gate == TFHE_XOR || gate == TFHE_XNOR) {
+        uint64_t *n1 = d.sc.lwe[3], *n2 = d.sc.lwe[4], *t1 = d.sc.lwe[5];
+        HCHECK(launch_lwe_op(LWE_NOT, n, q, 0, ct1, nullptr, n1, B, s));
+        HCHECK(launch_lwe_op(LWE_NOT, n, q, 0, ct2, nullptr, n2, B, s));
+        SCHECK(dev_gate(c, d, TFHE_AND, ct1, n2, q, t1, B));   // AND(ct1, NOT ct2)
+        SCHECK(dev_gate(c, d, TFHE_AND, n1, ct2, q, n2, B));   // AND(NOT ct1, ct2)
+        SCHECK(dev_gate(c, d, TFHE_OR, t1, n2, q, out, B));
+        if (gate == TFHE_XNOR) HCHECK(launch_lwe_op(LWE_NOT, n, q, 0, out, nullptr, out, B, s));
+        return TFHE_OK;
+    }
+    uint64_t* prep = d.sc.lwe[0];
+    HCHECK(launch_lwe_op((gate == TFHE_XOR_FAST || gate == TFHE_XNOR_FAST) ? LWE_DOUBLE_SUB : LWE_ADD, n, q, 0, ct1,
+                         ct2, prep, B, s));
+    TvParams tv{};
+    tv.mode = TV_GATE;
+    tv.ctmod = q;
+    tv.fmod = q;
+    tv.q1 = gate_const(gate, q);
+    tv.q2 = addmod(tv.q1, q >> 1, q);
+    return dev_bootstrap(c, d, tv, c->p.Q / 8 + 1, prep, out, B);
+}
+
+// binfhe-base-scheme.cpp:162-186
+int check_input_function(const uint64_t* lut, uint64_t len, uint64_t mod) {
+    const uint64_t h = len / 2;
+    if (lut[0] == mod - lut[h]) {
+        for (uint64_t i = 1; i < h; ++i)
+            if (lut[i] != mod - lut[h + i]) return 2;
+        return 0;
+    }
+    if (lut[0] == lut[h]) {
+        for (uint64_t i = 1; i < h; ++i)
+            if (lut[i] != lut[h + i]) return 2;
+        return 1;
+    }
+    return 2;
+}
+
+// vector EvalFunc, binfhe-base-scheme.cpp:679-924.  d_lut is a device LUT ([q] or [B][q]).
+tfhe_status dev_func(tfhe_ctx* c, Device& d, int prop, const uint64_t* ct, uint64_t q, const uint64_t* d_lut,
+                     uint64_t lut_stride, uint64_t* out, size_t B) {
+    const uint32_t n = c->p.n;
+    const uint64_t beta = 128;
+    hipStream_t s = d.stream;
+    uint64_t *ct1 = d.sc.lwe[0], *ct2 = d.sc.lwe[1], *ct3 = d.sc.lwe[2];
+    TvParams tv{};
+    tv.lut = d_lut;
+    tv.lut_stride = lut_stride;
+    tv.lut_len = q;
+    if (prop == 0) {  // negacyclic: one bootstrap
+        HCHECK(launch_lwe_op(LWE_ADD_CONST, n, q, beta, ct, nullptr, ct1, B, s));
+        tv.mode = TV_LUT;
+        tv.ctmod = q;
+        tv.fmod = q;
+        return dev_bootstrap(c, d, tv, 0, ct1, out, B);
+    }
+    if (prop == 2) {  // arbitrary: raise to 2q, two bootstraps
+        if (q > c->p.N) return fail(TFHE_ERR_UNSUPPORTED, "arbitrary function needs q <= N");
+        const uint64_t dq = q << 1;
+        HCHECK(launch_lwe_op(LWE_ADD_CONST, n, dq, beta, ct, nullptr, ct2, B, s));
+        tv.mode = TV_HALF;
+        tv.ctmod = dq;
+        tv.fmod = dq;
+        SCHECK(dev_bootstrap(c, d, tv, 0, ct2, ct3, B));
+        HCHECK(launch_lwe_op(LWE_SUB, n, dq, 0, ct, ct3, ct3, B, s));  // EvalSubEq2(ct1, ct3)
+        HCHECK(launch_lwe_op(LWE_ADD_CONST, n, dq, beta, ct3, nullptr, ct3, B, s));
+        HCHECK(launch_lwe_op(LWE_SUB_CONST, n, dq, q >> 1, ct3, nullptr, ct3, B, s));
+        tv.mode = TV_LUT2;
+        SCHECK(dev_bootstrap(c, d, tv, 0, ct3, out, B));
+        HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, out, nullptr, out, B, s));
+        return TFHE_OK;
+    }
+    // periodic
+    HCHECK(launch_lwe_op(LWE_ADD_CONST, n, q, beta, ct, nullptr, ct1, B, s));
+    tv.mode = TV_HALF;
+    tv.ctmod = q;
+    tv.fmod = q;
+    SCHECK(dev_bootstrap(c, d, tv, 0, ct1, ct2, B));
+    HCHECK(launch_lwe_op(LWE_SUB, n, q, 0, ct, ct2, ct2, B, s));  // EvalSubEq2(ct, ct2)
+    HCHECK(launch_lwe_op(LWE_ADD_CONST, n, q, beta, ct2, nullptr, ct2, B, s));
+    HCHECK(launch_lwe_op(LWE_SUB_CONST, n, q, q >> 2, ct2, nullptr, ct2, B, s));
+    tv.mode = TV_LUT1;
+    return dev_bootstrap(c, d, tv, 0, ct2, out, B);
+}
+
+// vector EvalFloor, binfhe-base-scheme.cpp:926-987.  out may alias nothing; uses lwe[3], lwe[4].
+tfhe_status dev_floor(tfhe_ctx* c, Device& d, const uint64_t* ct, uint64_t mod, uint32_t roundbits, uint64_t* out,
+                      size_t B) {
+    const uint32_t n = c->p.n;
+    const uint64_t beta = 128;
+    const uint64_t q = roundbits == 0 ? c->p.q : beta * 2 * (1ull << roundbits);
+    hipStream_t s = d.stream;
+    uint64_t *ctq = d.sc.lwe[3], *t = d.sc.lwe[4];
+    HCHECK(launch_lwe_op(LWE_ADD_CONST, n, mod, beta, ct, nullptr, out, B, s));  // ct1
+    HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, out, nullptr, ctq, B, s));
+    TvParams tv{};
+    tv.mode = TV_HALF;
+    tv.ctmod = q;
+    tv.fmod = mod;
+    SCHECK(dev_bootstrap(c, d, tv, 0, ctq, t, B));
+    HCHECK(launch_lwe_op(LWE_SUB, n, mod, 0, out, t, out, B, s));
+    HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, out, nullptr, ctq, B, s));
+    tv.mode = TV_FLOOR2;
+    SCHECK(dev_bootstrap(c, d, tv, 0, ctq, t, B));
+    HCHECK(launch_lwe_op(LWE_SUB, n, mod, 0, out, t, out, B, s));
+    return TFHE_OK;
+}
+
+// vector EvalSign, binfhe-base-scheme.cpp:989-1037 (in: lwe[1] holds the input copy)
+tfhe_status dev_sign(tfhe_ctx* c, Device& d, const uint64_t* ct, uint64_t mod, uint64_t* out, size_t B) {
+    const uint32_t n = c->p.n;
+    const uint64_t beta = 128, q = c->p.q;
+    hipStream_t s = d.stream;
+    uint64_t *tmp = d.sc.lwe[1], *fl = d.sc.lwe[2];
+    HCHECK(hipMemcpyAsync(tmp, ct, B * (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    while (mod > q) {
+        SCHECK(dev_floor(c, d, tmp, mod, 0, fl, B));
+        const uint64_t nm = mod / q * 2 * beta;
+        HCHECK(launch_lwe_op(LWE_MODSWITCH, n, nm, mod, fl, nullptr, tmp, B, s));
+        mod = nm;
+    }
+    HCHECK(launch_lwe_op(LWE_ADD_CONST, n, mod, beta, tmp, nullptr, tmp, B, s));
+    TvParams tv{};
+    tv.mode = TV_SIGN3;
+    tv.ctmod = mod;
+    tv.fmod = q;
+    SCHECK(dev_bootstrap(c, d, tv, 0, tmp, out, B));
+    HCHECK(launch_lwe_op(LWE_SUB_CONST, n, q, q >> 2, out, nullptr, out, B, s));
+    return TFHE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host-array front ends: shard over devices, chunk to scratch, H2D/D2H
+// ---------------------------------------------------------------------------
+template <typename F>
+tfhe_status for_each_shard(tfhe_ctx* c, size_t B, F&& body) {
+    const size_t D = c->devs.size();
+    if (D == 1 || B < 2 * D) {
+        HCHECK(hipSetDevice(c->devs[0].id));
+        return body(c->devs[0], (size_t)0, B);
+    }
+    std::vector<tfhe_status> st(D, TFHE_OK);
+    std::vector<std::string> msg(D);
+    std::vector<std::thread> th;
+    const size_t per = (B + D - 1) / D;
+    for (size_t g = 0; g < D; ++g) {
+        const size_t lo = std::min(B, g * per), hi = std::min(B, lo + per);
+        th.emplace_back([&, g, lo, hi] {
+            if (hipSetDevice(c->devs[g].id) != hipSuccess) {
+                st[g] = TFHE_ERR_DEVICE;
+                msg[g] = "hipSetDevice failed";
+                return;
+            }
+            if (hi > lo) st[g] = body(c->devs[g], lo, hi - lo);
+            if (st[g] != TFHE_OK) msg[g] = g_last_error;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (size_t g = 0; g < D; ++g)
+        if (st[g] != TFHE_OK) return fail(st[g], "device " + std::to_string(g) + ": " + msg[g]);
+    return TFHE_OK;
+}
+
+// Generic chunked runner: in-arrays are [B][in_words] (up to 2), out [B][out_words].
+template <typename Op>
+tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
+                          uint64_t* out, size_t wo, Op&& op) {
+    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+        const size_t chunk = std::min(cnt, c->max_chunk);
+        SCHECK(ensure_scratch(c, d, chunk));
+        // staging buffers for inputs/outputs live in lwe[...] slots reserved by the caller's op
+        uint64_t *din1 = nullptr, *din2 = nullptr, *dout = nullptr;
+        const size_t need1 = chunk * w1 * 8, need2 = chunk * w2 * 8, needo = chunk * wo * 8;
+        HCHECK(hipMalloc(&din1, std::max<size_t>(need1, 8)));
+        if (in2) HCHECK(hipMalloc(&din2, std::max<size_t>(need2, 8)));
+        HCHECK(hipMalloc(&dout, std::max<size_t>(needo, 8)));
+        tfhe_status st = TFHE_OK;
+        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
+            const size_t b = std::min(chunk, lo + cnt - off);
+            if (hipMemcpyAsync(din1, in1 + off * w1, b * w1 * 8, hipMemcpyHostToDevice, d.stream) != hipSuccess ||
+                (in2 && hipMemcpyAsync(din2, in2 + off * w2, b * w2 * 8, hipMemcpyHostToDevice, d.stream) !=
+                            hipSuccess)) {
+                st = fail(TFHE_ERR_DEVICE, "H2D copy failed");
+                break;
+            }
+            st = op(d, din1, din2, dout, b);
+            if (st != TFHE_OK) break;
+            if (hipMemcpyAsync(out + off * wo, dout, b * wo * 8, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+                hipStreamSynchronize(d.stream) != hipSuccess)
+                st = fail(TFHE_ERR_DEVICE, std::string("D2H/sync failed: ") + hipGetErrorString(hipGetLastError()));
+        }
+        hipStreamSynchronize(d.stream);
+        hipFree(din1);
+        hipFree(din2);
+        hipFree(dout);
+        return st;
+    });
+}
+
+tfhe_status check_ctx(tfhe_ctx* c) {
+    if (!c || c->devs.empty()) return fail(TFHE_ERR_NOT_SET_UP, "context not set up (call tfhe_setup)");
+    return TFHE_OK;
+}
+
+tfhe_status create_ctx(const tfhe_params* p, int num_gpus, std::unique_ptr<tfhe_ctx>& out) {
+    if (!p) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
+    auto c = std::make_unique<tfhe_ctx>();
+    c->p = *p;
+    std::string err;
+    if (params_finish(&c->p, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
+    SCHECK(init_derived(c.get()));
+    int count = 0;
+    HCHECK(hipGetDeviceCount(&count));
+    if (num_gpus < 1) num_gpus = 1;
+    if (num_gpus > count)
+        return fail(TFHE_ERR_INVALID_ARGUMENT,
+                    "requested " + std::to_string(num_gpus) + " GPUs, " + std::to_string(count) + " visible");
+    c->devs.resize(num_gpus);
+    for (int g = 0; g < num_gpus; ++g) c->devs[g].id = g;
+    out = std::move(c);
+    return TFHE_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// extern "C" entry points
+// ===========================================================================
+extern "C" {
+
+int tfhe_abi_version(void) { return TFHE_HIP_ABI_VERSION; }
+
+const char* tfhe_last_error(void) { return g_last_error.c_str(); }
+
+const char* tfhe_status_string(tfhe_status s) {
+    switch (s) {
+        case TFHE_OK: return "ok";
+        case TFHE_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case TFHE_ERR_UNSUPPORTED: return "unsupported";
+        case TFHE_ERR_NOT_SET_UP: return "not set up";
+        case TFHE_ERR_DEVICE: return "device error";
+        case TFHE_ERR_OUT_OF_MEMORY: return "out of memory";
+        default: return "internal error";
+    }
+}
+
+tfhe_status tfhe_params_from_set(int paramset, tfhe_params* out) {
+    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+    tfhe_status s = params_from_set(paramset, out);
+    if (s != TFHE_OK) return fail(s, "unknown parameter set");
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_params_from_logq(int paramset, int arb_func, uint32_t logQ, int64_t N, uint32_t baseG,
+                                  uint32_t num_digits_to_throw, tfhe_params* out) {
+    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+    tfhe_status s = params_from_logq(paramset, arb_func, logQ, N, baseG, num_digits_to_throw, out);
+    if (s != TFHE_OK) return fail(s, "unsupported logQ parameter request (STD128/TOY, 11 <= logQ <= 29)");
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_params_finish(tfhe_params* p) {
+    if (!p) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
+    std::string err;
+    tfhe_status s = params_finish(p, &err);
+    return s == TFHE_OK ? s : fail(s, err);
+}
+
+tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
+                       int num_gpus) {
+    if (!out || !bsk_coeff || !ksk) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    std::unique_ptr<tfhe_ctx> c;
+    SCHECK(create_ctx(p, num_gpus, c));
+    std::vector<unsigned char> img;
+    SCHECK(build_host_image(c.get(), bsk_coeff, ksk, img));
+    const size_t bytes = c->layout.total;
+    for (size_t g = 0; g < c->devs.size(); ++g) {
+        Device& d = c->devs[g];
+        HCHECK(hipSetDevice(d.id));
+        HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        HCHECK(hipMalloc(&d.arena, bytes));
+        if (g == 0) {
+            HCHECK(hipMemcpy(d.arena, img.data(), bytes, hipMemcpyHostToDevice));
+        } else {
+            // replicate device 0's image over xGMI (peer DMA; staged by the runtime if P2P is off)
+            HCHECK(hipMemcpyPeer(d.arena, d.id, c->devs[0].arena, c->devs[0].id, bytes));
+        }
+        SCHECK(finish_device(c.get(), d));
+    }
+    *out = c.release();
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, const void* d_src, size_t bytes,
+                                      int device) {
+    if (!out || !d_src) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    std::unique_ptr<tfhe_ctx> c;
+    SCHECK(create_ctx(p, 1, c));
+    if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+    Device& d = c->devs[0];
+    d.id = device;
+    HCHECK(hipSetDevice(device));
+    HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HCHECK(hipMalloc(&d.arena, bytes));
+    HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
+    SCHECK(finish_device(c.get(), d));
+    *out = c.release();
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_export_key_image(tfhe_ctx* c, void* d_dst, size_t bytes, void* stream) {
+    SCHECK(check_ctx(c));
+    if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+    HCHECK(hipSetDevice(c->devs[0].id));
+    hipStream_t s = stream ? (hipStream_t)stream : c->devs[0].stream;
+    HCHECK(hipMemcpyAsync(d_dst, c->devs[0].arena, bytes, hipMemcpyDeviceToDevice, s));
+    HCHECK(hipStreamSynchronize(s));
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_clean(tfhe_ctx* c) {
+    if (!c) return TFHE_OK;
+    for (auto& d : c->devs) free_device(d);
+    delete c;
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
+    SCHECK(check_ctx(c));
+    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+    out->num_devices = (int)c->devs.size();
+    out->word_bits = c->word_bits;
+    out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0);
+    out->ksk_device_bytes = c->layout.total - c->layout.ksk;
+    out->bootstraps = c->bootstraps.load();
+    out->key_image_bytes = c->layout.total;
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_mod, uint64_t* acc) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return TFHE_OK;
+    if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const tfhe_params& p = c->p;
+    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+        const size_t chunk = std::min(cnt, c->max_chunk);
+        SCHECK(ensure_scratch(c, d, chunk));
+        for (size_t off = lo; off < lo + cnt; off += chunk) {
+            const size_t b = std::min(chunk, lo + cnt - off);
+            HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
+            HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * 2 * p.N, b * 2 * p.N * 8, hipMemcpyHostToDevice, d.stream));
+            SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
+            HCHECK(hipMemcpyAsync(acc + off * 2 * p.N, d.sc.acc, b * 2 * p.N * 8, hipMemcpyDeviceToHost, d.stream));
+            HCHECK(hipStreamSynchronize(d.stream));
+        }
+        return TFHE_OK;
+    });
+}
+
+tfhe_status tfhe_eval_acc_device(tfhe_ctx* c, size_t B, const uint64_t* d_a, uint64_t a_mod, uint64_t* d_acc,
+                                 void* stream) {
+    SCHECK(check_ctx(c));
+    Device& d = c->devs[0];
+    HCHECK(hipSetDevice(d.id));
+    hipStream_t saved = d.stream;
+    if (stream) d.stream = (hipStream_t)stream;
+    tfhe_status st = dev_blind_rotate(c, d, d_a, a_mod, d_acc, B);
+    d.stream = saved;
+    return st;
+}
+
+tfhe_status tfhe_mkm_switch(tfhe_ctx* c, size_t B, const uint64_t* ct_ext, uint64_t fmod, uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return TFHE_OK;
+    if (!ct_ext || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const tfhe_params& p = c->p;
+    return run_lwe_batch(c, B, ct_ext, p.N + 1, nullptr, 0, out, p.n + 1,
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                             return dev_mkm(c, d, i1, fmod, o, b);
+                         });
+}
+
+tfhe_status tfhe_mkm_switch_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct_ext, uint64_t fmod, uint64_t* d_out,
+                                   void* stream) {
+    SCHECK(check_ctx(c));
+    Device& d = c->devs[0];
+    HCHECK(hipSetDevice(d.id));
+    hipStream_t saved = d.stream;
+    if (stream) d.stream = (hipStream_t)stream;
+    tfhe_status st = dev_mkm(c, d, d_ct_ext, fmod, d_out, B);
+    d.stream = saved;
+    return st;
+}
+
+tfhe_status tfhe_eval_bin_gate(tfhe_ctx* c, int gate, size_t B, const uint64_t* ct1, const uint64_t* ct2, uint64_t q,
+                               uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalBinGate: input vector is empty");
+    if (!ct1 || !ct2 || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    if (ct1 == ct2) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts should be independant");
+    if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
+    const size_t w = c->p.n + 1;
+    return run_lwe_batch(c, B, ct1, w, ct2, w, out, w,
+                         [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b) {
+                             return dev_gate(c, d, gate, i1, i2, q, o, b);
+                         });
+}
+
+tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* c, int gate, size_t B, const uint64_t* d_ct1, const uint64_t* d_ct2,
+                                      uint64_t q, uint64_t* d_out, void* stream) {
+    SCHECK(check_ctx(c));
+    if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
+    Device& d = c->devs[0];
+    HCHECK(hipSetDevice(d.id));
+    SCHECK(ensure_scratch(c, d, B));
+    hipStream_t saved = d.stream;
+    if (stream) d.stream = (hipStream_t)stream;
+    tfhe_status st = dev_gate(c, d, gate, d_ct1, d_ct2, q, d_out, B);
+    d.stream = saved;
+    return st;
+}
+
+tfhe_status tfhe_eval_func(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t q, const uint64_t* lut, int per_ct_lut,
+                           uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFunc: input vector is empty");
+    if (!ct || !lut || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    if (q < 4 || (2ull * c->p.N) % q) return fail(TFHE_ERR_INVALID_ARGUMENT, "q must divide 2N");
+    // LUT classification uses the first LUT, as the reference (binfhe-base-scheme.cpp:697-698, 815-816)
+    const int prop = check_input_function(lut, q, q);
+    const size_t w = c->p.n + 1;
+    const uint64_t stride = per_ct_lut ? q : 0;
+    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+        uint64_t* d_lut = nullptr;
+        const size_t lut_words = per_ct_lut ? cnt * q : q;
+        HCHECK(hipMalloc(&d_lut, lut_words * 8));
+        HCHECK(hipMemcpy(d_lut, lut + (per_ct_lut ? lo * q : 0), lut_words * 8, hipMemcpyHostToDevice));
+        const size_t chunk = std::min(cnt, c->max_chunk);
+        tfhe_status st = ensure_scratch(c, d, chunk);
+        uint64_t *din = nullptr, *dout = nullptr;
+        if (st == TFHE_OK && (hipMalloc(&din, chunk * w * 8) != hipSuccess || hipMalloc(&dout, chunk * w * 8) != hipSuccess))
+            st = fail(TFHE_ERR_OUT_OF_MEMORY, "staging allocation failed");
+        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
+            const size_t b = std::min(chunk, lo + cnt - off);
+            if (hipMemcpyAsync(din, ct + off * w, b * w * 8, hipMemcpyHostToDevice, d.stream) != hipSuccess) {
+                st = fail(TFHE_ERR_DEVICE, "H2D failed");
+                break;
+            }
+            st = dev_func(c, d, prop, din, q, d_lut + (per_ct_lut ? (off - lo) * q : 0), stride, dout, b);
+            if (st != TFHE_OK) break;
+            if (hipMemcpyAsync(out + off * w, dout, b * w * 8, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
+                hipStreamSynchronize(d.stream) != hipSuccess)
+                st = fail(TFHE_ERR_DEVICE, "D2H/sync failed");
+        }
+        hipStreamSynchronize(d.stream);
+        hipFree(din);
+        hipFree(dout);
+        hipFree(d_lut);
+        return st;
+    });
+}
+
+tfhe_status tfhe_eval_floor(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint32_t roundbits,
+                            uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFloor: input vector is empty");
+    if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const size_t w = c->p.n + 1;
+    return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                             return dev_floor(c, d, i1, mod, roundbits, o, b);
+                         });
+}
+
+tfhe_status tfhe_eval_sign(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalSign: input vector is empty");
+    if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const size_t w = c->p.n + 1;
+    return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                             return dev_sign(c, d, i1, mod, o, b);
+                         });
+}
+
+tfhe_status tfhe_eval_decomp(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint32_t max_digits,
+                             uint64_t* out, uint64_t* moduli, uint32_t* num_digits) {
+    SCHECK(check_ctx(c));
+    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalDecomp: input vector is empty");
+    if (!ct || !out || !moduli || !num_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const uint64_t q = c->p.q, beta = 128;
+    if (mod <= q) return fail(TFHE_ERR_UNSUPPORTED, "EvalDecomp is only for large precision");
+    // digit count and moduli are data independent (binfhe-base-scheme.cpp:1066-1080)
+    std::vector<uint64_t> mods;
+    for (uint64_t m = mod; m > q; m = m / q * 2 * beta) mods.push_back(q);
+    {
+        uint64_t m = mod;
+        while (m > q) m = m / q * 2 * beta;
+        mods.push_back(m);
+    }
+    if (mods.size() > max_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "max_digits too small");
+    for (size_t i = 0; i < mods.size(); ++i) moduli[i] = mods[i];
+    *num_digits = (uint32_t)mods.size();
+    const uint32_t n = c->p.n;
+    const size_t w = n + 1;
+    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+        const size_t chunk = std::min(cnt, c->max_chunk);
+        SCHECK(ensure_scratch(c, d, chunk));
+        uint64_t *tmp = nullptr, *fl = nullptr, *dig = nullptr;
+        HCHECK(hipMalloc(&tmp, chunk * w * 8));
+        HCHECK(hipMalloc(&fl, chunk * w * 8));
+        HCHECK(hipMalloc(&dig, chunk * w * 8));
+        std::vector<uint64_t> host_digit(chunk * w);
+        tfhe_status st = TFHE_OK;
+        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
+            const size_t b = std::min(chunk, lo + cnt - off);
+            HCHECK(hipMemcpyAsync(tmp, ct + off * w, b * w * 8, hipMemcpyHostToDevice, d.stream));
+            uint64_t m = mod;
+            for (size_t k = 0; k < mods.size() && st == TFHE_OK; ++k) {
+                if (k + 1 < mods.size()) HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, tmp, nullptr, dig, b, d.stream));
+                else HCHECK(hipMemcpyAsync(dig, tmp, b * w * 8, hipMemcpyDeviceToDevice, d.stream));
+                HCHECK(hipMemcpyAsync(host_digit.data(), dig, b * w * 8, hipMemcpyDeviceToHost, d.stream));
+                HCHECK(hipStreamSynchronize(d.stream));
+                for (size_t s = 0; s < b; ++s)
+                    std::memcpy(out + ((off + s) * max_digits + k) * w, host_digit.data() + s * w, w * 8);
+                if (k + 1 < mods.size()) {
+                    st = dev_floor(c, d, tmp, m, 0, fl, b);
+                    const uint64_t nm = m / q * 2 * beta;
+                    HCHECK(launch_lwe_op(LWE_MODSWITCH, n, nm, m, fl, nullptr, tmp, b, d.stream));
+                    m = nm;
+                }
+            }
+        }
+        hipStreamSynchronize(d.stream);
+        hipFree(tmp);
+        hipFree(fl);
+        hipFree(dig);
+        return st;
+    });
+}
+
+tfhe_status tfhe_ciphertext_mul_matrix(tfhe_ctx* c, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
+                                       uint64_t modulus, uint64_t* out) {
+    SCHECK(check_ctx(c));
+    if (K == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts are empty.");
+    if (cols == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input matrix is empty.");
+    if (!ct || !matrix || !out || modulus == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    const uint32_t w = c->p.n + 1;
+    Device& d = c->devs[0];
+    HCHECK(hipSetDevice(d.id));
+    uint64_t *dct = nullptr, *dout = nullptr;
+    int64_t* dm = nullptr;
+    HCHECK(hipMalloc(&dct, K * w * 8));
+    HCHECK(hipMalloc(&dm, K * cols * 8));
+    HCHECK(hipMalloc(&dout, cols * w * 8));
+    HCHECK(hipMemcpyAsync(dct, ct, K * w * 8, hipMemcpyHostToDevice, d.stream));
+    HCHECK(hipMemcpyAsync(dm, matrix, K * cols * 8, hipMemcpyHostToDevice, d.stream));
+    HCHECK(launch_ct_mul_matrix(w, K, dct, cols, dm, modulus, dout, d.stream));
+    HCHECK(hipMemcpyAsync(out, dout, cols * w * 8, hipMemcpyDeviceToHost, d.stream));
+    HCHECK(hipStreamSynchronize(d.stream));
+    hipFree(dct);
+    hipFree(dm);
+    hipFree(dout);
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_lwe_gpu_setup(int num_gpus) {
+    int count = 0;
+    HCHECK(hipGetDeviceCount(&count));
+    if (num_gpus > count) return fail(TFHE_ERR_INVALID_ARGUMENT, "not enough GPUs");
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_lwe_gpu_clean(void) { return TFHE_OK; }
+
+tfhe_status tfhe_host_selftest(const tfhe_params* pin) {
+    if (!pin) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
+    tfhe_params p = *pin;
+    std::string err;
+    if (params_finish(&p, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
+    NttTables t = make_ntt_tables(p.Q, p.N);
+    // (1) forward/inverse round trip and (2) product vs schoolbook on a pseudo-random pair
+    std::vector<uint64_t> a(p.N), b(p.N), ref(p.N, 0);
+    uint64_t s = 0x1234567;
+    for (uint32_t i = 0; i < p.N; ++i) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        a[i] = (s >> 7) % p.Q;
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        b[i] = (s >> 7) % p.Q;
+    }
+    for (uint32_t i = 0; i < p.N; ++i)
+        for (uint32_t j = 0; j < p.N; ++j) {
+            uint64_t v = mulmod(a[i], b[j], p.Q);
+            if (i + j < p.N) ref[i + j] = addmod(ref[i + j], v, p.Q);
+            else ref[i + j - p.N] = submod(ref[i + j - p.N], v, p.Q);
+        }
+    std::vector<uint64_t> A = a, Bv = b;
+    host_ntt_fwd(t, A.data());
+    host_ntt_fwd(t, Bv.data());
+    for (uint32_t i = 0; i < p.N; ++i) A[i] = mulmod(A[i], Bv[i], p.Q);
+    host_ntt_inv(t, A.data(), true);
+    if (A != ref) return fail(TFHE_ERR_INTERNAL, "host NTT product mismatch");
+    // (3) monomial table: NTT(X^m)[x] = psi^(e_x * m)
+    for (uint32_t m : {1u, 3u, p.N - 1, p.N + 5, 2 * p.N - 1}) {
+        std::vector<uint64_t> mon(p.N, 0);
+        if (m < p.N) mon[m] = 1;
+        else mon[m - p.N] = p.Q - 1;
+        host_ntt_fwd(t, mon.data());
+        for (uint32_t x = 0; x < p.N; ++x) {
+            uint32_t idx = (uint32_t)(((uint64_t)t.eidx[x] * m) % (2ull * p.N));
+            if (mon[x] != addmod(t.mono[idx], 1, p.Q)) return fail(TFHE_ERR_INTERNAL, "monomial table mismatch");
+        }
+    }
+    // (4) Shoup companions at the chosen word width
+    const int wb = word_bits_for(p);
+    const u128 R = (u128)1 << wb;
+    for (uint32_t x = 0; x < p.N; ++x) {
+        const uint64_t w = t.psi_br[x], wp = shoup_companion(w, p.Q, wb);
+        const uint64_t aa = a[x] | (wb == 32 ? 0x80000000ull : 0x8000000000000000ull);
+        const uint64_t mask = wb == 32 ? 0xFFFFFFFFull : ~0ull;
+        const uint64_t qt = (uint64_t)(((u128)aa * wp) >> wb);
+        const uint64_t r = (uint64_t)(((u128)aa * w - (u128)qt * p.Q) % R) & mask;
+        if (r >= 2 * p.Q || r % p.Q != mulmod(aa % p.Q, w, p.Q)) return fail(TFHE_ERR_INTERNAL, "Shoup bound");
+    }
+    return TFHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,252 @@
+// host_math.cpp -- see host_math.hpp.
+#include "host_math.hpp"
+
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+
+namespace tfhe {
+
+uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
+    uint64_t r = 1 % m;
+    b %= m;
+    for (; e; e >>= 1) {
+        if (e & 1) r = mulmod(r, b, m);
+        b = mulmod(b, b, m);
+    }
+    return r;
+}
+
+bool is_prime(uint64_t x) {
+    // deterministic Miller-Rabin, valid for all 64-bit x
+    static const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    if (x < 2) return false;
+    for (uint64_t b : bases) {
+        if (x == b) return true;
+        if (x % b == 0) return false;
+    }
+    uint64_t d = x - 1;
+    int s = 0;
+    while ((d & 1) == 0) d >>= 1, ++s;
+    for (uint64_t b : bases) {
+        uint64_t y = powmod(b, d, x);
+        if (y == 1 || y == x - 1) continue;
+        bool witness = true;
+        for (int r = 1; r < s && witness; ++r) {
+            y = mulmod(y, y, x);
+            if (y == x - 1) witness = false;
+        }
+        if (witness) return false;
+    }
+    return true;
+}
+
+uint32_t ilog2(uint64_t x) {
+    uint32_t r = 0;
+    while (x > 1) x >>= 1, ++r;
+    return r;
+}
+
+uint32_t bitrev(uint32_t x, uint32_t bits) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < bits; ++i) r = (r << 1) | ((x >> i) & 1u);
+    return r;
+}
+
+// nbtheory.cpp:481-516 (FirstPrime) and :565-579 (PreviousPrime): primes = 1 mod m
+static uint64_t first_prime(uint32_t bits, uint64_t m) {
+    uint64_t r = powmod(2, bits, m);
+    uint64_t c = (uint64_t(1) << bits) + (r ? (m - r) + 1 : 1);
+    while (!is_prime(c)) c += m;
+    return c;
+}
+static uint64_t previous_prime(uint64_t q, uint64_t m) {
+    uint64_t c = q - m;
+    while (!is_prime(c)) c -= m;
+    return c;
+}
+
+tfhe_status params_finish(tfhe_params* p, std::string* err) {
+    auto fail = [&](const char* m) {
+        if (err) *err = m;
+        return TFHE_ERR_INVALID_ARGUMENT;
+    };
+    if (p->N < 16 || (p->N & (p->N - 1))) return fail("N must be a power of two >= 16");
+    if (p->baseG < 2 || (p->baseG & (p->baseG - 1))) return fail("gadget base must be a power of two");
+    if (p->Q < 3 || p->Q % (2ull * p->N) != 1) return fail("Q must be a prime = 1 mod 2N");
+    if (p->Q >= (1ull << 58)) return fail("Q >= 2^58 not supported");
+    if (p->q == 0 || (2ull * p->N) % p->q != 0) return fail("q must divide 2N");
+    if (p->qKS < 2 || p->baseKS < 2) return fail("bad key-switching modulus/base");
+    // rgsw-cryptoparameters.h:87 and lwe-pke.cpp:305: natural-log ratios, as the reference computes them
+    p->digitsG = (uint32_t)std::ceil(std::log((double)p->Q) / std::log((double)p->baseG));
+    p->dKS = (uint32_t)std::ceil(std::log((double)p->qKS) / std::log((double)p->baseKS));
+    if (p->digitsG <= p->numDigitsToThrow) return fail("numDigitsToThrow leaves no gadget digit");
+    p->dG2 = 2 * (p->digitsG - p->numDigitsToThrow);
+    return TFHE_OK;
+}
+
+tfhe_status params_from_set(int set, tfhe_params* p) {
+    // binfhecontext.cpp:137-155 (numberBits, cyclOrder, n, q, qKS [0 = Q], baseKS, baseG)
+    struct Row { int set; uint32_t bits, cycl, n, q; uint64_t qks; uint32_t bks, g; };
+    static const Row rows[] = {
+        {TFHE_TOY, 27, 1024, 64, 512, 0, 25, 1u << 9},
+        {TFHE_MEDIUM, 28, 2048, 422, 1024, 1u << 14, 1u << 7, 1u << 10},
+        {TFHE_STD128_AP, 27, 2048, 512, 1024, 1u << 14, 1u << 7, 1u << 9},
+        {TFHE_STD128_APOPT, 27, 2048, 502, 1024, 1u << 14, 1u << 7, 1u << 9},
+        {TFHE_STD128, 27, 2048, 512, 1024, 1u << 14, 1u << 7, 1u << 7},
+        {TFHE_STD128_OPT, 27, 2048, 502, 1024, 1u << 14, 1u << 7, 1u << 7},
+        {TFHE_STD192, 37, 4096, 1024, 1024, 1u << 19, 28, 1u << 14},
+        {TFHE_STD192_OPT, 37, 4096, 805, 1024, 1u << 15, 32, 1u << 13},
+        {TFHE_STD256, 29, 4096, 1024, 2048, 1u << 14, 1u << 7, 1u << 8},
+        {TFHE_STD256_OPT, 29, 4096, 990, 2048, 1u << 14, 1u << 7, 1u << 8},
+        {TFHE_STD128Q, 50, 4096, 1024, 1024, 1u << 25, 32, 1u << 25},
+        {TFHE_STD128Q_OPT, 50, 4096, 585, 1024, 1u << 15, 32, 1u << 25},
+        {TFHE_STD192Q, 35, 4096, 1024, 1024, 1u << 17, 64, 1u << 14},
+        {TFHE_STD192Q_OPT, 35, 4096, 875, 1024, 1u << 15, 32, 1u << 12},
+        {TFHE_STD256Q, 27, 4096, 2048, 2048, 1u << 16, 16, 1u << 7},
+        {TFHE_STD256Q_OPT, 27, 4096, 1225, 1024, 1u << 16, 16, 1u << 7},
+        {TFHE_SIGNED_MOD_TEST, 28, 2048, 512, 1024, 0, 25, 1u << 7},
+    };
+    for (const Row& r : rows) {
+        if (r.set != set) continue;
+        std::memset(p, 0, sizeof(*p));
+        p->Q = previous_prime(first_prime(r.bits, r.cycl), r.cycl);
+        p->N = r.cycl / 2;
+        p->n = r.n;
+        p->q = r.q;
+        p->qKS = r.qks ? r.qks : p->Q;
+        p->baseKS = r.bks;
+        p->baseG = r.g;
+        return params_finish(p, nullptr);
+    }
+    return TFHE_ERR_INVALID_ARGUMENT;
+}
+
+// StdLatticeParm::FindRingDim(HEStd_ternary, HEStd_128_classic, logQ), stdlatticeparms.cpp:110-130
+static uint32_t ring_dim_ternary128(uint32_t logQ) {
+    static const uint32_t dim[] = {1024, 2048, 4096, 8192, 16384, 32768, 65536};
+    static const uint32_t maxlogq[] = {27, 54, 109, 218, 438, 881, 1772};
+    uint32_t prev = 0;
+    for (int i = 0; i < 7; ++i) {
+        if (logQ <= maxlogq[i] && logQ > prev) return dim[i];
+        prev = maxlogq[i];
+    }
+    return 131072;
+}
+
+tfhe_status params_from_logq(int set, int arb_func, uint32_t logQ, int64_t N, uint32_t baseG, uint32_t thr,
+                             tfhe_params* p) {
+    // binfhecontext.cpp:51-113
+    if (set != TFHE_STD128 && set != TFHE_TOY) return TFHE_ERR_UNSUPPORTED;
+    if (logQ > 29 || logQ < 11) return TFHE_ERR_UNSUPPORTED;
+    uint32_t logQprime = 54;
+    if (baseG == 0) {
+        if (logQ > 25) baseG = 1u << 14;
+        else if (logQ > 16) baseG = 1u << 18;
+        else if (logQ > 11) baseG = 1u << 27;
+        else baseG = 1u << 5, logQprime = 27;
+    }
+    uint32_t ring = ring_dim_ternary128(logQprime);
+    if (N >= (int64_t)ring) ring = (uint32_t)N;
+    std::memset(p, 0, sizeof(*p));
+    p->Q = previous_prime(first_prime(logQprime, 2ull * ring), 2ull * ring);
+    p->N = ring;
+    p->q = arb_func ? ring : 2ull * ring;
+    p->qKS = 1ull << 35;
+    p->n = set == TFHE_TOY ? 32 : 1305;
+    p->baseKS = 32;
+    p->baseG = baseG;
+    p->numDigitsToThrow = thr;
+    return params_finish(p, nullptr);
+}
+
+int word_bits_for(const tfhe_params& p) {
+    if (p.Q < (1ull << 31) && (u128)2 * p.dG2 * p.Q < ((u128)1 << 32)) return 32;
+    return 64;
+}
+
+NttTables make_ntt_tables(uint64_t Q, uint32_t N) {
+    NttTables t;
+    t.N = N;
+    t.logN = ilog2(N);
+    t.Q = Q;
+    for (uint64_t g = 2;; ++g) {
+        uint64_t x = powmod(g, (Q - 1) / (2ull * N), Q);
+        if (powmod(x, N, Q) == Q - 1) {
+            t.psi = x;
+            break;
+        }
+    }
+    uint64_t ipsi = powmod(t.psi, Q - 2, Q);
+    t.Ninv = powmod(N, Q - 2, Q);
+    t.psi_br.resize(N);
+    t.ipsi_br.resize(N);
+    for (uint32_t k = 0; k < N; ++k) {
+        uint32_t e = bitrev(k, t.logN);
+        t.psi_br[k] = powmod(t.psi, e, Q);
+        t.ipsi_br[k] = powmod(ipsi, e, Q);
+    }
+    t.mono.resize(2ull * N);
+    std::unordered_map<uint64_t, uint32_t> dlog;
+    uint64_t pw = 1;
+    for (uint32_t k = 0; k < 2 * N; ++k) {
+        t.mono[k] = submod(pw, 1, Q);
+        dlog[pw] = k;
+        pw = mulmod(pw, t.psi, Q);
+    }
+    // e_x from the transform itself: NTT(X)[x] = psi^(e_x)
+    std::vector<uint64_t> x(N, 0);
+    x[1] = 1;
+    host_ntt_fwd(t, x.data());
+    t.eidx.resize(N);
+    for (uint32_t k = 0; k < N; ++k) t.eidx[k] = dlog.at(x[k]);
+    return t;
+}
+
+void host_ntt_fwd(const NttTables& t, uint64_t* a) {
+    const uint64_t Q = t.Q;
+    uint32_t len = t.N;
+    for (uint32_t m = 1; m < t.N; m <<= 1) {
+        len >>= 1;
+        for (uint32_t i = 0; i < m; ++i) {
+            const uint64_t S = t.psi_br[m + i];
+            for (uint32_t j = 2 * i * len; j < 2 * i * len + len; ++j) {
+                uint64_t U = a[j], V = mulmod(a[j + len], S, Q);
+                a[j] = addmod(U, V, Q);
+                a[j + len] = submod(U, V, Q);
+            }
+        }
+    }
+}
+
+void host_ntt_inv(const NttTables& t, uint64_t* a, bool scale) {
+    const uint64_t Q = t.Q;
+    uint32_t len = 1;
+    for (uint32_t m = t.N; m > 1; m >>= 1, len <<= 1) {
+        const uint32_t h = m >> 1;
+        for (uint32_t i = 0; i < h; ++i) {
+            const uint64_t S = t.ipsi_br[h + i];
+            for (uint32_t j = 2 * i * len; j < 2 * i * len + len; ++j) {
+                uint64_t U = a[j], V = a[j + len];
+                a[j] = addmod(U, V, Q);
+                a[j + len] = mulmod(submod(U, V, Q), S, Q);
+            }
+        }
+    }
+    if (scale)
+        for (uint32_t j = 0; j < t.N; ++j) a[j] = mulmod(a[j], t.Ninv, Q);
+}
+
+void bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk_coeff, uint64_t* out) {
+    const size_t polys = (size_t)p.n * 2 * p.dG2 * 2;
+    const uint32_t N = p.N;
+    parallel_for(polys, [&](size_t k) {
+        uint64_t* dst = out + (size_t)k * N;
+        const uint64_t* src = bsk_coeff + (size_t)k * N;
+        for (uint32_t x = 0; x < N; ++x) dst[x] = src[x] % p.Q;
+        host_ntt_fwd(t, dst);
+        for (uint32_t x = 0; x < N; ++x) dst[x] = mulmod(dst[x], t.Ninv, p.Q);
+    });
+}
+
+}  // namespace tfhe

@@ -1,0 +1,93 @@
+// host_math.hpp -- host-side number theory for the engine: parameter selection
+// (binfhecontext.cpp:42-181), negacyclic NTT tables, Shoup companions, and the
+// one-time BSK/KSK conversion into the device layout.  Pure C++ (no HIP), so it
+// is unit-testable without a GPU (tfhe_host_selftest).
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tfhe_hip.h"
+
+namespace tfhe {
+
+// Host worker count: hardware threads, capped (TFHE_HOST_THREADS overrides; the
+// GPU box grants 16 CPUs per GPU although nproc reports the whole machine).
+inline unsigned host_threads() {
+    if (const char* e = std::getenv("TFHE_HOST_THREADS")) {
+        int v = std::atoi(e);
+        if (v > 0) return (unsigned)v;
+    }
+    unsigned h = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(h ? h : 1u, 16u));
+}
+
+// Static-partition parallel loop over [0, n) with std::thread.
+template <typename F>
+void parallel_for(size_t n, F&& f) {
+    const size_t T = std::min<size_t>(host_threads(), n ? n : 1);
+    if (T <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + T - 1) / T;
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            const size_t lo = t * per, hi = std::min(n, lo + per);
+            for (size_t i = lo; i < hi; ++i) f(i);
+        });
+    for (auto& x : th) x.join();
+}
+
+using u128 = unsigned __int128;
+
+inline uint64_t mulmod(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)(((u128)a * b) % m); }
+inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t m) {
+    uint64_t r = a + b;
+    return r >= m ? r - m : r;
+}
+inline uint64_t submod(uint64_t a, uint64_t b, uint64_t m) { return a >= b ? a - b : a + (m - b); }
+uint64_t powmod(uint64_t b, uint64_t e, uint64_t m);
+bool is_prime(uint64_t x);
+uint32_t ilog2(uint64_t x);
+uint32_t bitrev(uint32_t x, uint32_t bits);
+
+// Shoup companion: floor(w * 2^bits / Q), bits = 32 or 64
+inline uint64_t shoup_companion(uint64_t w, uint64_t Q, int bits) {
+    return (uint64_t)(((u128)w << bits) / Q);
+}
+
+tfhe_status params_from_set(int set, tfhe_params* p);
+tfhe_status params_from_logq(int set, int arb_func, uint32_t logQ, int64_t N, uint32_t baseG, uint32_t thr,
+                             tfhe_params* p);
+tfhe_status params_finish(tfhe_params* p, std::string* err);
+
+// Word width chosen for the blind rotation: 32 when every lazy sum fits a u32
+// (2*dG2*Q < 2^32, Q < 2^31), else 64 (needs Q < 2^58 for the lazy sums).
+int word_bits_for(const tfhe_params& p);
+
+// NTT tables for one (Q, N): psi = primitive 2N-th root; forward CT twiddles in
+// bit-reversed order (Longa-Naehrig), inverse GS twiddles, monomial table
+// psi^k - 1 (k < 2N) and the exponent e_x of the forward-NTT output slot x
+// (NTT(X)[x] = psi^(e_x)).
+struct NttTables {
+    uint32_t N = 0, logN = 0;
+    uint64_t Q = 0, psi = 0, Ninv = 0;
+    std::vector<uint64_t> psi_br, ipsi_br;  // [N]
+    std::vector<uint64_t> mono;             // [2N] psi^k - 1
+    std::vector<uint32_t> eidx;             // [N]
+};
+NttTables make_ntt_tables(uint64_t Q, uint32_t N);
+void host_ntt_fwd(const NttTables& t, uint64_t* a);
+void host_ntt_inv(const NttTables& t, uint64_t* a, bool scale);
+
+// BSK [n][2][dG2][2][N] coefficient form -> NTT domain, scaled by N^-1 (so the
+// device INTT needs no final scaling), same layout.  OpenMP over polynomials.
+void bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk_coeff, uint64_t* out);
+
+}  // namespace tfhe

@@ -1,0 +1,100 @@
+// kernels.hpp -- launch wrappers for the HIP kernels (definitions in *.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace tfhe {
+
+// Scalar parameters every blind-rotation kernel needs (the reference's
+// params_CUDA[10], bootstrapping.cu:917-929, plus derived constants).
+struct BRParams {
+    uint32_t N, logN, n, dG2, digits, thr, logG;
+    uint64_t Q;
+    uint64_t r1;  // floor(2^b / Q), b = word bits, for lazy-sum reduction
+};
+
+// Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
+struct DevTables {
+    const void* psi;     // [N]  forward twiddles, bit-reversed order
+    const void* psi_sh;  // [N]  Shoup companions
+    const void* ipsi;    // [N]  inverse twiddles
+    const void* ipsi_sh; // [N]
+    const void* mono;    // [2N] psi^k - 1
+    const void* mono_sh; // [2N]
+    const uint32_t* eidx;// [N]  NTT(X)[x] = psi^eidx[x]
+};
+
+// Generic LDS-resident blind rotation: one workgroup per ciphertext.
+//   a[B][n] mod amod, acc[B][2][N] (u64, coefficient) in/out, acc0 transposed on exit.
+//   bsk/bsk_sh: [n][2][dG2][2][N] in W, NTT domain, scaled by N^-1.
+hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const DevTables& T, const void* bsk,
+                                       const void* bsk_sh, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B,
+                                       hipStream_t s);
+
+// Fast STD128-class blind rotation (W = u32, N = 1024, dG2 = 8): register-resident
+// transforms, one wavefront per ciphertext.  Returns hipErrorNotSupported when the
+// parameters do not match its specialisation.
+hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables& T, const void* bsk_fast, const uint64_t* a,
+                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+bool fast_path_supported(const BRParams& P, int word_bits);
+// Rearranges the generic device BSK (+companions) into the fast kernel's layout.
+hipError_t launch_pack_bsk_fast(const BRParams& P, const void* bsk, const void* bsk_sh, void* bsk_fast,
+                                hipStream_t s);
+size_t bsk_fast_bytes(const BRParams& P);
+
+// MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
+//   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.  ksk: [N][baseKS][dKS][n+1] in ksk_bits words.
+struct KSParams {
+    uint32_t N, n, baseKS, dKS;
+    uint64_t Q, qKS;
+};
+hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* ksk, const uint64_t* ext, uint64_t fmod,
+                      uint64_t* out, size_t B, hipStream_t s);
+
+// ---- test vectors, extraction and LWE glue (binfhe-base-scheme.cpp) ----
+enum TvMode : uint32_t {
+    TV_GATE = 0,    // BootstrapGateCore: +-(Q/8+1) by range [q1,q2)
+    TV_HALF = 1,    // f0/f1: x<q/2 ? fmod-q/4 : q/4
+    TV_FLOOR2 = 2,  // f2 of EvalFloor
+    TV_SIGN3 = 3,   // f3 of EvalSign
+    TV_LUT = 4,     // LUT[x]
+    TV_LUT1 = 5,    // x<q/2 ? LUT[x] : fmod - LUT[x-q/2]
+    TV_LUT2 = 6,    // LUT2 = LUT++LUT, arbitrary-function second bootstrap
+};
+struct TvParams {
+    uint32_t mode, N, n;
+    uint64_t Q, ctmod, fmod;
+    uint64_t q1, q2;        // gate range
+    uint64_t Q8;            // Q/8 + 1
+    const uint64_t* lut;    // TV_LUT*: [q] or [B][q]
+    uint64_t lut_stride;    // 0: shared LUT
+    uint64_t lut_len;       // original LUT length (q)
+};
+// ct[B][n+1] -> acc[B][2][N] (acc0 = 0, acc1 = test vector), a_out[B][n] = a part
+hipError_t launch_build_testvector(const TvParams& P, const uint64_t* ct, uint64_t* acc, uint64_t* a_out, size_t B,
+                                   hipStream_t s);
+// acc[B][2][N] (acc0 transposed) -> ext[B][N+1]: a = acc0, b = acc1[0] + b_add mod Q
+hipError_t launch_extract(uint32_t N, uint64_t Q, uint64_t b_add, const uint64_t* acc, uint64_t* ext, size_t B,
+                          hipStream_t s);
+
+enum LweOp : uint32_t {
+    LWE_ADD = 0,        // out = x + y mod m
+    LWE_SUB = 1,        // out = x - y mod m
+    LWE_DOUBLE_SUB = 2, // out = 2(x - y) mod m   (XOR_FAST prep)
+    LWE_NOT = 3,        // out = NOT x (EvalNOT, binfhe-base-scheme.cpp:147-159)
+    LWE_ADD_CONST = 4,  // b += c mod m
+    LWE_SUB_CONST = 5,  // b -= c mod m
+    LWE_SET_MOD = 6,    // every word mod m (LWECiphertextImpl::SetModulus)
+    LWE_MODSWITCH = 7,  // RoundqQ(x, m, c)  (lwe-pke.cpp:204-215), c = old modulus
+    LWE_COPY = 8,
+};
+// element-wise over B ciphertexts of n+1 words; y may be null for unary ops
+hipError_t launch_lwe_op(uint32_t op, uint32_t n, uint64_t m, uint64_t c, const uint64_t* x, const uint64_t* y,
+                         uint64_t* out, size_t B, hipStream_t s);
+
+// CiphertextMulMatrix: out[c][w] = sum_k matrix[k][c] * ct[k][w] mod modulus
+hipError_t launch_ct_mul_matrix(uint32_t width, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
+                                uint64_t modulus, uint64_t* out, hipStream_t s);
+
+}  // namespace tfhe

@@ -1,0 +1,139 @@
+"""ctypes declarations of include/tfhe_hip.h."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_amd/
+_ROOT = os.path.dirname(_PKG)
+_LIB = os.path.join(_PKG, "lib", "libtfhe_hip.so")
+HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
+
+# BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
+PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
+             "STD192_OPT": 7, "STD256": 8, "STD256_OPT": 9, "STD128Q": 10, "STD128Q_OPT": 11, "STD192Q": 12,
+             "STD192Q_OPT": 13, "STD256Q": 14, "STD256Q_OPT": 15, "SIGNED_MOD_TEST": 16}
+BINGATE = {"OR": 0, "AND": 1, "NOR": 2, "NAND": 3, "XOR_FAST": 4, "XNOR_FAST": 5, "XOR": 6, "XNOR": 7}
+
+
+class TfheError(RuntimeError):
+    def __init__(self, status: int, where: str, msg: str):
+        super().__init__(f"{where}: status {status}: {msg}")
+        self.status = status
+
+
+class Params(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("N", C.c_uint32), ("q", C.c_uint64), ("Q", C.c_uint64), ("qKS", C.c_uint64),
+                ("baseKS", C.c_uint32), ("baseG", C.c_uint32), ("numDigitsToThrow", C.c_uint32),
+                ("digitsG", C.c_uint32), ("dKS", C.c_uint32), ("dG2", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+    def bsk_words(self):
+        return self.n * 2 * self.dG2 * 2 * self.N
+
+    def ksk_words(self):
+        return self.N * self.baseKS * self.dKS * (self.n + 1)
+
+
+class Info(C.Structure):
+    _fields_ = [("num_devices", C.c_int), ("word_bits", C.c_int), ("bsk_device_bytes", C.c_uint64),
+                ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64)]
+
+
+u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+VP = C.c_void_p
+SZ = C.c_size_t
+U64 = C.c_uint64
+P = C.POINTER(Params)
+
+_SIGS = {
+    "tfhe_abi_version": ([], C.c_int),
+    "tfhe_last_error": ([], C.c_char_p),
+    "tfhe_status_string": ([C.c_int], C.c_char_p),
+    "tfhe_params_from_set": ([C.c_int, P], C.c_int),
+    "tfhe_params_from_logq": ([C.c_int, C.c_int, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, P], C.c_int),
+    "tfhe_params_finish": ([P], C.c_int),
+    "tfhe_setup": ([C.POINTER(VP), P, u64p, u64p, C.c_int], C.c_int),
+    "tfhe_clean": ([VP], C.c_int),
+    "tfhe_eval_acc": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_ciphertext_mul_matrix": ([VP, SZ, u64p, SZ, i64p, U64, u64p], C.c_int),
+    "tfhe_lwe_gpu_setup": ([C.c_int], C.c_int),
+    "tfhe_lwe_gpu_clean": ([], C.c_int),
+    "tfhe_eval_bin_gate": ([VP, C.c_int, SZ, u64p, u64p, U64, u64p], C.c_int),
+    "tfhe_eval_func": ([VP, SZ, u64p, U64, u64p, C.c_int, u64p], C.c_int),
+    "tfhe_eval_floor": ([VP, SZ, u64p, U64, C.c_uint32, u64p], C.c_int),
+    "tfhe_eval_sign": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_eval_decomp": ([VP, SZ, u64p, U64, C.c_uint32, u64p, u64p, C.POINTER(C.c_uint32)], C.c_int),
+    "tfhe_eval_bin_gate_device": ([VP, C.c_int, SZ, VP, VP, U64, VP, VP], C.c_int),
+    "tfhe_eval_acc_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
+    "tfhe_mkm_switch_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
+    "tfhe_export_key_image": ([VP, VP, SZ, VP], C.c_int),
+    "tfhe_setup_from_key_image": ([C.POINTER(VP), P, VP, SZ, C.c_int], C.c_int),
+    "tfhe_get_info": ([VP, C.POINTER(Info)], C.c_int),
+    "tfhe_host_selftest": ([P], C.c_int),
+}
+
+
+def library_path() -> str:
+    return _LIB
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP library for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", _PKG, f"-j{jobs}"], check=True)
+    return _LIB
+
+
+def exported_symbols() -> list[str]:
+    """Function names declared in include/tfhe_hip.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(tfhe_[a-z0-9_]+)\s*\(", txt)))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            raise TfheError(-1, "load", f"{_LIB} missing: run tfhe_amd.build() (make -C tfhe-gpu_amd)")
+        L = C.CDLL(_LIB)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(status: int, where: str):
+    if status != 0:
+        msg = lib().tfhe_last_error().decode(errors="replace")
+        raise TfheError(status, where, msg)
+
+
+def params_from_set(name: str) -> Params:
+    p = Params()
+    check(lib().tfhe_params_from_set(PARAMSETS[name], C.byref(p)), "tfhe_params_from_set")
+    return p
+
+
+def params_from_logq(name: str, arb_func: bool, logQ: int, N: int = 0, baseG: int = 0, throw: int = 0) -> Params:
+    """GenerateBinFHEContext(set, arbFunc, logQ, N, GINX, false, baseG, numDigitsToThrow)."""
+    p = Params()
+    check(lib().tfhe_params_from_logq(PARAMSETS[name], int(arb_func), logQ, N, baseG, throw, C.byref(p)),
+          "tfhe_params_from_logq")
+    return p
+
+
+def host_selftest(p: Params):
+    check(lib().tfhe_host_selftest(C.byref(p)), "tfhe_host_selftest")

@@ -1,0 +1,149 @@
+"""BinFHEContextHIP: the vector BinFHEContext surface (binfhecontext.cpp:316-365)
+over the C-ABI.  Ciphertexts are numpy uint64 arrays of shape [B, n+1]
+(a[0..n-1], b), keys are flat coefficient-form arrays (see include/tfhe_hip.h)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .capi import BINGATE, Info, Params, check, lib
+
+
+def _u64(x):
+    return np.ascontiguousarray(x, dtype=np.uint64)
+
+
+class BinFHEContextHIP:
+    BETA = 128  # BinFHEContext::GetBeta, binfhecontext.h:348-350
+
+    def __init__(self, params: Params):
+        self.params = params
+        self._h = C.c_void_p()
+
+    # -- GPUSetup / GPUClean (binfhecontext.cpp:349-365) --
+    def GPUSetup(self, bsk_coeff, ksk, num_gpus: int = 1):
+        if self._h:
+            self.GPUClean()
+        p = self.params
+        bsk = _u64(bsk_coeff).ravel()
+        kk = _u64(ksk).ravel()
+        if bsk.size != p.bsk_words() or kk.size != p.ksk_words():
+            raise ValueError("key sizes do not match the parameters")
+        check(lib().tfhe_setup(C.byref(self._h), C.byref(p), bsk, kk, num_gpus), "tfhe_setup")
+        return self
+
+    @classmethod
+    def from_key_image(cls, params: Params, d_src: int, nbytes: int, device: int = 0):
+        ctx = cls(params)
+        check(lib().tfhe_setup_from_key_image(C.byref(ctx._h), C.byref(params), C.c_void_p(d_src), nbytes, device),
+              "tfhe_setup_from_key_image")
+        return ctx
+
+    def export_key_image(self, d_dst: int, nbytes: int, stream: int = 0):
+        check(lib().tfhe_export_key_image(self._h, C.c_void_p(d_dst), nbytes, C.c_void_p(stream)),
+              "tfhe_export_key_image")
+
+    def GPUClean(self):
+        if self._h:
+            check(lib().tfhe_clean(self._h), "tfhe_clean")
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.GPUClean()
+        except Exception:
+            pass
+
+    def info(self) -> Info:
+        inf = Info()
+        check(lib().tfhe_get_info(self._h, C.byref(inf)), "tfhe_get_info")
+        return inf
+
+    @property
+    def handle(self):
+        return self._h
+
+    def GetBeta(self):
+        return self.BETA
+
+    def GetMaxPlaintextSpace(self):
+        return self.params.q // self.BETA // 2
+
+    # -- reference boundary calls --
+    def EvalAcc(self, a, a_mod, acc):
+        """EvalAcc_CUDA: a[B][n] mod a_mod, acc[B][2][N] -> new acc (acc0 transposed)."""
+        a = _u64(a)
+        out = np.array(acc, dtype=np.uint64, copy=True, order="C")
+        B = a.size // self.params.n
+        check(lib().tfhe_eval_acc(self._h, B, a.ravel(), a_mod, out.ravel()), "tfhe_eval_acc")
+        return out
+
+    def MKMSwitch(self, ct_ext, fmod):
+        ct_ext = _u64(ct_ext)
+        B = ct_ext.size // (self.params.N + 1)
+        out = np.empty((B, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_mkm_switch(self._h, B, ct_ext.ravel(), fmod, out.ravel()), "tfhe_mkm_switch")
+        return out
+
+    def CiphertextMulMatrix(self, ct, matrix, modulus):
+        ct = _u64(ct)
+        m = np.ascontiguousarray(matrix, dtype=np.int64)
+        K, cols = m.shape
+        out = np.empty((cols, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_ciphertext_mul_matrix(self._h, K, ct.ravel(), cols, m.ravel(), modulus, out.ravel()),
+              "tfhe_ciphertext_mul_matrix")
+        return out
+
+    # -- vector BinFHEContext surface --
+    def _batch(self, ct):
+        ct = _u64(ct)
+        if ct.ndim == 1:
+            ct = ct[None]
+        return ct, ct.shape[0]
+
+    def EvalBinGate(self, gate, ct1, ct2, q=None):
+        ct1, B = self._batch(ct1)
+        ct2, _ = self._batch(ct2)
+        g = BINGATE[gate] if isinstance(gate, str) else int(gate)
+        out = np.empty((B, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_eval_bin_gate(self._h, g, B, ct1.ravel(), ct2.ravel(), q or self.params.q, out.ravel()),
+              "tfhe_eval_bin_gate")
+        return out
+
+    def EvalFunc(self, ct, lut, q=None):
+        ct, B = self._batch(ct)
+        lut = _u64(lut)
+        out = np.empty((B, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_eval_func(self._h, B, ct.ravel(), q or self.params.q, lut.ravel(), int(lut.ndim == 2),
+                                   out.ravel()), "tfhe_eval_func")
+        return out
+
+    def EvalFloor(self, ct, mod, roundbits=0):
+        ct, B = self._batch(ct)
+        out = np.empty((B, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_eval_floor(self._h, B, ct.ravel(), mod, roundbits, out.ravel()), "tfhe_eval_floor")
+        return out
+
+    def EvalSign(self, ct, mod):
+        ct, B = self._batch(ct)
+        out = np.empty((B, self.params.n + 1), dtype=np.uint64)
+        check(lib().tfhe_eval_sign(self._h, B, ct.ravel(), mod, out.ravel()), "tfhe_eval_sign")
+        return out
+
+    def EvalDecomp(self, ct, mod, max_digits=16):
+        ct, B = self._batch(ct)
+        out = np.zeros((B, max_digits, self.params.n + 1), dtype=np.uint64)
+        moduli = np.zeros(max_digits, dtype=np.uint64)
+        nd = C.c_uint32()
+        check(lib().tfhe_eval_decomp(self._h, B, ct.ravel(), mod, max_digits, out.ravel(), moduli, C.byref(nd)),
+              "tfhe_eval_decomp")
+        d = nd.value
+        return out[:, :d, :], [int(m) for m in moduli[:d]]
+
+    # -- device-resident (pointers are integers, e.g. torch tensor.data_ptr()) --
+    def EvalBinGateDevice(self, gate, B, d_ct1, d_ct2, d_out, q=None, stream=0):
+        g = BINGATE[gate] if isinstance(gate, str) else int(gate)
+        check(lib().tfhe_eval_bin_gate_device(self._h, g, B, C.c_void_p(d_ct1), C.c_void_p(d_ct2),
+                                              q or self.params.q, C.c_void_p(d_out), C.c_void_p(stream)),
+              "tfhe_eval_bin_gate_device")
