@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""bench.py -- bootstraps/sec of the batched STD128 GINX bootstrap on MI355X.
+
+Workload (BASELINE.json configs[1]): STD128 (n=512, N=1024, Q=2^27-2^11+1,
+baseG=2^7) EvalBinGate(NAND), batch 8192 per GPU.  One step = one vector
+EvalBinGate call over the batch with both input vectors already resident in HBM:
+test vector -> blind rotation (n external products) -> extraction -> MKM, all on
+device (the fused tfhe_eval_bin_gate_device entry point).  One bootstrap per gate.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU; the key image is built once on rank 0 and broadcast over
+RCCL/xGMI (torch.distributed, backend "nccl" = RCCL), then every rank bootstraps
+its own 8192-ciphertext shard with no data-path collective (weak scaling).
+
+Extra JSON fields:
+  roofline      the blind-rotation kernel, timed alone with HIP events on its
+                stream; algorithmic bytes per SURVEY.md 8(d) (B_alg = BSK key
+                stream per bootstrap + KS gather + LWE I/O, no cross-ciphertext
+                reuse); traffic from rocprofv3 PMC if --pmc-json is given.
+  valu          the real bound: modular multiplies/s vs the measured gfx950
+                Shoup-modmul peak (profiles/r01_valu_rates.txt).
+  cpu_baseline  the C oracle (oracle/tfhe_oracle.c, OpenMP) on a bounded sample
+                of the same workload on this host's cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+
+MIB = 1 << 20
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
+MODMUL_PEAK = 7.66e12              # measured Shoup u32 modmul/s, profiles/r01_valu_rates.txt
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8192, help="ciphertexts per GPU")
+    ap.add_argument("--kernel-reps", type=int, default=2, help="blind-rotation launches timed for the roofline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_blind_rotate.json"))
+    return ap.parse_args()
+
+
+def synthetic_keys(p, seed=1):
+    """Uniform random BSK/KSK of the right shapes (throughput does not depend on key validity)."""
+    rs = np.random.default_rng(seed)
+    bsk = rs.integers(0, p.Q, p.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, p.qKS, p.ksk_words(), dtype=np.uint64)
+    return bsk, ksk
+
+
+def modmuls_per_bootstrap(p):
+    """n[(dG2+2)(N/2)log2N + 4 dG2 N + 4N]."""
+    logN = p.N.bit_length() - 1
+    return p.n * ((p.dG2 + 2) * (p.N // 2) * logN + 4 * p.dG2 * p.N + 4 * p.N)
+
+
+def b_alg_per_bootstrap(p):
+    """BSK packed (u32 if Q < 2^32) + KS gather (packed) + LWE I/O."""
+    wb = 4 if p.Q < (1 << 32) else 8
+    kb = 2 if p.qKS <= (1 << 16) else (4 if p.qKS <= (1 << 32) else 8)
+    bsk = p.n * 2 * p.dG2 * 2 * p.N * wb
+    ks = p.N * p.dKS * (p.n + 1) * kb
+    io = 3 * (p.n + 1) * 8
+    return bsk + ks + io, bsk
+
+
+def cpu_baseline(p, bsk, ksk, seconds):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    pyoracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    orc = pyoracle.Oracle(p_oracle(pyoracle, p), bsk, ksk, threads=threads)
+    rs = np.random.default_rng(5)
+    # calibrate on one gate per thread, then size the sample to ~`seconds`
+    B0 = threads
+    c1 = rs.integers(0, p.q, (B0, p.n + 1), dtype=np.uint64)
+    c2 = rs.integers(0, p.q, (B0, p.n + 1), dtype=np.uint64)
+    t0 = time.perf_counter()
+    orc.eval_bin_gate("NAND", c1, c2)
+    t_cal = time.perf_counter() - t0
+    reps = max(1, int(seconds / max(t_cal, 1e-3)))
+    B = B0 * reps
+    c1 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+    c2 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+    t0 = time.perf_counter()
+    orc.eval_bin_gate("NAND", c1, c2)
+    dt = time.perf_counter() - t0
+    orc.close()
+    return {"value": round(B / dt, 3), "unit": "bootstraps/s", "cores": threads, "kind": "port",
+            "sample": f"STD128 EvalBinGate(NAND) on {B} random ciphertext pairs, same synthetic keys; "
+                      f"oracle/tfhe_oracle.c (exact u128 CPU restatement, OpenMP one ciphertext per thread); "
+                      f"{dt:.1f} s"}
+
+
+def p_oracle(pyoracle, p):
+    return pyoracle.params_from_set("STD128")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import tfhe_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    p = tfhe_amd.params_from_set("STD128")
+    B = args.batch
+    # a dedicated (non-null) stream: the engine's kernels, torch's tensors and the
+    # HIP events below are all ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+
+    # ---- GPUSetup: rank 0 converts the keys, the image is broadcast over RCCL ----
+    t_setup = time.perf_counter()
+    bcast_ms = None
+    if rank == 0:
+        bsk, ksk = synthetic_keys(p)
+        ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+    else:
+        bsk = ksk = None
+    if world > 1:
+        nbytes = torch.tensor([ctx.info().key_image_bytes if rank == 0 else 0], dtype=torch.int64, device=dev)
+        dist.broadcast(nbytes, 0)
+        nbytes = int(nbytes.item())
+        img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            ctx.export_key_image(img.data_ptr(), nbytes, sptr)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.broadcast(img, 0)
+        torch.cuda.synchronize(dev)
+        bcast_ms = (time.perf_counter() - t0) * 1e3
+        if rank != 0:
+            ctx = tfhe_amd.BinFHEContextHIP.from_key_image(p, img.data_ptr(), nbytes, local)
+        del img
+    setup_s = time.perf_counter() - t_setup
+
+    # ---- inputs resident in HBM ----
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    ct1 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    ct2 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    out = torch.empty((B, p.n + 1), dtype=torch.int64, device=dev)
+
+    def step():
+        ctx.EvalBinGateDevice("NAND", B, ct1.data_ptr(), ct2.data_ptr(), out.data_ptr(), stream=sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_bs = B * args.steps * world
+    value = total_bs / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- dominant kernel (blind rotation) timed alone with HIP events on its stream ----
+    a = ct1[:, : p.n].contiguous()
+    acc = torch.zeros((B, 2, p.N), dtype=torch.int64, device=dev)
+    acc[:, 1, ::2] = int(p.Q // 8 + 1)
+    lib = tfhe_amd.lib()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sptr),
+                        "tfhe_eval_acc_device")
+    e0.record(stream)
+    for _ in range(args.kernel_reps):
+        tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sptr),
+                            "tfhe_eval_acc_device")
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    br_ms = e0.elapsed_time(e1) / args.kernel_reps
+    balg, bsk_bytes = b_alg_per_bootstrap(p)
+    achieved = balg * B / (br_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    mm = modmuls_per_bootstrap(p)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
+                "kernel": "blind_rotate (tfhe_eval_acc_device)", "kernel_ms": round(br_ms, 3),
+                "units_per_launch": B, "alg_bytes_per_unit": balg,
+                "note": "B_alg per SURVEY.md 8(d): key-stream bytes with no cross-ciphertext reuse; frac > 1 means "
+                        "the 64 MiB BSK is re-served from L2/MALL across the batch. The kernel is VALU-bound: "
+                        "see 'valu'."}
+    valu = {"modmul_per_bootstrap": mm, "achieved_modmul_per_s": round(mm * B / (br_ms * 1e-3), 1),
+            "peak_modmul_per_s": MODMUL_PEAK,
+            "frac": round(mm * B / (br_ms * 1e-3) / MODMUL_PEAK, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if bsk is None:
+            bsk, ksk = synthetic_keys(p)
+        cpu = cpu_baseline(p, bsk, ksk, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "bootstraps/sec (whole node), STD128 GINX batch=8192",
+            "value": round(value, 2), "unit": "bootstraps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "STD128 GINX EvalBinGate(NAND), inputs resident in HBM",
+                       "global_batch": B * world, "batch_per_gpu": B, "n": p.n, "N": p.N, "Q": p.Q,
+                       "dG2": p.dG2, "parallelism": f"shard{world}"},
+            "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+            "setup_s": round(setup_s, 2), "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2),
+            "key_image_bytes": int(ctx.info().key_image_bytes),
+        }
+        print(json.dumps(line), flush=True)
+    ctx.GPUClean()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV output for one kernel into per-launch HBM bytes.
+
+Usage: pmc_summary.py KERNEL_SUBSTRING FETCH_DIR WRITE_DIR OUT_JSON
+FETCH_SIZE/WRITE_SIZE are KiB (TCC_EA0_RDREQ/WRREQ based).  Per
+MI355X_MICROARCH.md 'HBM', gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide
+(16 B/lane) coalesced stream; other access widths are uncalibrated, so both the
+raw and the x2-corrected read figures are recorded.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def rows(d):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        out += list(csv.DictReader(open(f)))
+    return out
+
+
+def per_launch(rs, kname, counter):
+    vals = [float(r["Counter_Value"]) for r in rs if kname in r.get("Kernel_Name", "") and r["Counter_Name"] == counter]
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    kname, fdir, wdir, out = sys.argv[1:5]
+    fetch, nf = per_launch(rows(fdir), kname, "FETCH_SIZE")
+    write, nw = per_launch(rows(wdir), kname, "WRITE_SIZE")
+    res = {"kernel": kname, "launches": [nf, nw], "fetch_kib_raw": fetch, "write_kib": write}
+    if fetch is not None and write is not None:
+        res["hbm_bytes_per_launch_raw"] = (fetch + write) * 1024
+        res["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
+        res["correction"] = "read side x2 per MI355X_MICROARCH.md HBM section (wide-stream calibration)"
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
