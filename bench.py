@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=8192, help="ciphertexts per GPU")
     ap.add_argument("--kernel-reps", type=int, default=2, help="blind-rotation launches timed for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--generic", action="store_true", help="force the generic LDS blind-rotation kernel")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_blind_rotate.json"))
     return ap.parse_args()
@@ -112,6 +113,8 @@ def p_oracle(pyoracle, p):
 
 def main():
     args = parse()
+    if args.generic:
+        os.environ["TFHE_FORCE_GENERIC"] = "1"
     import torch
     import torch.distributed as dist
     import tfhe_amd

@@ -45,14 +45,21 @@ def test_gpu_reproduces_reference_kat(capi, oracle, name):
 
 
 # ---------------------------------------------------------------- boundary calls
-@pytest.fixture(scope="module")
-def std128(capi, oracle):
+@pytest.fixture(scope="module", params=["fast", "generic"])
+def std128(request, capi, oracle):
+    """STD128 with valid keys, on the specialised kernel (default) and on the
+    generic LDS kernel (TFHE_FORCE_GENERIC=1 at setup)."""
     op = oracle.params_from_set("STD128")
     rng = oracle.Rng(7)
     sk, bsk, ksk = oracle.keygen(op, rng)
     cp = capi.params_from_set("STD128")
-    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
-    yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng)
+    if request.param == "generic":
+        os.environ["TFHE_FORCE_GENERIC"] = "1"
+    try:
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    finally:
+        os.environ.pop("TFHE_FORCE_GENERIC", None)
+    yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng, path=request.param)
     ctx.GPUClean()
     orc.close()
 
@@ -64,7 +71,7 @@ def test_eval_acc_parity(std128):
     a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
     acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
     acc[0, 0, :] = 0  # a sparse test-vector-like accumulator too
-    for amod in (op.q, op.q // 2, 2 * op.N):
+    for amod in (op.q, op.q // 2, 2 * op.N, 4):
         g = ctx.EvalAcc(a % amod, amod, acc)
         c = orc.eval_acc(a % amod, amod, acc)
         assert np.array_equal(g, c), amod

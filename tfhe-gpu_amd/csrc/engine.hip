@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -144,7 +145,8 @@ tfhe_status init_derived(tfhe_ctx* c) {
     c->ks.dKS = p.dKS;
     c->ks.Q = p.Q;
     c->ks.qKS = p.qKS;
-    c->use_fast = fast_path_supported(c->br, c->word_bits);
+    const char* force = std::getenv("TFHE_FORCE_GENERIC");
+    c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
         return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
     if (p.baseKS > 256) return fail(TFHE_ERR_UNSUPPORTED, "baseKS > 256 not supported");
@@ -227,8 +229,7 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
     bind_tables(c, d);
     if (c->use_fast) {
         HCHECK(hipMalloc(&d.bsk_fast, bsk_fast_bytes(c->br)));
-        HCHECK(launch_pack_bsk_fast(c->br, d.arena + c->layout.bsk, d.arena + c->layout.bsk_sh, d.bsk_fast,
-                                    d.stream));
+        HCHECK(launch_pack_bsk_fast(c->br, d.tables, d.arena + c->layout.bsk, d.bsk_fast, d.stream));
         HCHECK(hipStreamSynchronize(d.stream));
     }
     return TFHE_OK;
@@ -272,7 +273,7 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
 tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B) {
     if (amod == 0 || (2ull * c->p.N) % amod != 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "a-modulus must divide 2N");
     const ArenaLayout& L = c->layout;
-    if (c->use_fast) {
+    if (c->use_fast && (amod & (amod - 1)) == 0) {
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,

@@ -38,8 +38,8 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
 hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables& T, const void* bsk_fast, const uint64_t* a,
                                     uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
 bool fast_path_supported(const BRParams& P, int word_bits);
-// Rearranges the generic device BSK (+companions) into the fast kernel's layout.
-hipError_t launch_pack_bsk_fast(const BRParams& P, const void* bsk, const void* bsk_sh, void* bsk_fast,
+// Converts the generic device BSK and tables into the fast kernel's Montgomery form.
+hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s);
 size_t bsk_fast_bytes(const BRParams& P);
 
