@@ -31,6 +31,8 @@
 //    stage and never reduce (digits enter < 2Q, outputs < 22Q < 2^32); inverse GS
 //    butterflies keep values < 2Q; the accumulator is reduced to [0, Q) once per
 //    round, which the next decomposition needs.
+#include <cstdlib>
+
 #include "device_math.hpp"
 #include "kernels.hpp"
 
@@ -47,7 +49,8 @@ constexpr int THREADS = TPC * CTS;
 
 // device table block (words): psiM[1024] ipsiM[1024] monoM[2048] eidx[1024]
 constexpr uint32_t T_PSI = 0, T_IPSI = 1024, T_MONO = 2048, T_EIDX = 4096, T_WORDS = 5120;
-constexpr uint32_t BUF_WORDS = 2 * FN;  // per ciphertext: two polynomials
+constexpr uint32_t PFN = FN + FN / 8;      // padded polynomial (swz)
+constexpr uint32_t BUF_WORDS = 2 * PFN;    // per ciphertext: two polynomials
 constexpr size_t LDS_BYTES = (size_t)(T_WORDS + CTS * BUF_WORDS) * 4;
 
 struct FastConst {
@@ -63,9 +66,10 @@ __device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t bM, const FastCons
 }
 __device__ __forceinline__ uint32_t csub32(uint32_t a, uint32_t m) { return min(a, a - m); }
 
-// LDS word index of natural index i: XOR swizzle that makes every layout's
-// 32-lane access pattern hit 32 distinct banks (L4: at most 2-way)
-__device__ __forceinline__ uint32_t swz(uint32_t i) { return i ^ (((i >> 5) & 7u) << 1) ^ (((i >> 7) & 1u) << 4); }
+// LDS word index of natural index i: 2 pad words per 16.  Affine in the register
+// index for all four layouts (address = base(lane) + immediate), and at most
+// 2-way bank conflicts per 32-lane group (exhaustive search, tools/ notes).
+__device__ __forceinline__ uint32_t swz(uint32_t i) { return i + 2 * (i >> 4); }
 
 __device__ __forceinline__ uint32_t ix1(uint32_t t, uint32_t r) { return r * 128 + t; }
 __device__ __forceinline__ uint32_t ix2(uint32_t t, uint32_t r) { return (t >> 4) * 128 + r * 16 + (t & 15); }
@@ -89,6 +93,15 @@ template <int L>
 __device__ __forceinline__ void lds_load(const uint32_t* buf, uint32_t (&x)[8], uint32_t t) {
 #pragma unroll
     for (uint32_t r = 0; r < 8; ++r) x[r] = buf[swz(ix<L>(t, r))];
+}
+
+// An opaque zero: adding it to a table base stops the compiler from hoisting the
+// (loop-invariant) twiddle loads out of the round loop into registers, which
+// would cost ~36 VGPRs for values one LDS read away.
+__device__ __forceinline__ uint32_t opaque_zero() {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
 }
 
 // ordering of LDS traffic between lanes of one wavefront
@@ -154,26 +167,26 @@ __device__ __forceinline__ void ntt_fwd2(uint32_t (&x0)[8], uint32_t (&x1)[8], u
     fwd_pass<true>(x1, psi, 1, 0, K);
     __syncthreads();  // the other wavefront has finished reading buf
     lds_store<1>(buf, x0, t);
-    lds_store<1>(buf + FN, x1, t);
+    lds_store<1>(buf + PFN, x1, t);
     __syncthreads();
     lds_load<2>(buf, x0, t);
-    lds_load<2>(buf + FN, x1, t);
+    lds_load<2>(buf + PFN, x1, t);
     fwd_pass<true>(x0, psi, 8, t >> 4, K);
     fwd_pass<true>(x1, psi, 8, t >> 4, K);
     wave_sync();
     lds_store<2>(buf, x0, t);
-    lds_store<2>(buf + FN, x1, t);
+    lds_store<2>(buf + PFN, x1, t);
     wave_sync();
     lds_load<3>(buf, x0, t);
-    lds_load<3>(buf + FN, x1, t);
+    lds_load<3>(buf + PFN, x1, t);
     fwd_pass<true>(x0, psi, 64, t >> 1, K);
     fwd_pass<true>(x1, psi, 64, t >> 1, K);
     wave_sync();
     lds_store<3>(buf, x0, t);
-    lds_store<3>(buf + FN, x1, t);
+    lds_store<3>(buf + PFN, x1, t);
     wave_sync();
     lds_load<4>(buf, x0, t);
-    lds_load<4>(buf + FN, x1, t);
+    lds_load<4>(buf + PFN, x1, t);
     fwd_pass<false>(x0, psi, 128, t, K);
     fwd_pass<false>(x1, psi, 128, t, K);
 }
@@ -185,31 +198,34 @@ __device__ __forceinline__ void ntt_inv2(uint32_t (&x0)[8], uint32_t (&x1)[8], u
     inv_pass<false>(x1, ipsi, 128, t, K);
     wave_sync();
     lds_store<4>(buf, x0, t);
-    lds_store<4>(buf + FN, x1, t);
+    lds_store<4>(buf + PFN, x1, t);
     wave_sync();
     lds_load<3>(buf, x0, t);
-    lds_load<3>(buf + FN, x1, t);
+    lds_load<3>(buf + PFN, x1, t);
     inv_pass<true>(x0, ipsi, 64, t >> 1, K);
     inv_pass<true>(x1, ipsi, 64, t >> 1, K);
     wave_sync();
     lds_store<3>(buf, x0, t);
-    lds_store<3>(buf + FN, x1, t);
+    lds_store<3>(buf + PFN, x1, t);
     wave_sync();
     lds_load<2>(buf, x0, t);
-    lds_load<2>(buf + FN, x1, t);
+    lds_load<2>(buf + PFN, x1, t);
     inv_pass<true>(x0, ipsi, 8, t >> 4, K);
     inv_pass<true>(x1, ipsi, 8, t >> 4, K);
     wave_sync();
     lds_store<2>(buf, x0, t);  // own half (b9 = wavefront)
-    lds_store<2>(buf + FN, x1, t);
+    lds_store<2>(buf + PFN, x1, t);
     __syncthreads();
     lds_load<1>(buf, x0, t);
-    lds_load<1>(buf + FN, x1, t);
+    lds_load<1>(buf + PFN, x1, t);
     inv_pass<true>(x0, ipsi, 1, 0, K);
     inv_pass<true>(x1, ipsi, 1, 0, K);
 }
 
-__global__ void __launch_bounds__(THREADS)
+// MINW: minimum waves per SIMD requested from the register allocator;
+// ACC32: reduce every digit pair into 32-bit accumulators (fewer VGPRs, +2 ops per term pair)
+template <int MINW, bool ACC32>
+__global__ void __launch_bounds__(THREADS, MINW)
 k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __restrict__ tabs,
                     const uint32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
                     uint32_t B) {
@@ -249,13 +265,17 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
 #pragma unroll
             for (int r = 0; r < 8; ++r) d[p][r] = acc[p][r] < K.Qhalf ? (int32_t)acc[p][r] : (int32_t)(acc[p][r] - K.Q);
 
-        uint64_t s[2][2][8];
+        uint64_t s[2][2][8];   // exact 64-bit sums (ACC32 = false)
+        uint32_t s32[2][2][8]; // per-pair reduced sums < 4 * 2.4Q (ACC32 = true)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 8; ++r) s[k][j][r] = 0;
+                for (int r = 0; r < 8; ++r) {
+                    if constexpr (ACC32) s32[k][j][r] = 0;
+                    else s[k][j][r] = 0;
+                }
 
         const uint32_t* ek = bsk + (size_t)i * (2 * FDG2 * 2 * FN) + t * 8;
 #pragma unroll 1
@@ -270,7 +290,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
                 x0[r] = (uint32_t)(r0 + (int32_t)K.Q);  // = r mod Q, in [Q-64, Q+64)
                 x1[r] = (uint32_t)(r1 + (int32_t)K.Q);
             }
-            ntt_fwd2(x0, x1, buf, psi, t, K);
+            ntt_fwd2(x0, x1, buf, psi + opaque_zero(), t, K);
             // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l)
 #pragma unroll
             for (int k = 0; k < 2; ++k)
@@ -278,11 +298,21 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
                 for (int j = 0; j < 2; ++j) {
                     const uint4* e0 = reinterpret_cast<const uint4*>(ek + ((k * FDG2 + 2 * l) * 2 + j) * FN);
                     const uint4* e1 = reinterpret_cast<const uint4*>(ek + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN);
+                    // one (key, poly) group of BSK words at a time: bounds the staging registers
+                    __builtin_amdgcn_sched_barrier(0);
                     const uint4 a0 = e0[0], a1 = e0[1], b0 = e1[0], b1 = e1[1];
                     const uint32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
                     const uint32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) s[k][j][r] += (uint64_t)x0[r] * w0[r] + (uint64_t)x1[r] * w1[r];
+                    for (int r = 0; r < 8; ++r) {
+                        if constexpr (ACC32) {
+                            const uint64_t T = (uint64_t)x0[r] * w0[r] + (uint64_t)x1[r] * w1[r];
+                            s32[k][j][r] += redc(T, K.Q, K.qinv);
+                        } else {  // two chained v_mad_u64_u32 into the exact sum
+                            s[k][j][r] = (uint64_t)x0[r] * w0[r] + s[k][j][r];
+                            s[k][j][r] = (uint64_t)x1[r] * w1[r] + s[k][j][r];
+                        }
+                    }
                 }
         }
 
@@ -293,12 +323,17 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
             const uint32_t ip = (eidx[t * 8 + r] * ai) & (2 * FN - 1);
             const uint32_t in = (2 * FN - ip) & (2 * FN - 1);
             const uint32_t mp = mono[ip], mn = mono[in];
-            const uint32_t A00 = redc(s[0][0][r], K.Q, K.qinv), A01 = redc(s[0][1][r], K.Q, K.qinv);
-            const uint32_t A10 = redc(s[1][0][r], K.Q, K.qinv), A11 = redc(s[1][1][r], K.Q, K.qinv);
+            uint32_t A00, A01, A10, A11;
+            if constexpr (ACC32) {
+                A00 = s32[0][0][r], A01 = s32[0][1][r], A10 = s32[1][0][r], A11 = s32[1][1][r];
+            } else {
+                A00 = redc(s[0][0][r], K.Q, K.qinv), A01 = redc(s[0][1][r], K.Q, K.qinv);
+                A10 = redc(s[1][0][r], K.Q, K.qinv), A11 = redc(s[1][1][r], K.Q, K.qinv);
+            }
             S0[r] = redc((uint64_t)A00 * mp + (uint64_t)A10 * mn, K.Q, K.qinv);
             S1[r] = redc((uint64_t)A01 * mp + (uint64_t)A11 * mn, K.Q, K.qinv);
         }
-        ntt_inv2(S0, S1, buf, ipsi, t, K);
+        ntt_inv2(S0, S1, buf, ipsi + opaque_zero(), t, K);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             acc[0][r] = csub32(csub32(acc[0][r] + S0[r], K.twoQ), K.Q);
@@ -364,7 +399,20 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     K.Qhalf = K.Q >> 1;
     const uint32_t* tabs = (const uint32_t*)bsk_fast;
     const uint32_t* bsk = tabs + T_WORDS;
-    auto k = k_blind_rotate_fast;
+    static const int variant = [] {
+        const char* e = std::getenv("TFHE_FAST_VARIANT");
+        return e ? std::atoi(e) : 0;
+    }();
+    // default: 3 waves/SIMD with per-pair 32-bit accumulation (fastest measured,
+    // tools/variant_sweep.sh: 68.6 ms vs 75.1 ms for <2,false> per 8192-batch)
+    auto k = k_blind_rotate_fast<3, true>;
+    switch (variant) {
+        case 1: k = k_blind_rotate_fast<3, false>; break;
+        case 5: k = k_blind_rotate_fast<2, false>; break;
+        case 3: k = k_blind_rotate_fast<4, true>; break;
+        case 4: k = k_blind_rotate_fast<2, true>; break;
+        default: break;
+    }
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
     hipLaunchKernelGGL(k, dim3((unsigned)((B + CTS - 1) / CTS)), dim3(THREADS), LDS_BYTES, s, K, P.n, loga, tabs,
                        bsk, a, acc, (uint32_t)B);
