@@ -63,8 +63,8 @@ int ksk_bits_for(uint64_t qKS) {
 // Byte offsets of everything inside the key arena; a pure function of the params,
 // so an importing process can locate the sections of a broadcast image.
 struct ArenaLayout {
-    size_t psi, psi_sh, ipsi, ipsi_sh, mono, mono_sh, eidx, bsk, bsk_sh, ksk, total;
-    size_t bsk_words, ksk_words;
+    size_t psi, psi_sh, ipsi, ipsi_sh, mono, mono_sh, eidx, bsk, bsk_sh, ksk, kskb, total;
+    size_t bsk_words, ksk_words, ksk_rows, n_pad;
 };
 
 ArenaLayout arena_layout(const tfhe_params& p, int word_bits) {
@@ -72,7 +72,10 @@ ArenaLayout arena_layout(const tfhe_params& p, int word_bits) {
     const size_t wb = word_bits / 8, N = p.N;
     const size_t kb = ksk_bits_for(p.qKS) / 8;
     L.bsk_words = (size_t)p.n * 2 * p.dG2 * 2 * N;
-    L.ksk_words = (size_t)N * p.baseKS * p.dKS * (p.n + 1);
+    L.ksk_rows = (size_t)N * p.baseKS * p.dKS;
+    const size_t vec = 16 / kb;  // KSK row padded to a multiple of 16 bytes
+    L.n_pad = (p.n + vec - 1) / vec * vec;
+    L.ksk_words = L.ksk_rows * (p.n + 1);  // caller's layout (B at index n)
     size_t o = 0;
     L.psi = o; o = align_up(o + N * wb);
     L.psi_sh = o; o = align_up(o + N * wb);
@@ -83,7 +86,8 @@ ArenaLayout arena_layout(const tfhe_params& p, int word_bits) {
     L.eidx = o; o = align_up(o + N * 4);
     L.bsk = o; o = align_up(o + L.bsk_words * wb);
     L.bsk_sh = o; o = align_up(o + L.bsk_words * wb);
-    L.ksk = o; o = align_up(o + L.ksk_words * kb);
+    L.ksk = o; o = align_up(o + L.ksk_rows * L.n_pad * kb);
+    L.kskb = o; o = align_up(o + L.ksk_rows * kb);
     L.total = o;
     return L;
 }
@@ -145,6 +149,7 @@ tfhe_status init_derived(tfhe_ctx* c) {
     c->ks.dKS = p.dKS;
     c->ks.Q = p.Q;
     c->ks.qKS = p.qKS;
+    c->ks.n_pad = (uint32_t)c->layout.n_pad;
     const char* force = std::getenv("TFHE_FORCE_GENERIC");
     c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
@@ -169,6 +174,23 @@ void fill_companions(std::vector<unsigned char>& host, size_t off, const uint64_
     const size_t blk = 1 << 14;
     parallel_for((count + blk - 1) / blk, [&](size_t b) {
         for (size_t i = b * blk; i < std::min(count, (b + 1) * blk); ++i) dst[i] = (W)shoup_companion(src[i], Q, bits);
+    });
+}
+
+// KSK [rows][n+1] -> A part [rows][n_pad] (zero padded) + B part [rows]
+template <typename W>
+void pack_ksk(std::vector<unsigned char>& img, const ArenaLayout& L, uint32_t n, const uint64_t* ksk) {
+    W* A = reinterpret_cast<W*>(img.data() + L.ksk);
+    W* Bp = reinterpret_cast<W*>(img.data() + L.kskb);
+    const size_t blk = 4096;
+    parallel_for((L.ksk_rows + blk - 1) / blk, [&](size_t b) {
+        for (size_t r = b * blk; r < std::min(L.ksk_rows, (b + 1) * blk); ++r) {
+            const uint64_t* src = ksk + r * (n + 1);
+            W* dst = A + r * L.n_pad;
+            for (uint32_t k = 0; k < n; ++k) dst[k] = (W)src[k];
+            for (size_t k = n; k < L.n_pad; ++k) dst[k] = 0;
+            Bp[r] = (W)src[n];
+        }
     });
 }
 
@@ -208,9 +230,9 @@ tfhe_status build_host_image(tfhe_ctx* c, const uint64_t* bsk_coeff, const uint6
             if (ksk[i] >= qks) bad = true;
     });
     if (bad) return fail(TFHE_ERR_INVALID_ARGUMENT, "KSK entry >= qKS");
-    if (c->ksk_bits == 16) fill_words<uint16_t>(img, L.ksk, ksk, L.ksk_words);
-    else if (c->ksk_bits == 32) fill_words<uint32_t>(img, L.ksk, ksk, L.ksk_words);
-    else fill_words<uint64_t>(img, L.ksk, ksk, L.ksk_words);
+    if (c->ksk_bits == 16) pack_ksk<uint16_t>(img, L, p.n, ksk);
+    else if (c->ksk_bits == 32) pack_ksk<uint32_t>(img, L, p.n, ksk);
+    else pack_ksk<uint64_t>(img, L, p.n, ksk);
     return TFHE_OK;
 }
 
@@ -285,7 +307,8 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
 
 tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
     if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
-    HCHECK(launch_mkm(c->ks, c->ksk_bits, d.arena + c->layout.ksk, ext, fmod, out, B, d.stream));
+    HCHECK(launch_mkm(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb, ext, fmod, out, B,
+                      d.stream));
     return TFHE_OK;
 }
 

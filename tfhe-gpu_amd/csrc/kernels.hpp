@@ -44,13 +44,15 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
 size_t bsk_fast_bytes(const BRParams& P);
 
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
-//   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.  ksk: [N][baseKS][dKS][n+1] in ksk_bits words.
+//   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.
+//   kska: [N][baseKS][dKS][n_pad] (A part, rows padded to 16 bytes), kskb: [N][baseKS][dKS] (B),
+//   both in ksk_bits words.
 struct KSParams {
-    uint32_t N, n, baseKS, dKS;
+    uint32_t N, n, baseKS, dKS, n_pad;
     uint64_t Q, qKS;
 };
-hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* ksk, const uint64_t* ext, uint64_t fmod,
-                      uint64_t* out, size_t B, hipStream_t s);
+hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
+                      uint64_t fmod, uint64_t* out, size_t B, hipStream_t s);
 
 // ---- test vectors, extraction and LWE glue (binfhe-base-scheme.cpp) ----
 enum TvMode : uint32_t {

@@ -11,88 +11,115 @@
 namespace tfhe {
 
 // ---------------------------------------------------------------------------
-// MKM.  Workgroup = MKM_CTS ciphertexts x MKM_COLS output coordinates.
-// Phase 1: every workgroup rounds its ciphertexts' N+1 words to qKS and stores
+// MKM.  One wavefront per ciphertext, four per workgroup.
+// Phase 1: the wavefront rounds its extract's N+1 words to qKS (RoundqQ) and keeps
 //          the base-baseKS digits of a'_i in LDS (u8: every baseKS <= 256).
-// Phase 2: thread k accumulates the gathered KSK rows' column k (coalesced:
-//          consecutive threads read consecutive words of one row), exact u64 sum,
-//          one reduction, then RoundqQ to fmod.
+// Phase 2: for each of the N*dKS gathered rows every lane loads 16 bytes of the
+//          row (VEC columns of the packed, 16-byte-padded KSK A part) and adds
+//          them into exact per-column sums; the B column lives in its own array
+//          and is accumulated wave-uniformly.  One reduction, then RoundqQ to fmod.
+// The gather is L2/MALL-bandwidth bound: STD128 reads N*dKS rows x 1 KiB per
+// ciphertext (SURVEY.md 8(d) "KS gather", 2 MiB u16).
 // ---------------------------------------------------------------------------
-constexpr int MKM_COLS = 256;
-constexpr int MKM_CTS = 4;
+constexpr int MKM_WAVES = 4;
+
+template <typename KW> struct MkmAcc { using T = uint64_t; };
+template <> struct MkmAcc<uint16_t> { using T = uint32_t; };  // N*dKS*2^16 < 2^32
 
 template <typename KW>
-__global__ void __launch_bounds__(MKM_COLS)
-k_mkm(KSParams P, const KW* __restrict__ ksk, const uint64_t* __restrict__ ext, uint64_t fmod,
-      uint64_t* __restrict__ out, size_t B) {
+__global__ void __launch_bounds__(64 * MKM_WAVES)
+k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, const uint64_t* __restrict__ ext,
+      uint64_t fmod, uint64_t* __restrict__ out, size_t B) {
+    constexpr uint32_t VEC = 16 / sizeof(KW);
+    using Acc = typename MkmAcc<KW>::T;
     extern __shared__ __align__(16) unsigned char smem[];
-    const uint32_t N = P.N, n = P.n, dks = P.dKS, bks = P.baseKS, tid = threadIdx.x;
-    uint8_t* dig = smem;                                          // [MKM_CTS][N][dKS]
-    uint64_t* bq = reinterpret_cast<uint64_t*>(smem + ((size_t)MKM_CTS * N * dks + 15) / 16 * 16);  // [MKM_CTS]
-    const size_t ct0 = (size_t)blockIdx.x * MKM_CTS;
-    const uint32_t ncts = (uint32_t)min((size_t)MKM_CTS, B - ct0);
+    const uint32_t N = P.N, n = P.n, dks = P.dKS, bks = P.baseKS, npad = P.n_pad;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const size_t ct = (size_t)blockIdx.x * MKM_WAVES + w;
+    if (ct >= B) return;  // whole wavefront; no workgroup barrier below
+    uint8_t* dig = smem + (size_t)w * N * dks;
+    const uint64_t* e = ext + ct * (N + 1);
 
-    for (uint32_t c = 0; c < ncts; ++c) {
-        const uint64_t* e = ext + (ct0 + c) * (N + 1);
-        for (uint32_t i = tid; i <= N; i += blockDim.x) {
-            uint64_t x = round_qQ(e[i], P.qKS, P.Q);
-            if (i == N) {
-                bq[c] = x;
-            } else {
-                uint8_t* d = dig + ((size_t)c * N + i) * dks;
-                for (uint32_t j = 0; j < dks; ++j, x /= bks) d[j] = (uint8_t)(x % bks);
-            }
+    uint64_t bq = 0;
+    for (uint32_t i = lane; i <= N; i += 64) {
+        uint64_t x = round_qQ(e[i], P.qKS, P.Q);
+        if (i == N) {
+            bq = x;
+        } else {
+            for (uint32_t j = 0; j < dks; ++j, x /= bks) dig[(size_t)i * dks + j] = (uint8_t)(x % bks);
         }
     }
-    __syncthreads();
+    bq = __shfl(bq, (int)(N & 63));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
-    const uint32_t k = blockIdx.y * MKM_COLS + tid;
-    if (k > n) return;
-    const size_t row_stride = (size_t)n + 1;
-    for (uint32_t c = 0; c < ncts; ++c) {
-        const uint8_t* d = dig + (size_t)c * N * dks;
-        uint64_t sum = 0;
+    const uint64_t qks = P.qKS;
+    uint64_t* o = out + ct * (size_t)(n + 1);
+    uint64_t bsum = 0;
+    for (uint32_t c0 = 0; c0 < npad; c0 += 64 * VEC) {
+        const uint32_t col = c0 + lane * VEC;
+        const bool on = col < npad;
+        Acc acc[VEC];
+#pragma unroll
+        for (uint32_t v = 0; v < VEC; ++v) acc[v] = 0;
+        const KW* base = kska + (on ? col : 0);
 #pragma unroll 4
         for (uint32_t i = 0; i < N; ++i) {
             for (uint32_t j = 0; j < dks; ++j) {
-                const uint32_t a0 = d[(size_t)i * dks + j];
-                sum += (uint64_t)ksk[(((size_t)i * bks + a0) * dks + j) * row_stride + k];
+                const uint32_t a0 = dig[(size_t)i * dks + j];
+                const size_t row = ((size_t)i * bks + a0) * dks + j;
+                if (on) {
+                    const uint4 u = *reinterpret_cast<const uint4*>(base + row * npad);
+                    const KW* vals = reinterpret_cast<const KW*>(&u);
+#pragma unroll
+                    for (uint32_t v = 0; v < VEC; ++v) acc[v] += (Acc)vals[v];
+                }
+                if (c0 == 0) bsum += (uint64_t)kskb[row];
             }
         }
-        const uint64_t qks = P.qKS;
-        const uint64_t s = sum % qks;
-        uint64_t v;
-        if (k == n) v = bq[c] >= s ? bq[c] - s : bq[c] + (qks - s);  // b - sum
-        else v = s == 0 ? 0 : qks - s;                              // 0 - sum
-        out[(ct0 + c) * row_stride + k] = round_qQ(v, fmod, qks);
+#pragma unroll
+        for (uint32_t v = 0; v < VEC; ++v) {
+            const uint32_t k = col + v;
+            if (on && k < n) {
+                const uint64_t r = (uint64_t)acc[v] % qks;
+                o[k] = round_qQ(r == 0 ? 0 : qks - r, fmod, qks);  // 0 - sum
+            }
+        }
+    }
+    if (lane == 0) {
+        const uint64_t r = bsum % qks;
+        o[n] = round_qQ(bq >= r ? bq - r : bq + (qks - r), fmod, qks);  // b - sum
     }
 }
 
-hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* ksk, const uint64_t* ext, uint64_t fmod,
-                      uint64_t* out, size_t B, hipStream_t s) {
+hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
+                      uint64_t fmod, uint64_t* out, size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
     if (P.baseKS > 256) return hipErrorNotSupported;
-    const size_t lds = ((size_t)MKM_CTS * P.N * P.dKS + 15) / 16 * 16 + MKM_CTS * sizeof(uint64_t);
+    const size_t lds = (size_t)MKM_WAVES * P.N * P.dKS;
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    dim3 grid((unsigned)((B + MKM_CTS - 1) / MKM_CTS), (unsigned)((P.n + 1 + MKM_COLS - 1) / MKM_COLS));
-    dim3 block(MKM_COLS);
+    dim3 grid((unsigned)((B + MKM_WAVES - 1) / MKM_WAVES)), block(64 * MKM_WAVES);
     switch (ksk_bits) {
         case 16: {
             auto k = k_mkm<uint16_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint16_t*)ksk, ext, fmod, out, B);
+            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint16_t*)kska, (const uint16_t*)kskb, ext, fmod, out,
+                               B);
             break;
         }
         case 32: {
             auto k = k_mkm<uint32_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint32_t*)ksk, ext, fmod, out, B);
+            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint32_t*)kska, (const uint32_t*)kskb, ext, fmod, out,
+                               B);
             break;
         }
         default: {
             auto k = k_mkm<uint64_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint64_t*)ksk, ext, fmod, out, B);
+            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint64_t*)kska, (const uint64_t*)kskb, ext, fmod, out,
+                               B);
             break;
         }
     }
