@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=2, help="blind-rotation launches timed for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--generic", action="store_true", help="force the generic LDS blind-rotation kernel")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend ('nccl' = RCCL; 'gloo' only to rehearse N ranks on fewer GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_blind_rotate.json"))
     return ap.parse_args()
@@ -118,16 +120,21 @@ def main():
     import torch
     import torch.distributed as dist
     import tfhe_amd
+    from tfhe_amd import dist as tdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    local_dev = local % max(1, torch.cuda.device_count())  # == local on a full node
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     p = tfhe_amd.params_from_set("STD128")
     B = args.batch
@@ -146,20 +153,20 @@ def main():
     else:
         bsk = ksk = None
     if world > 1:
-        nbytes = torch.tensor([ctx.info().key_image_bytes if rank == 0 else 0], dtype=torch.int64, device=dev)
-        dist.broadcast(nbytes, 0)
-        nbytes = int(nbytes.item())
-        img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        # one RCCL broadcast of the packed device key image over xGMI (tfhe_amd/dist.py)
+        img = None
+        nbytes = ctx.info().key_image_bytes if rank == 0 else None
         if rank == 0:
+            img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
             ctx.export_key_image(img.data_ptr(), nbytes, sptr)
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
-        dist.broadcast(img, 0)
+        img = tdist.broadcast_key_image(img, nbytes, dev)
         torch.cuda.synchronize(dev)
         bcast_ms = (time.perf_counter() - t0) * 1e3
         if rank != 0:
-            ctx = tfhe_amd.BinFHEContextHIP.from_key_image(p, img.data_ptr(), nbytes, local)
+            ctx = tfhe_amd.BinFHEContextHIP.from_key_image(p, img.data_ptr(), img.numel(), local_dev)
         del img
     setup_s = time.perf_counter() - t_setup
 
@@ -188,9 +195,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = tdist.max_over_ranks(elapsed, dev)
     total_bs = B * args.steps * world
     value = total_bs / elapsed
     ms_per_step = elapsed / args.steps * 1e3

@@ -1,0 +1,90 @@
+"""World-size-2 torch.distributed (gloo, CPU) tests of the multi-rank path:
+contiguous sharding, the key-image broadcast, max-over-ranks timing, and an
+end-to-end sharded batch (each rank bootstraps its shard with the CPU oracle,
+standing in for its GPU) that must equal the unsharded result."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tfhe_amd import dist as tdist
+    import pyoracle
+
+    dev = torch.device("cpu")
+    # 1) key image broadcast (stand-in bytes of a real image size)
+    nbytes = 4096 + 17
+    img = None
+    if rank == 0:
+        g = torch.Generator().manual_seed(7)
+        img = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g)
+    got = tdist.broadcast_key_image(img, nbytes if rank == 0 else None, dev)
+    torch.save(got, os.path.join(outdir, f"img{rank}.pt"))
+    # 2) max over ranks
+    m = tdist.max_over_ranks(1.5 + rank, dev)
+    # 3) sharded batch: TOY keys from a shared seed, NAND over B=5 pairs
+    p = pyoracle.params_from_set("TOY")
+    rng = pyoracle.Rng(99)
+    sk, bsk, ksk = pyoracle.keygen(p, rng)
+    B = 5
+    c1 = np.stack([pyoracle.encrypt(p, rng, sk, i % 2, 4, p.q) for i in range(B)])
+    c2 = np.stack([pyoracle.encrypt(p, rng, sk, (i // 2) % 2, 4, p.q) for i in range(B)])
+    lo, hi = tdist.shard_range(B, world, rank)
+    orc = pyoracle.Oracle(p, bsk, ksk, threads=1)
+    part = orc.eval_bin_gate("NAND", c1[lo:hi], c2[lo:hi]) if hi > lo else np.zeros((0, p.n + 1), np.uint64)
+    parts = [None] * world
+    dist.all_gather_object(parts, (lo, hi, part))
+    total = tdist.sum_over_ranks(hi - lo, dev)
+    if rank == 0:
+        full = np.concatenate([x[2] for x in sorted(parts, key=lambda t: t[0])])
+        ref = orc.eval_bin_gate("NAND", c1, c2)
+        np.save(os.path.join(outdir, "sharded.npy"), full)
+        np.save(os.path.join(outdir, "ref.npy"), ref)
+        with open(os.path.join(outdir, "meta.txt"), "w") as f:
+            f.write(f"{m} {total}\n")
+    orc.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_covers_exactly():
+    sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+    from tfhe_amd.dist import shard_range
+
+    for total in (0, 1, 7, 8192, 65536, 65537):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            for a, b in zip(spans, spans[1:]):
+                assert a[1] == b[0]
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_gloo_world2_broadcast_and_sharded_batch(tmp_path, oracle):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    a = torch.load(tmp_path / "img0.pt")
+    b = torch.load(tmp_path / "img1.pt")
+    assert torch.equal(a, b) and a.numel() == 4096 + 17
+    m, total = open(tmp_path / "meta.txt").read().split()
+    assert float(m) == 2.5 and int(total) == 5
+    assert np.array_equal(np.load(tmp_path / "sharded.npy"), np.load(tmp_path / "ref.npy"))

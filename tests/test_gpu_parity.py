@@ -190,3 +190,41 @@ def test_full_batch_nand_decrypts(std128, oracle):
     assert np.array_equal(dec, 1 - (m1 & m2))
     idx = [0, 1, 4095, 8191]
     assert np.array_equal(out[idx], orc.eval_bin_gate("NAND", c1[idx], c2[idx]))
+
+
+def test_key_image_export_import_roundtrip(std128, capi):
+    """tfhe_export_key_image -> device buffer -> tfhe_setup_from_key_image (the
+    one-process-per-GPU replication path used with RCCL broadcast) yields an
+    identical engine."""
+    import torch
+
+    ctx, cp = std128["ctx"], std128["cp"]
+    nbytes = ctx.info().key_image_bytes
+    img = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    ctx.export_key_image(img.data_ptr(), nbytes)
+    torch.cuda.synchronize()
+    ctx2 = capi.BinFHEContextHIP.from_key_image(cp, img.data_ptr(), nbytes, 0)
+    rs = np.random.default_rng(11)
+    c1 = random_cts(rs, 6, cp.n, cp.q)
+    c2 = random_cts(rs, 6, cp.n, cp.q)
+    assert np.array_equal(ctx.EvalBinGate("XOR", c1, c2), ctx2.EvalBinGate("XOR", c1, c2))
+    with pytest.raises(capi.TfheError):
+        capi.BinFHEContextHIP.from_key_image(cp, img.data_ptr(), nbytes - 1, 0)
+    ctx2.GPUClean()
+
+
+def test_device_gate_entry_matches_host_entry(std128):
+    """tfhe_eval_bin_gate_device (bench path, HBM-resident inputs) == host-array entry."""
+    import torch
+
+    ctx, cp = std128["ctx"], std128["cp"]
+    rs = np.random.default_rng(12)
+    c1 = random_cts(rs, 10, cp.n, cp.q)
+    c2 = random_cts(rs, 10, cp.n, cp.q)
+    d1 = torch.from_numpy(c1.astype(np.int64)).cuda()
+    d2 = torch.from_numpy(c2.astype(np.int64)).cuda()
+    do = torch.empty_like(d1)
+    s = torch.cuda.Stream()
+    ctx.EvalBinGateDevice("NAND", 10, d1.data_ptr(), d2.data_ptr(), do.data_ptr(), stream=s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(do.cpu().numpy().astype(np.uint64), ctx.EvalBinGate("NAND", c1, c2))

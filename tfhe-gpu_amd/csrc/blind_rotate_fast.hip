@@ -223,8 +223,10 @@ __device__ __forceinline__ void ntt_inv2(uint32_t (&x0)[8], uint32_t (&x1)[8], u
 }
 
 // MINW: minimum waves per SIMD requested from the register allocator;
-// ACC32: reduce every digit pair into 32-bit accumulators (fewer VGPRs, +2 ops per term pair)
-template <int MINW, bool ACC32>
+// ACC32: reduce every digit pair into 32-bit accumulators (fewer VGPRs, +2 ops per term pair);
+// RECOMP: recompute digit l from the accumulator in pass l instead of carrying the
+//         16-register decomposition state (fewer VGPRs, +3 ops per extra digit step)
+template <int MINW, bool ACC32, bool RECOMP = false>
 __global__ void __launch_bounds__(THREADS, MINW)
 k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __restrict__ tabs,
                     const uint32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -260,10 +262,13 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
         const uint32_t ai = ((amask + 1 - ar) & amask) << ashift;
 
         int32_t d[2][8];  // centred coefficients, consumed digit by digit (rgsw-acc.cpp:83-109)
+        if constexpr (!RECOMP) {
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+            for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int r = 0; r < 8; ++r) d[p][r] = acc[p][r] < K.Qhalf ? (int32_t)acc[p][r] : (int32_t)(acc[p][r] - K.Q);
+                for (int r = 0; r < 8; ++r)
+                    d[p][r] = acc[p][r] < K.Qhalf ? (int32_t)acc[p][r] : (int32_t)(acc[p][r] - K.Q);
+        }
 
         uint64_t s[2][2][8];   // exact 64-bit sums (ACC32 = false)
         uint32_t s32[2][2][8]; // per-pair reduced sums < 4 * 2.4Q (ACC32 = true)
@@ -277,18 +282,34 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
                     else s[k][j][r] = 0;
                 }
 
-        const uint32_t* ek = bsk + (size_t)i * (2 * FDG2 * 2 * FN) + t * 8;
+        // wave-uniform round base (SGPRs) + 32-bit lane offset: global_load_dwordx4 v, voff, s[base]
+        const uint32_t* ek = bsk + (size_t)i * (2 * FDG2 * 2 * FN);
+        const uint32_t toff = t * 8;
 #pragma unroll 1
         for (uint32_t l = 0; l < FDIG; ++l) {
             uint32_t x0[8], x1[8];
+            if constexpr (RECOMP) {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int32_t r0 = (d[0][r] << (32 - FLOGG)) >> (32 - FLOGG);  // signed low digit
-                const int32_t r1 = (d[1][r] << (32 - FLOGG)) >> (32 - FLOGG);
-                d[0][r] = (d[0][r] - r0) >> FLOGG;
-                d[1][r] = (d[1][r] - r1) >> FLOGG;
-                x0[r] = (uint32_t)(r0 + (int32_t)K.Q);  // = r mod Q, in [Q-64, Q+64)
-                x1[r] = (uint32_t)(r1 + (int32_t)K.Q);
+                for (int r = 0; r < 8; ++r) {
+                    int32_t e0 = acc[0][r] < K.Qhalf ? (int32_t)acc[0][r] : (int32_t)(acc[0][r] - K.Q);
+                    int32_t e1 = acc[1][r] < K.Qhalf ? (int32_t)acc[1][r] : (int32_t)(acc[1][r] - K.Q);
+                    for (uint32_t z = 0; z < l; ++z) {  // drop the l lower digits (carries included)
+                        e0 = (e0 - ((e0 << (32 - FLOGG)) >> (32 - FLOGG))) >> FLOGG;
+                        e1 = (e1 - ((e1 << (32 - FLOGG)) >> (32 - FLOGG))) >> FLOGG;
+                    }
+                    x0[r] = (uint32_t)(((e0 << (32 - FLOGG)) >> (32 - FLOGG)) + (int32_t)K.Q);
+                    x1[r] = (uint32_t)(((e1 << (32 - FLOGG)) >> (32 - FLOGG)) + (int32_t)K.Q);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int32_t r0 = (d[0][r] << (32 - FLOGG)) >> (32 - FLOGG);  // signed low digit
+                    const int32_t r1 = (d[1][r] << (32 - FLOGG)) >> (32 - FLOGG);
+                    d[0][r] = (d[0][r] - r0) >> FLOGG;
+                    d[1][r] = (d[1][r] - r1) >> FLOGG;
+                    x0[r] = (uint32_t)(r0 + (int32_t)K.Q);  // = r mod Q, in [Q-64, Q+64)
+                    x1[r] = (uint32_t)(r1 + (int32_t)K.Q);
+                }
             }
             ntt_fwd2(x0, x1, buf, psi + opaque_zero(), t, K);
             // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l)
@@ -296,8 +317,10 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
             for (int k = 0; k < 2; ++k)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const uint4* e0 = reinterpret_cast<const uint4*>(ek + ((k * FDG2 + 2 * l) * 2 + j) * FN);
-                    const uint4* e1 = reinterpret_cast<const uint4*>(ek + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN);
+                    const uint32_t* r0p = ek + ((k * FDG2 + 2 * l) * 2 + j) * FN;      // uniform
+                    const uint32_t* r1p = ek + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN;  // uniform
+                    const uint4* e0 = reinterpret_cast<const uint4*>(r0p + toff);
+                    const uint4* e1 = reinterpret_cast<const uint4*>(r1p + toff);
                     // one (key, poly) group of BSK words at a time: bounds the staging registers
                     __builtin_amdgcn_sched_barrier(0);
                     const uint4 a0 = e0[0], a1 = e0[1], b0 = e1[0], b1 = e1[1];
@@ -411,6 +434,8 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 5: k = k_blind_rotate_fast<2, false>; break;
         case 3: k = k_blind_rotate_fast<4, true>; break;
         case 4: k = k_blind_rotate_fast<2, true>; break;
+        case 6: k = k_blind_rotate_fast<4, true, true>; break;
+        case 7: k = k_blind_rotate_fast<3, true, true>; break;
         default: break;
     }
     hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);

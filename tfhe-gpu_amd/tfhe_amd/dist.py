@@ -1,0 +1,56 @@
+"""Multi-GPU helpers: one process per GPU over torch.distributed.
+
+The bootstrap path shards with no exchange step (independent ciphertexts,
+SURVEY.md 8(e)), so the only collectives are at setup and for timing:
+
+* ``broadcast_key_image``: rank 0's packed device key image (NTT-domain BSK,
+  packed KSK, tables; ``tfhe_export_key_image``) is broadcast once.  With the
+  "nccl" backend (RCCL on ROCm) this moves device memory over xGMI; the reference
+  instead replicates keys host-to-device per GPU (bootstrapping.cu:1005-1069).
+* ``shard_range``: contiguous shards [g*B/G, (g+1)*B/G) (the reference deals
+  SM_count-sized chunks round-robin, bootstrapping.cu:1617).
+* ``max_over_ranks``: the bench's whole-job time is the slowest rank's.
+
+Everything here is backend-agnostic and is exercised on CPU with gloo
+(tests/test_dist_gloo.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) of `total` units for `rank` of `world` (sizes differ by <= 1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    base, extra = divmod(total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def broadcast_key_image(image: torch.Tensor | None, nbytes: int | None, device, src: int = 0) -> torch.Tensor:
+    """Broadcast a uint8 key image from `src`.  On src pass the filled tensor; elsewhere
+    pass None (its size is broadcast first).  Returns the tensor holding the image."""
+    rank = dist.get_rank()
+    size = torch.tensor([nbytes if rank == src else 0], dtype=torch.int64, device=device)
+    dist.broadcast(size, src)
+    n = int(size.item())
+    if rank != src:
+        image = torch.empty(n, dtype=torch.uint8, device=device)
+    elif image is None or image.numel() != n or image.dtype != torch.uint8:
+        raise ValueError("source rank must pass a uint8 image of nbytes")
+    dist.broadcast(image, src)
+    return image
+
+
+def max_over_ranks(x: float, device) -> float:
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: int, device) -> int:
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
