@@ -19,18 +19,25 @@
 //    8 consecutive NTT slots, so every BSK read is two 16-byte loads.  INTT:
 //    L4 -> L1, so the accumulator never leaves registers in coefficient order.
 //
-//  * Montgomery arithmetic (R = 2^32) through v_mad_u64_u32, which gfx950 issues
-//    at the rate of v_mul_lo_u32 (profiles/r01_valu_rates.txt):
-//        redc(T) = hi32(m*Q + T),  m = lo32(T) * (-Q^-1)        (T < 2^62)
-//    A twiddle product is 3 instructions and needs no Shoup companion, so the
-//    BSK is stored once (u32, Montgomery form, pre-scaled by N^-1).  The 8-row
-//    external product accumulates exact 64-bit sums (one v_mad_u64_u32 per term)
-//    and reduces once per output.
+//  * Signed Montgomery arithmetic (R = 2^32) on v_mad_i64_i32, which gfx950 issues
+//    at the rate of v_mul_lo_u32 (profiles/r01_valu_rates.txt).  Every value is a
+//    signed 32-bit representative; constants (twiddles, BSK, monomials) are stored
+//    centred (|w| <= Q/2) in Montgomery form:
+//        sredc(T) = hi32(T - m*Q),  m = lo32(T) * Q^-1   (one v_mul_lo + one v_mad_i64_i32)
+//    |sredc(T)| <= |T|/2^32 + Q/2.  A twiddle product is 3 instructions, a CT
+//    butterfly 5 (no "+2Q" offsets, no conditional subtractions), a GS butterfly 5.
+//    Value bounds (tools/bounds_fast.py checks them): forward outputs < 6.3Q + 64;
+//    inverse passes keep everything < 16Q by reducing the two a-paths that would
+//    double a third time; every 64-bit sum stays < 2^60.
 //
-//  * Lazy ranges (Q < 2^27): forward CT butterflies grow values by < 2Q per
-//    stage and never reduce (digits enter < 2Q, outputs < 22Q < 2^32); inverse GS
-//    butterflies keep values < 2Q; the accumulator is reduced to [0, Q) once per
-//    round, which the next decomposition needs.
+//  * The accumulator is kept as the centred canonical representative in
+//    [-(Q>>1)-1, Q>>1), exactly OpenFHE's signed view before its digit
+//    decomposition (rgsw-acc.cpp:83-109), so a digit is one v_bfe_i32 and the carry
+//    two instructions; the top digit is the remainder itself.
+//
+//  * Monomials: NTT(X^m - 1)[x] = psi^(e_x m) - 1 with e_x = 2 bitrev(x) + 1
+//    (checked at setup), so in L4 e = 256 bitrev3(r) + (2 bitrev7(t) + 1): one
+//    per-lane product per round plus a wave-uniform stride, and one 2N-entry table.
 #include <cstdlib>
 
 #include "device_math.hpp"
@@ -44,31 +51,35 @@ constexpr uint32_t FDG2 = 8;
 constexpr uint32_t FDIG = 4;
 constexpr uint32_t FLOGG = 7;
 constexpr int TPC = 128;  // threads per ciphertext
-constexpr int CTS = 2;    // ciphertexts per workgroup
-constexpr int THREADS = TPC * CTS;
 
-// device table block (words): psiM[1024] ipsiM[1024] monoM[2048] eidx[1024]
-constexpr uint32_t T_PSI = 0, T_IPSI = 1024, T_MONO = 2048, T_EIDX = 4096, T_WORDS = 5120;
+// device table block (int32 words, centred Montgomery): psi[1024] ipsi[1024] mono[2048]
+constexpr uint32_t T_PSI = 0, T_IPSI = 1024, T_MONO = 2048, T_WORDS = 4096;
 constexpr uint32_t PFN = FN + FN / 8;      // padded polynomial (swz)
 constexpr uint32_t BUF_WORDS = 2 * PFN;    // per ciphertext: two polynomials
-constexpr size_t LDS_BYTES = (size_t)(T_WORDS + CTS * BUF_WORDS) * 4;
+constexpr size_t lds_bytes(int cts) { return (size_t)(T_WORDS + cts * BUF_WORDS) * 4; }
 
 struct FastConst {
-    uint32_t Q, qinv, twoQ, Qhalf;
+    int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x
+    uint32_t Q2, Q4, h1, kacc;  // 2Q, 4Q, (Q>>1)+1, (Q>>1)+1+4Q
 };
 
-__device__ __forceinline__ uint32_t redc(uint64_t T, uint32_t Q, uint32_t qinv) {
-    const uint32_t m = (uint32_t)T * qinv;
-    return (uint32_t)(((uint64_t)m * Q + T) >> 32);
+__device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
+    const int32_t m = (int32_t)((uint32_t)T * (uint32_t)K.qinv);
+    return (int32_t)(((int64_t)m * K.nQ + T) >> 32);
 }
-__device__ __forceinline__ uint32_t mmul(uint32_t a, uint32_t bM, const FastConst& K) {
-    return redc((uint64_t)a * bM, K.Q, K.qinv);
+__device__ __forceinline__ int32_t smul(int32_t a, int32_t wM, const FastConst& K) {
+    return sredc((int64_t)a * wM, K);
 }
 __device__ __forceinline__ uint32_t csub32(uint32_t a, uint32_t m) { return min(a, a - m); }
 
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i ld_bsk(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+
 // LDS word index of natural index i: 2 pad words per 16.  Affine in the register
 // index for all four layouts (address = base(lane) + immediate), and at most
-// 2-way bank conflicts per 32-lane group (exhaustive search, tools/ notes).
+// 2-way bank conflicts per 32-lane group.
 __device__ __forceinline__ uint32_t swz(uint32_t i) { return i + 2 * (i >> 4); }
 
 __device__ __forceinline__ uint32_t ix1(uint32_t t, uint32_t r) { return r * 128 + t; }
@@ -85,19 +96,18 @@ __device__ __forceinline__ uint32_t ix(uint32_t t, uint32_t r) {
 }
 
 template <int L>
-__device__ __forceinline__ void lds_store(uint32_t* buf, const uint32_t (&x)[8], uint32_t t) {
+__device__ __forceinline__ void lds_store(int32_t* buf, const int32_t (&x)[8], uint32_t t) {
 #pragma unroll
     for (uint32_t r = 0; r < 8; ++r) buf[swz(ix<L>(t, r))] = x[r];
 }
 template <int L>
-__device__ __forceinline__ void lds_load(const uint32_t* buf, uint32_t (&x)[8], uint32_t t) {
+__device__ __forceinline__ void lds_load(const int32_t* buf, int32_t (&x)[8], uint32_t t) {
 #pragma unroll
     for (uint32_t r = 0; r < 8; ++r) x[r] = buf[swz(ix<L>(t, r))];
 }
 
 // An opaque zero: adding it to a table base stops the compiler from hoisting the
-// (loop-invariant) twiddle loads out of the round loop into registers, which
-// would cost ~36 VGPRs for values one LDS read away.
+// (loop-invariant) twiddle loads out of the round loop into registers.
 __device__ __forceinline__ uint32_t opaque_zero() {
     uint32_t z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
@@ -111,29 +121,32 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ __forceinline__ void bfly_ct(uint32_t& a, uint32_t& b, uint32_t w, const FastConst& K) {
-    const uint32_t v = mmul(b, w, K), u = a;
+// Cooley-Tukey: (a, b) -> (a + wb, a - wb);  |out| <= |a| + |b||w|/2^32 + Q/2
+__device__ __forceinline__ void bfly_ct(int32_t& a, int32_t& b, int32_t w, const FastConst& K) {
+    const int32_t v = smul(b, w, K), u = a;
     a = u + v;
-    b = u - v + K.twoQ;
+    b = u - v;
 }
-__device__ __forceinline__ void bfly_gs(uint32_t& a, uint32_t& b, uint32_t w, const FastConst& K) {
-    const uint32_t u = a, v = b;
-    a = csub32(u + v, K.twoQ);
-    b = mmul(u - v + K.twoQ, w, K);
+// Gentleman-Sande: (a, b) -> (a + b, (a - b) w); RED also reduces the sum
+template <bool RED = false>
+__device__ __forceinline__ void bfly_gs(int32_t& a, int32_t& b, int32_t w, const FastConst& K) {
+    const int32_t u = a, v = b;
+    a = RED ? smul(u + v, K.rM, K) : u + v;
+    b = smul(u - v, w, K);
 }
 
 // radix-8 Cooley-Tukey pass over register bits (r2, r1, r0) = three index bits,
 // twiddle psi[2^s + block] with block prefix c; FULL=false runs only the r0 stage.
 template <bool FULL>
-__device__ __forceinline__ void fwd_pass(uint32_t (&x)[8], const uint32_t* psi, uint32_t m, uint32_t c,
+__device__ __forceinline__ void fwd_pass(int32_t (&x)[8], const int32_t* psi, uint32_t m, uint32_t c,
                                          const FastConst& K) {
     if constexpr (FULL) {
-        const uint32_t w = psi[m + c];
+        const int32_t w = psi[m + c];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bfly_ct(x[r], x[r + 4], w, K);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const uint32_t w1 = psi[2 * m + 2 * c + h];
+            const int32_t w1 = psi[2 * m + 2 * c + h];
             bfly_ct(x[4 * h], x[4 * h + 2], w1, K);
             bfly_ct(x[4 * h + 1], x[4 * h + 3], w1, K);
         }
@@ -142,26 +155,29 @@ __device__ __forceinline__ void fwd_pass(uint32_t (&x)[8], const uint32_t* psi, 
     for (int q = 0; q < 4; ++q) bfly_ct(x[2 * q], x[2 * q + 1], psi[4 * m + 4 * c + q], K);
 }
 
+// Inverse radix-8 pass.  With inputs < B the doubling a-paths reach 4B after two
+// stages; x[0] and x[4] (the only ones) are reduced there, so the outputs stay < 3Q
+// for any B <= 3Q (tools/bounds_fast.py).
 template <bool FULL>
-__device__ __forceinline__ void inv_pass(uint32_t (&x)[8], const uint32_t* ipsi, uint32_t m, uint32_t c,
+__device__ __forceinline__ void inv_pass(int32_t (&x)[8], const int32_t* ipsi, uint32_t m, uint32_t c,
                                          const FastConst& K) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) bfly_gs(x[2 * q], x[2 * q + 1], ipsi[4 * m + 4 * c + q], K);
     if constexpr (FULL) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const uint32_t w1 = ipsi[2 * m + 2 * c + h];
-            bfly_gs(x[4 * h], x[4 * h + 2], w1, K);
+            const int32_t w1 = ipsi[2 * m + 2 * c + h];
+            bfly_gs<true>(x[4 * h], x[4 * h + 2], w1, K);
             bfly_gs(x[4 * h + 1], x[4 * h + 3], w1, K);
         }
-        const uint32_t w = ipsi[m + c];
+        const int32_t w = ipsi[m + c];
 #pragma unroll
         for (int r = 0; r < 4; ++r) bfly_gs(x[r], x[r + 4], w, K);
     }
 }
 
 // forward transform of two polynomials, L1 -> L4 (one cross-wave exchange)
-__device__ __forceinline__ void ntt_fwd2(uint32_t (&x0)[8], uint32_t (&x1)[8], uint32_t* buf, const uint32_t* psi,
+__device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], int32_t* buf, const int32_t* psi,
                                          uint32_t t, const FastConst& K) {
     fwd_pass<true>(x0, psi, 1, 0, K);
     fwd_pass<true>(x1, psi, 1, 0, K);
@@ -192,7 +208,7 @@ __device__ __forceinline__ void ntt_fwd2(uint32_t (&x0)[8], uint32_t (&x1)[8], u
 }
 
 // inverse transform of two polynomials (no N^-1: folded into the BSK), L4 -> L1
-__device__ __forceinline__ void ntt_inv2(uint32_t (&x0)[8], uint32_t (&x1)[8], uint32_t* buf, const uint32_t* ipsi,
+__device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], int32_t* buf, const int32_t* ipsi,
                                          uint32_t t, const FastConst& K) {
     inv_pass<false>(x0, ipsi, 128, t, K);
     inv_pass<false>(x1, ipsi, 128, t, K);
@@ -222,38 +238,44 @@ __device__ __forceinline__ void ntt_inv2(uint32_t (&x0)[8], uint32_t (&x1)[8], u
     inv_pass<true>(x1, ipsi, 1, 0, K);
 }
 
-// MINW: minimum waves per SIMD requested from the register allocator;
-// ACC32: reduce every digit pair into 32-bit accumulators (fewer VGPRs, +2 ops per term pair);
-// RECOMP: recompute digit l from the accumulator in pass l instead of carrying the
-//         16-register decomposition state (fewer VGPRs, +3 ops per extra digit step)
-template <int MINW, bool ACC32, bool RECOMP = false>
-__global__ void __launch_bounds__(THREADS, MINW)
-k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __restrict__ tabs,
-                    const uint32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
+// MINW: minimum waves per SIMD requested from the register allocator.
+// ACC64: exact 64-bit sums over all 8 rows, one reduction per output (32 more VGPRs);
+//        otherwise every digit's row pair is reduced into a 32-bit sum.
+// CTS: ciphertexts per workgroup (a workgroup barrier then spans 2*CTS wavefronts).
+template <int MINW, bool ACC64, int CTS>
+__global__ void __launch_bounds__(TPC * CTS, MINW)
+k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
+                    const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
                     uint32_t B) {
-    extern __shared__ __align__(16) uint32_t lds[];
+    extern __shared__ __align__(16) int32_t lds[];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < T_WORDS; k += THREADS) lds[k] = tabs[k];
-    const uint32_t cl = tid / TPC, t = tid % TPC;
+    for (uint32_t k = tid; k < T_WORDS; k += TPC * CTS) lds[k] = tabs[k];
+    const uint32_t cl = __builtin_amdgcn_readfirstlane(tid / TPC), t = tid % TPC;
     const uint32_t ct = blockIdx.x * CTS + cl;
     const bool active = ct < B;
-    uint32_t* buf = lds + T_WORDS + cl * BUF_WORDS;
-    const uint32_t* psi = lds + T_PSI;
-    const uint32_t* ipsi = lds + T_IPSI;
-    const uint32_t* mono = lds + T_MONO;
-    const uint32_t* eidx = lds + T_EIDX;
+    int32_t* buf = lds + T_WORDS + cl * BUF_WORDS;
+    const int32_t* psi = lds + T_PSI;
+    const int32_t* ipsi = lds + T_IPSI;
+    const char* mono = reinterpret_cast<const char*>(lds + T_MONO);
 
     uint64_t* g = acc_io + (size_t)(active ? ct : 0) * 2 * FN;
-    uint32_t acc[2][8];
+    const uint32_t Qh = (uint32_t)K.Q >> 1;
+    int32_t acc[2][8];  // centred canonical, [-(Q>>1)-1, Q>>1)
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            uint64_t v = active ? g[p * FN + ix1(t, r)] : 0;
-            acc[p][r] = (uint32_t)(v >= K.Q ? v % K.Q : v);
+            const uint64_t v0 = active ? g[p * FN + ix1(t, r)] : 0;
+            const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
+            acc[p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
         }
     __syncthreads();
 
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * (2 * FDG2 * 2 * FN * 4)), 0x00020000);
+    const uint32_t voff = t * 32;  // 8 consecutive words per lane in L4
+    // slot exponent of L4 slot 8t + r: e = 256 bitrev3(r) + et, et = 2 bitrev7(t) + 1
+    const uint32_t et = 2 * (__builtin_bitreverse32(t) >> 25) + 1;
     const uint64_t* ap = a + (size_t)(active ? ct : 0) * n;
     const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;  // 2N = 2^11
     for (uint32_t i = 0; i < n; ++i) {
@@ -261,55 +283,31 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
         const uint32_t ar = active ? (uint32_t)(ap[i] & amask) : 0;
         const uint32_t ai = ((amask + 1 - ar) & amask) << ashift;
 
-        int32_t d[2][8];  // centred coefficients, consumed digit by digit (rgsw-acc.cpp:83-109)
-        if constexpr (!RECOMP) {
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int r = 0; r < 8; ++r)
-                    d[p][r] = acc[p][r] < K.Qhalf ? (int32_t)acc[p][r] : (int32_t)(acc[p][r] - K.Q);
-        }
-
-        uint64_t s[2][2][8];   // exact 64-bit sums (ACC32 = false)
-        uint32_t s32[2][2][8]; // per-pair reduced sums < 4 * 2.4Q (ACC32 = true)
+        int64_t s[2][2][8];   // ACC64: exact sums
+        int32_t s32[2][2][8]; // otherwise: per-digit reduced sums
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
-                    if constexpr (ACC32) s32[k][j][r] = 0;
-                    else s[k][j][r] = 0;
+                    if constexpr (ACC64) s[k][j][r] = 0;
+                    else s32[k][j][r] = 0;
                 }
 
-        // wave-uniform round base (SGPRs) + 32-bit lane offset: global_load_dwordx4 v, voff, s[base]
-        const uint32_t* ek = bsk + (size_t)i * (2 * FDG2 * 2 * FN);
-        const uint32_t toff = t * 8;
-#pragma unroll 1
+        // BSK rows through a buffer resource: lane offset in a VGPR, row offset in an SGPR
+        const uint32_t round_off = i * (2 * FDG2 * 2 * FN * 4);
+#pragma unroll
         for (uint32_t l = 0; l < FDIG; ++l) {
-            uint32_t x0[8], x1[8];
-            if constexpr (RECOMP) {
+            // signed digit l of the centred c (rgsw-acc.cpp:83-109, carries included):
+            //   d_l = (c + 64 (1 + 128 + ... + 128^(l-1))) >> 7l,  digit = sext7(d_l);
+            //   the top digit |d_3| <= 33 is its own sext7, so one v_bfe_i32 serves all four
+            const int32_t kl = (int32_t)(((1u << (FLOGG * l)) - 1) / ((1u << FLOGG) - 1)) << (FLOGG - 1);
+            int32_t x0[8], x1[8];
 #pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    int32_t e0 = acc[0][r] < K.Qhalf ? (int32_t)acc[0][r] : (int32_t)(acc[0][r] - K.Q);
-                    int32_t e1 = acc[1][r] < K.Qhalf ? (int32_t)acc[1][r] : (int32_t)(acc[1][r] - K.Q);
-                    for (uint32_t z = 0; z < l; ++z) {  // drop the l lower digits (carries included)
-                        e0 = (e0 - ((e0 << (32 - FLOGG)) >> (32 - FLOGG))) >> FLOGG;
-                        e1 = (e1 - ((e1 << (32 - FLOGG)) >> (32 - FLOGG))) >> FLOGG;
-                    }
-                    x0[r] = (uint32_t)(((e0 << (32 - FLOGG)) >> (32 - FLOGG)) + (int32_t)K.Q);
-                    x1[r] = (uint32_t)(((e1 << (32 - FLOGG)) >> (32 - FLOGG)) + (int32_t)K.Q);
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const int32_t r0 = (d[0][r] << (32 - FLOGG)) >> (32 - FLOGG);  // signed low digit
-                    const int32_t r1 = (d[1][r] << (32 - FLOGG)) >> (32 - FLOGG);
-                    d[0][r] = (d[0][r] - r0) >> FLOGG;
-                    d[1][r] = (d[1][r] - r1) >> FLOGG;
-                    x0[r] = (uint32_t)(r0 + (int32_t)K.Q);  // = r mod Q, in [Q-64, Q+64)
-                    x1[r] = (uint32_t)(r1 + (int32_t)K.Q);
-                }
+            for (int r = 0; r < 8; ++r) {
+                x0[r] = __builtin_amdgcn_sbfe(acc[0][r] + kl, FLOGG * l, FLOGG);
+                x1[r] = __builtin_amdgcn_sbfe(acc[1][r] + kl, FLOGG * l, FLOGG);
             }
             ntt_fwd2(x0, x1, buf, psi + opaque_zero(), t, K);
             // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l)
@@ -317,74 +315,85 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const uint32_t* __re
             for (int k = 0; k < 2; ++k)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const uint32_t* r0p = ek + ((k * FDG2 + 2 * l) * 2 + j) * FN;      // uniform
-                    const uint32_t* r1p = ek + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN;  // uniform
-                    const uint4* e0 = reinterpret_cast<const uint4*>(r0p + toff);
-                    const uint4* e1 = reinterpret_cast<const uint4*>(r1p + toff);
+                    const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;      // uniform
+                    const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;  // uniform
                     // one (key, poly) group of BSK words at a time: bounds the staging registers
                     __builtin_amdgcn_sched_barrier(0);
-                    const uint4 a0 = e0[0], a1 = e0[1], b0 = e1[0], b1 = e1[1];
-                    const uint32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                    const uint32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                    const v4i a0 = ld_bsk(rsrc, voff, s0), a1 = ld_bsk(rsrc, voff + 16, s0);
+                    const v4i b0 = ld_bsk(rsrc, voff, s1), b1 = ld_bsk(rsrc, voff + 16, s1);
+                    const int32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                    const int32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
-                        if constexpr (ACC32) {
-                            const uint64_t T = (uint64_t)x0[r] * w0[r] + (uint64_t)x1[r] * w1[r];
-                            s32[k][j][r] += redc(T, K.Q, K.qinv);
-                        } else {  // two chained v_mad_u64_u32 into the exact sum
-                            s[k][j][r] = (uint64_t)x0[r] * w0[r] + s[k][j][r];
-                            s[k][j][r] = (uint64_t)x1[r] * w1[r] + s[k][j][r];
+                        if constexpr (ACC64) {
+                            s[k][j][r] = (int64_t)x0[r] * w0[r] + s[k][j][r];
+                            s[k][j][r] = (int64_t)x1[r] * w1[r] + s[k][j][r];
+                        } else {
+                            const int64_t T = (int64_t)x0[r] * w0[r] + (int64_t)x1[r] * w1[r];
+                            s32[k][j][r] += sredc(T, K);
                         }
                     }
                 }
         }
 
         // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1)
-        uint32_t S0[8], S1[8];
+        const uint32_t b4 = (et * ai) << 2;       // byte offsets into the 2N-entry table
+        const uint32_t st4 = (ai << 10) & 8191;   // 256 * ai * 4 mod 8192
+        int32_t S0[8], S1[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const uint32_t ip = (eidx[t * 8 + r] * ai) & (2 * FN - 1);
-            const uint32_t in = (2 * FN - ip) & (2 * FN - 1);
-            const uint32_t mp = mono[ip], mn = mono[in];
-            uint32_t A00, A01, A10, A11;
-            if constexpr (ACC32) {
-                A00 = s32[0][0][r], A01 = s32[0][1][r], A10 = s32[1][0][r], A11 = s32[1][1][r];
+            const uint32_t c = __builtin_bitreverse32((uint32_t)r) >> 29;
+            const uint32_t e4 = b4 + c * st4;
+            const int32_t mp = *reinterpret_cast<const int32_t*>(mono + (e4 & 8188));
+            const int32_t mn = *reinterpret_cast<const int32_t*>(mono + ((0u - e4) & 8188));
+            int32_t A00, A01, A10, A11;
+            if constexpr (ACC64) {
+                A00 = sredc(s[0][0][r], K), A01 = sredc(s[0][1][r], K);
+                A10 = sredc(s[1][0][r], K), A11 = sredc(s[1][1][r], K);
             } else {
-                A00 = redc(s[0][0][r], K.Q, K.qinv), A01 = redc(s[0][1][r], K.Q, K.qinv);
-                A10 = redc(s[1][0][r], K.Q, K.qinv), A11 = redc(s[1][1][r], K.Q, K.qinv);
+                A00 = s32[0][0][r], A01 = s32[0][1][r], A10 = s32[1][0][r], A11 = s32[1][1][r];
             }
-            S0[r] = redc((uint64_t)A00 * mp + (uint64_t)A10 * mn, K.Q, K.qinv);
-            S1[r] = redc((uint64_t)A01 * mp + (uint64_t)A11 * mn, K.Q, K.qinv);
+            S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
+            S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
         }
         ntt_inv2(S0, S1, buf, ipsi + opaque_zero(), t, K);
+        // acc <- centred canonical (acc + S): u = acc + S + (Q>>1) + 1 + 4Q in (0, 8Q)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            acc[0][r] = csub32(csub32(acc[0][r] + S0[r], K.twoQ), K.Q);
-            acc[1][r] = csub32(csub32(acc[1][r] + S1[r], K.twoQ), K.Q);
+            uint32_t u0 = (uint32_t)(acc[0][r] + S0[r]) + K.kacc;
+            uint32_t u1 = (uint32_t)(acc[1][r] + S1[r]) + K.kacc;
+            u0 = csub32(csub32(csub32(u0, K.Q4), K.Q2), (uint32_t)K.Q);
+            u1 = csub32(csub32(csub32(u1, K.Q4), K.Q2), (uint32_t)K.Q);
+            acc[0][r] = (int32_t)(u0 - K.h1);
+            acc[1][r] = (int32_t)(u1 - K.h1);
         }
     }
     if (active) {
         // acc0 transposed (X -> X^-1, poly.cpp:762-770): out[(N-k) mod N] = -acc0[k]
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const uint32_t k = ix1(t, r), v = acc[0][r];
-            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : K.Q - v);
-            g[FN + k] = acc[1][r];
+            const uint32_t k = ix1(t, r);
+            const uint32_t v = (uint32_t)(acc[0][r] < 0 ? acc[0][r] + K.Q : acc[0][r]);
+            const uint32_t v1 = (uint32_t)(acc[1][r] < 0 ? acc[1][r] + K.Q : acc[1][r]);
+            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
+            g[FN + k] = v1;
         }
     }
 }
 
-// generic (plain, N^-1-scaled) BSK and tables -> Montgomery-form copies
+// generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies
 __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t words, const uint32_t* __restrict__ psi,
                             const uint32_t* __restrict__ ipsi, const uint32_t* __restrict__ mono,
-                            const uint32_t* __restrict__ eidx, uint32_t* __restrict__ out) {
+                            int32_t* __restrict__ out) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    auto mont = [Q](uint32_t v) { return (uint32_t)(((uint64_t)v << 32) % Q); };
+    auto mont = [Q](uint32_t v) {
+        const uint32_t m = (uint32_t)(((uint64_t)v << 32) % Q);
+        return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+    };
     if (idx < words) out[T_WORDS + idx] = mont(bsk[idx]);
     if (idx < FN) {
         out[T_PSI + idx] = mont(psi[idx]);
         out[T_IPSI + idx] = mont(ipsi[idx]);
-        out[T_EIDX + idx] = eidx[idx];
     }
     if (idx < 2 * FN) out[T_MONO + idx] = mont(mono[idx]);
 }
@@ -403,7 +412,7 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
     const size_t words = (size_t)P.n * 2 * FDG2 * 2 * FN;
     hipLaunchKernelGGL(k_pack_fast, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint32_t)P.Q,
                        (const uint32_t*)bsk, words, (const uint32_t*)T.psi, (const uint32_t*)T.ipsi,
-                       (const uint32_t*)T.mono, T.eidx, (uint32_t*)bsk_fast);
+                       (const uint32_t*)T.mono, (int32_t*)bsk_fast);
     return hipGetLastError();
 }
 
@@ -413,34 +422,37 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     if (amod == 0 || (amod & (amod - 1)) || amod > 2 * FN) return hipErrorNotSupported;
     uint32_t loga = 0;
     while ((1ull << loga) < amod) ++loga;
-    FastConst K;
-    K.Q = (uint32_t)P.Q;
+    const uint32_t Q = (uint32_t)P.Q;
     uint32_t inv = 1;  // Q^-1 mod 2^32 by Newton iteration
-    for (int it = 0; it < 5; ++it) inv *= 2u - K.Q * inv;
-    K.qinv = 0u - inv;
-    K.twoQ = 2 * K.Q;
-    K.Qhalf = K.Q >> 1;
-    const uint32_t* tabs = (const uint32_t*)bsk_fast;
-    const uint32_t* bsk = tabs + T_WORDS;
+    for (int it = 0; it < 5; ++it) inv *= 2u - Q * inv;
+    FastConst K;
+    K.Q = (int32_t)Q;
+    K.nQ = -(int32_t)Q;
+    K.qinv = (int32_t)inv;
+    const uint32_t rm = (uint32_t)((1ull << 32) % Q);
+    K.rM = rm > Q / 2 ? (int32_t)rm - (int32_t)Q : (int32_t)rm;
+    K.Q2 = 2 * Q;
+    K.Q4 = 4 * Q;
+    K.h1 = (Q >> 1) + 1;
+    K.kacc = K.h1 + 4 * Q;
+    const int32_t* tabs = (const int32_t*)bsk_fast;
+    const int32_t* bsk = tabs + T_WORDS;
     static const int variant = [] {
         const char* e = std::getenv("TFHE_FAST_VARIANT");
         return e ? std::atoi(e) : 0;
     }();
-    // default: 3 waves/SIMD with per-pair 32-bit accumulation (fastest measured,
-    // tools/variant_sweep.sh: 68.6 ms vs 75.1 ms for <2,false> per 8192-batch)
-    auto k = k_blind_rotate_fast<3, true>;
+    auto launch = [&](auto kern, int cts) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts), s, K, P.n,
+                           loga, tabs, bsk, a, acc, (uint32_t)B);
+    };
     switch (variant) {
-        case 1: k = k_blind_rotate_fast<3, false>; break;
-        case 5: k = k_blind_rotate_fast<2, false>; break;
-        case 3: k = k_blind_rotate_fast<4, true>; break;
-        case 4: k = k_blind_rotate_fast<2, true>; break;
-        case 6: k = k_blind_rotate_fast<4, true, true>; break;
-        case 7: k = k_blind_rotate_fast<3, true, true>; break;
-        default: break;
+        case 1: launch(k_blind_rotate_fast<3, false, 2>, 2); break;
+        case 2: launch(k_blind_rotate_fast<3, true, 1>, 1); break;
+        case 3: launch(k_blind_rotate_fast<2, true, 2>, 2); break;
+        case 4: launch(k_blind_rotate_fast<3, false, 1>, 1); break;
+        default: launch(k_blind_rotate_fast<3, true, 2>, 2); break;
     }
-    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
-    hipLaunchKernelGGL(k, dim3((unsigned)((B + CTS - 1) / CTS)), dim3(THREADS), LDS_BYTES, s, K, P.n, loga, tabs,
-                       bsk, a, acc, (uint32_t)B);
     return hipGetLastError();
 }
 

@@ -221,6 +221,9 @@ tfhe_status build_host_image(tfhe_ctx* c, const uint64_t* bsk_coeff, const uint6
         put(uint64_t{}, L.bsk, L.bsk_sh, bsk_ntt.data(), L.bsk_words);
     }
     std::memcpy(img.data() + L.eidx, t.eidx.data(), sizeof(uint32_t) * p.N);
+    if (c->use_fast)  // the fast kernel derives e_x = 2 bitrev(x) + 1 in registers
+        for (uint32_t x = 0; x < p.N; ++x)
+            if (t.eidx[x] != 2 * bitrev(x, t.logN) + 1) return fail(TFHE_ERR_INTERNAL, "eidx is not 2 bitrev(x) + 1");
     // KSK: packed to the narrowest word holding qKS (reference keeps u64, bootstrapping.cu:963)
     const uint64_t qks = p.qKS;
     std::atomic<bool> bad{false};
@@ -951,6 +954,9 @@ tfhe_status tfhe_host_selftest(const tfhe_params* pin) {
             if (mon[x] != addmod(t.mono[idx], 1, p.Q)) return fail(TFHE_ERR_INTERNAL, "monomial table mismatch");
         }
     }
+    // (3b) the slot exponents are 2 bitrev(x) + 1 (the fast kernel relies on it)
+    for (uint32_t x = 0; x < p.N; ++x)
+        if (t.eidx[x] != 2 * bitrev(x, t.logN) + 1) return fail(TFHE_ERR_INTERNAL, "eidx is not 2 bitrev(x) + 1");
     // (4) Shoup companions at the chosen word width
     const int wb = word_bits_for(p);
     const u128 R = (u128)1 << wb;

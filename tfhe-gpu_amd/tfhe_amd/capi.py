@@ -106,6 +106,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(_LIB):
             raise TfheError(-1, "load", f"{_LIB} missing: run tfhe_amd.build() (make -C tfhe-gpu_amd)")
+        # One HIP runtime per process: torch wheels bundle libamdhip64/libhsa-runtime64
+        # with the same sonames as /opt/rocm's but are NEEDED under unversioned names,
+        # so loading ours first would put two HSA runtimes on one GPU and torch would
+        # then see no devices.  Loading torch first makes ours bind to its runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(_LIB)
         for name, (args, res) in _SIGS.items():
             fn = getattr(L, name)

@@ -41,6 +41,10 @@ __global__ void NAME(uint32_t* out, int iters, uint32_t seed) {                 
 #define S_SUBMIN(x) asm volatile("v_min_u32 %0, %0, %1" : "+v"(x) : "v"(c));
 #define S_ALIGN(x) asm volatile("v_alignbit_b32 %0, %0, %1, 5" : "+v"(x) : "v"(c));
 #define S_CVT(x) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(x));
+#define S_BFE(x) asm volatile("v_bfe_i32 %0, %0, 0, 7" : "+v"(x));
+#define S_ADD3(x) asm volatile("v_add3_u32 %0, %0, %1, %0" : "+v"(x) : "v"(c));
+#define S_SUB(x) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(x) : "v"(c));
+#define S_ASHR(x) asm volatile("v_ashrrev_i32 %0, 3, %0" : "+v"(x));
 
 DEF_U32_KERNEL(k_mul_lo_u32, S_MUL_LO)
 DEF_U32_KERNEL(k_mul_hi_u32, S_MUL_HI)
@@ -51,6 +55,10 @@ DEF_U32_KERNEL(k_add_u32, S_ADD)
 DEF_U32_KERNEL(k_min_u32, S_SUBMIN)
 DEF_U32_KERNEL(k_alignbit, S_ALIGN)
 DEF_U32_KERNEL(k_cvt_f32_u32, S_CVT)
+DEF_U32_KERNEL(k_bfe_i32, S_BFE)
+DEF_U32_KERNEL(k_add3_u32, S_ADD3)
+DEF_U32_KERNEL(k_sub_u32, S_SUB)
+DEF_U32_KERNEL(k_ashr_i32, S_ASHR)
 
 #define DEF_U64_KERNEL(NAME, ASM)                                                   \
 __global__ void NAME(uint64_t* out, int iters, uint32_t seed) {                     \
@@ -69,7 +77,9 @@ __global__ void NAME(uint64_t* out, int iters, uint32_t seed) {                 
 #define S_MAD64(x) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x) : "v"(c), "v"(d) : "vcc");
 #define S_LSHR64(x) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(x));
 #define S_ADD64(x) asm volatile("v_lshl_add_u64 %0, %0, 0, %0" : "+v"(x));
+#define S_MADI64(x) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(x) : "v"(c), "v"(d) : "vcc");
 DEF_U64_KERNEL(k_mad_u64_u32, S_MAD64)
+DEF_U64_KERNEL(k_mad_i64_i32, S_MADI64)
 DEF_U64_KERNEL(k_lshrrev_b64, S_LSHR64)
 DEF_U64_KERNEL(k_lshl_add_u64, S_ADD64)
 
@@ -222,6 +232,11 @@ int main() {
     run<uint32_t>("v_mul_lo_u32", k_mul_lo_u32, ops, peak);
     run<uint32_t>("v_mul_hi_u32", k_mul_hi_u32, ops, peak);
     run<uint64_t>("v_mad_u64_u32", k_mad_u64_u32, ops, peak);
+    run<uint64_t>("v_mad_i64_i32", k_mad_i64_i32, ops, peak);
+    run<uint32_t>("v_bfe_i32", k_bfe_i32, ops, peak);
+    run<uint32_t>("v_add3_u32", k_add3_u32, ops, peak);
+    run<uint32_t>("v_sub_u32", k_sub_u32, ops, peak);
+    run<uint32_t>("v_ashrrev_i32", k_ashr_i32, ops, peak);
     run<uint64_t>("v_lshrrev_b64", k_lshrrev_b64, ops, peak);
     run<uint64_t>("v_lshl_add_u64", k_lshl_add_u64, ops, peak);
     run<double>("v_fma_f64", k_fma_f64, ops, peak);
