@@ -52,11 +52,21 @@ constexpr uint32_t FDIG = 4;
 constexpr uint32_t FLOGG = 7;
 constexpr int TPC = 128;  // threads per ciphertext
 
-// device table block (int32 words, centred Montgomery): psi[1024] ipsi[1024] mono[2048]
-constexpr uint32_t T_PSI = 0, T_IPSI = 1024, T_MONO = 2048, T_WORDS = 4096;
-constexpr uint32_t PFN = FN + FN / 8;      // padded polynomial (swz)
-constexpr uint32_t BUF_WORDS = 2 * PFN;    // per ciphertext: two polynomials
-constexpr size_t lds_bytes(int cts) { return (size_t)(T_WORDS + cts * BUF_WORDS) * 4; }
+// Table block (int32 words, centred Montgomery form).  Twiddles are packed per radix-8
+// pass so that a lane fetches the 7 twiddles of its block with two ds_read_b128:
+//   TW1[8]        pass on (b9 b8 b7), one block
+//   TW2[8][8]     pass on (b6 b5 b4), block c = i >> 7
+//   TW3[64][8]    pass on (b3 b2 b1), block c = i >> 4
+//   TW4[512]      single stage on b0: psi[512 + (i >> 1)]
+// block c of a pass with stride m holds psi[m+c], psi[2m+2c], psi[2m+2c+1], psi[4m+4c .. +3], 0.
+// Forward (psi) and inverse (psi^-1) sets, then mono[2N] = psi^k - 1.
+constexpr uint32_t TW1 = 0, TW2 = 8, TW3 = 72, TW4 = 584, TW_WORDS = 1096;
+constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS = 2 * TW_WORDS + 2 * FN;
+// Exchange buffers per ciphertext: two alternating buffers, each 2 regions (one per
+// reading wavefront) x 2 polynomials x PS words.
+// (NB = 1: one buffer and an extra barrier before each cross-wavefront store)
+constexpr uint32_t PS = 576, WS = 2 * PS, XBUF = 2 * WS;
+constexpr size_t lds_bytes(int cts, int nb) { return (size_t)(T_WORDS + cts * nb * XBUF) * 4; }
 
 struct FastConst {
     int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x
@@ -77,48 +87,152 @@ __device__ __forceinline__ v4i ld_bsk(__amdgpu_buffer_rsrc_t r, uint32_t voff, u
     return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
 
-// LDS word index of natural index i: 2 pad words per 16.  Affine in the register
-// index for all four layouts (address = base(lane) + immediate), and at most
-// 2-way bank conflicts per 32-lane group.
-__device__ __forceinline__ uint32_t swz(uint32_t i) { return i + 2 * (i >> 4); }
-
-__device__ __forceinline__ uint32_t ix1(uint32_t t, uint32_t r) { return r * 128 + t; }
-__device__ __forceinline__ uint32_t ix2(uint32_t t, uint32_t r) { return (t >> 4) * 128 + r * 16 + (t & 15); }
-__device__ __forceinline__ uint32_t ix3(uint32_t t, uint32_t r) { return (t >> 1) * 16 + r * 2 + (t & 1); }
-__device__ __forceinline__ uint32_t ix4(uint32_t t, uint32_t r) { return t * 8 + r; }
-
-template <int L>
-__device__ __forceinline__ uint32_t ix(uint32_t t, uint32_t r) {
-    if constexpr (L == 1) return ix1(t, r);
-    else if constexpr (L == 2) return ix2(t, r);
-    else if constexpr (L == 3) return ix3(t, r);
-    else return ix4(t, r);
+// ---- layouts and exchanges (model and proof: tools/lds_layouts.py) ----
+// A layout names the index bit (b9..b0 of the natural index i) carried by each register
+// bit (r = 0..7) and lane bit (lane = 0..127 of the ciphertext, bit 6 = wavefront):
+//   L1 regs (b7 b8 b9)  lanes (b4 b5 b1 b2 b3 b0 | b6)   coefficient order, pass on b9 b8 b7
+//   L2 regs (b4 b5 b6)  lanes (b1 b2 b3 b7 b8 b0 | b9)   pass on b6 b5 b4
+//   L3 regs (b1 b2 b3)  lanes (b4 b5 b6 b7 b8 b0 | b9)   pass on b3 b2 b1
+//   L4 regs (b0 b1 b2)  lanes (b4 b5 b6 b7 b8 b3 | b9)   stage on b0; MAC (8 consecutive slots)
+// Only L1 <-> L2 crosses wavefronts.  An exchange A -> B stores each register of A as one
+// lane-contiguous row (ds_write_addtid_b32: no address VGPR, 2 cycles) and B gathers with
+// ds_read_b32 at F(lane) + G(register).  Rows are placed in the region of the wavefront
+// that reads them, with strides chosen so every 32-lane read group hits 32 distinct banks.
+struct Lay {
+    int reg[3];
+    int lane[7];
+};
+__host__ __device__ constexpr Lay lay(int L) {
+    return L == 1   ? Lay{{7, 8, 9}, {4, 5, 1, 2, 3, 0, 6}}
+           : L == 2 ? Lay{{4, 5, 6}, {1, 2, 3, 7, 8, 0, 9}}
+           : L == 3 ? Lay{{1, 2, 3}, {4, 5, 6, 7, 8, 0, 9}}
+                    : Lay{{0, 1, 2}, {4, 5, 6, 7, 8, 3, 9}};
 }
-
-template <int L>
-__device__ __forceinline__ void lds_store(int32_t* buf, const int32_t (&x)[8], uint32_t t) {
+__host__ __device__ constexpr int row_bit(int A, int B, int k) {
+    return (A == 1 && B == 2)   ? (k == 0 ? 7 : k == 1 ? 8 : 6)
+           : (A == 2 && B == 1) ? (k == 0 ? 4 : k == 1 ? 5 : 9)
+                                : lay(A).reg[k];
+}
+__host__ __device__ constexpr int row_stride(int A, int B) { return (A == 2 && B == 1) ? 72 : 65; }
+// words contributed to the LDS address by index bit b in exchange A -> B
+__host__ __device__ constexpr int wt(int A, int B, int b) {
+    if (b == lay(B).lane[6]) return (int)WS;
+    for (int k = 0; k < 3; ++k)
+        if (row_bit(A, B, k) == b) return row_stride(A, B) << k;
+    for (int k = 0; k < 6; ++k)
+        if (lay(A).lane[k] == b) return 1 << k;
+    return 1 << 24;  // unreachable for the layouts above
+}
+__host__ __device__ constexpr int st_off(int A, int B, int r, int p) {  // bytes, writer register r
+    int o = p * (int)PS;
+    for (int k = 0; k < 3; ++k)
+        if ((r >> k) & 1) o += wt(A, B, lay(A).reg[k]);
+    return o * 4;
+}
+__host__ __device__ constexpr int ld_off(int A, int B, int r, int p) {  // bytes, reader register r
+    int o = p * (int)PS;
+    for (int k = 0; k < 3; ++k)
+        if ((r >> k) & 1) o += wt(A, B, lay(B).reg[k]);
+    return o * 4;
+}
+template <int A, int B>
+__device__ __forceinline__ uint32_t ld_lane(uint32_t t) {  // bytes, reader lane t
+    uint32_t o = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < 8; ++r) buf[swz(ix<L>(t, r))] = x[r];
+    for (int k = 0; k < 7; ++k) o += ((t >> k) & 1) * (uint32_t)wt(A, B, lay(B).lane[k]);
+    return o * 4;
 }
 template <int L>
-__device__ __forceinline__ void lds_load(const int32_t* buf, int32_t (&x)[8], uint32_t t) {
+__device__ __forceinline__ uint32_t elem(uint32_t t, uint32_t r) {  // natural index of (lane, register)
+    uint32_t i = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < 8; ++r) x[r] = buf[swz(ix<L>(t, r))];
+    for (int k = 0; k < 3; ++k) i |= ((r >> k) & 1) << lay(L).reg[k];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) i |= ((t >> k) & 1) << lay(L).lane[k];
+    return i;
 }
 
-// An opaque zero: adding it to a table base stops the compiler from hoisting the
-// (loop-invariant) twiddle loads out of the round loop into registers.
-__device__ __forceinline__ uint32_t opaque_zero() {
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    return z;
+// one polynomial's 8 registers as 8 lane-contiguous rows (M0 = this wavefront's base)
+template <int A, int B, int P>
+__device__ __forceinline__ void store_rows(const int32_t (&x)[8], uint32_t m0, const int32_t* lds) {
+    asm volatile(
+        "s_mov_b32 m0, %8\n\t"
+        "s_nop 0\n\t"
+        "ds_write_addtid_b32 %0 offset:%10\n\t"
+        "ds_write_addtid_b32 %1 offset:%11\n\t"
+        "ds_write_addtid_b32 %2 offset:%12\n\t"
+        "ds_write_addtid_b32 %3 offset:%13\n\t"
+        "ds_write_addtid_b32 %4 offset:%14\n\t"
+        "ds_write_addtid_b32 %5 offset:%15\n\t"
+        "ds_write_addtid_b32 %6 offset:%16\n\t"
+        "ds_write_addtid_b32 %7 offset:%17" ::"v"(x[0]),
+        "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "s"(m0), "s"(lds),
+        "i"(st_off(A, B, 0, P)), "i"(st_off(A, B, 1, P)), "i"(st_off(A, B, 2, P)), "i"(st_off(A, B, 3, P)),
+        "i"(st_off(A, B, 4, P)), "i"(st_off(A, B, 5, P)), "i"(st_off(A, B, 6, P)), "i"(st_off(A, B, 7, P))
+        : "memory");
 }
 
-// ordering of LDS traffic between lanes of one wavefront
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+// LDS traffic of the transforms is issued from inline asm so that its completion can be
+// awaited with counted waits (LDS operations complete in order): one polynomial's pass runs
+// while the other one's rows are in flight.  The wait statements take the awaited
+// registers as read-write operands, which orders every consumer after the wait.
+//
+// 8 single-dword gathers from one base address (16-bit immediates, one address VGPR)
+template <int A, int B, int P>
+__device__ __forceinline__ void gather_rows(int32_t (&x)[8], uint32_t base, const int32_t* lds) {
+    asm volatile(
+        "ds_read_b32 %0, %8 offset:%10\n\t"
+        "ds_read_b32 %1, %8 offset:%11\n\t"
+        "ds_read_b32 %2, %8 offset:%12\n\t"
+        "ds_read_b32 %3, %8 offset:%13\n\t"
+        "ds_read_b32 %4, %8 offset:%14\n\t"
+        "ds_read_b32 %5, %8 offset:%15\n\t"
+        "ds_read_b32 %6, %8 offset:%16\n\t"
+        "ds_read_b32 %7, %8 offset:%17"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7])
+        : "v"(base), "s"(lds), "i"(ld_off(A, B, 0, P)), "i"(ld_off(A, B, 1, P)), "i"(ld_off(A, B, 2, P)),
+          "i"(ld_off(A, B, 3, P)), "i"(ld_off(A, B, 4, P)), "i"(ld_off(A, B, 5, P)), "i"(ld_off(A, B, 6, P)),
+          "i"(ld_off(A, B, 7, P))
+        : "memory");
+}
+// packed twiddles of one block: two ds_read_b128 (one for the single-stage pass)
+template <uint32_t OFF>
+__device__ __forceinline__ void tw_load(v4i& lo, v4i& hi, uint32_t addr, const int32_t* lds) {
+    asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b128 %1, %2 offset:%5"
+                 : "=&v"(lo), "=&v"(hi)
+                 : "v"(addr), "s"(lds), "i"(OFF), "i"(OFF + 16)
+                 : "memory");
+}
+template <uint32_t OFF>
+__device__ __forceinline__ void tw_load(v4i& lo, uint32_t addr, const int32_t* lds) {
+    asm volatile("ds_read_b128 %0, %1 offset:%3" : "=&v"(lo) : "v"(addr), "s"(lds), "i"(OFF) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(int32_t (&x)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                 : "i"(N)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(int32_t (&x)[8], v4i& lo, v4i& hi) {
+    asm volatile("s_waitcnt lgkmcnt(%10)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                   "+v"(lo), "+v"(hi)
+                 : "i"(N)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(int32_t (&x)[8], v4i& lo) {
+    asm volatile("s_waitcnt lgkmcnt(%9)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                   "+v"(lo)
+                 : "i"(N)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(v4i& lo, v4i& hi) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(lo), "+v"(hi) : "i"(N) : "memory");
 }
 
 // Cooley-Tukey: (a, b) -> (a + wb, a - wb);  |out| <= |a| + |b||w|/2^32 + Q/2
@@ -135,114 +249,163 @@ __device__ __forceinline__ void bfly_gs(int32_t& a, int32_t& b, int32_t w, const
     b = smul(u - v, w, K);
 }
 
-// radix-8 Cooley-Tukey pass over register bits (r2, r1, r0) = three index bits,
-// twiddle psi[2^s + block] with block prefix c; FULL=false runs only the r0 stage.
-template <bool FULL>
-__device__ __forceinline__ void fwd_pass(int32_t (&x)[8], const int32_t* psi, uint32_t m, uint32_t c,
-                                         const FastConst& K) {
-    if constexpr (FULL) {
-        const int32_t w = psi[m + c];
+// radix-8 CT pass over register bits (2, 1, 0); lo/hi = packed twiddles of the block
+__device__ __forceinline__ void fwd_pass8(int32_t (&x)[8], v4i lo, v4i hi, const FastConst& K) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bfly_ct(x[r], x[r + 4], w, K);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int32_t w1 = psi[2 * m + 2 * c + h];
-            bfly_ct(x[4 * h], x[4 * h + 2], w1, K);
-            bfly_ct(x[4 * h + 1], x[4 * h + 3], w1, K);
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bfly_ct(x[2 * q], x[2 * q + 1], psi[4 * m + 4 * c + q], K);
+    for (int r = 0; r < 4; ++r) bfly_ct(x[r], x[r + 4], lo.x, K);
+    bfly_ct(x[0], x[2], lo.y, K);
+    bfly_ct(x[1], x[3], lo.y, K);
+    bfly_ct(x[4], x[6], lo.z, K);
+    bfly_ct(x[5], x[7], lo.z, K);
+    bfly_ct(x[0], x[1], lo.w, K);
+    bfly_ct(x[2], x[3], hi.x, K);
+    bfly_ct(x[4], x[5], hi.y, K);
+    bfly_ct(x[6], x[7], hi.z, K);
 }
-
+__device__ __forceinline__ void fwd_pass1(int32_t (&x)[8], v4i w, const FastConst& K) {
+    bfly_ct(x[0], x[1], w.x, K);
+    bfly_ct(x[2], x[3], w.y, K);
+    bfly_ct(x[4], x[5], w.z, K);
+    bfly_ct(x[6], x[7], w.w, K);
+}
 // Inverse radix-8 pass.  With inputs < B the doubling a-paths reach 4B after two
 // stages; x[0] and x[4] (the only ones) are reduced there, so the outputs stay < 3Q
 // for any B <= 3Q (tools/bounds_fast.py).
-template <bool FULL>
-__device__ __forceinline__ void inv_pass(int32_t (&x)[8], const int32_t* ipsi, uint32_t m, uint32_t c,
-                                         const FastConst& K) {
+__device__ __forceinline__ void inv_pass8(int32_t (&x)[8], v4i lo, v4i hi, const FastConst& K) {
+    bfly_gs(x[0], x[1], lo.w, K);
+    bfly_gs(x[2], x[3], hi.x, K);
+    bfly_gs(x[4], x[5], hi.y, K);
+    bfly_gs(x[6], x[7], hi.z, K);
+    bfly_gs<true>(x[0], x[2], lo.y, K);
+    bfly_gs(x[1], x[3], lo.y, K);
+    bfly_gs<true>(x[4], x[6], lo.z, K);
+    bfly_gs(x[5], x[7], lo.z, K);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bfly_gs(x[2 * q], x[2 * q + 1], ipsi[4 * m + 4 * c + q], K);
-    if constexpr (FULL) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int32_t w1 = ipsi[2 * m + 2 * c + h];
-            bfly_gs<true>(x[4 * h], x[4 * h + 2], w1, K);
-            bfly_gs(x[4 * h + 1], x[4 * h + 3], w1, K);
-        }
-        const int32_t w = ipsi[m + c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bfly_gs(x[r], x[r + 4], w, K);
+    for (int r = 0; r < 4; ++r) bfly_gs(x[r], x[r + 4], lo.x, K);
+}
+__device__ __forceinline__ void inv_pass1(int32_t (&x)[8], v4i w, const FastConst& K) {
+    bfly_gs(x[0], x[1], w.x, K);
+    bfly_gs(x[2], x[3], w.y, K);
+    bfly_gs(x[4], x[5], w.z, K);
+    bfly_gs(x[6], x[7], w.w, K);
+}
+
+// per-lane constants of the transforms
+struct LaneCtx {
+    uint32_t w;                               // wavefront of the ciphertext (uniform)
+    uint32_t f12, f23, f34, f43, f32, f21;    // gather offsets (bytes)
+    uint32_t a2, a3, a4;                      // twiddle block offsets (bytes)
+    uint32_t zero;                            // 0, as an address VGPR
+};
+
+// Forward transform of two polynomials, L1 -> L4; sbuf = the ciphertext's current
+// exchange buffer (bytes).  The two polynomials are staggered: while one polynomial's
+// rows travel through LDS, the other one's radix-8 pass runs.  Wait counts are the LDS
+// operations issued after the awaited ones (15 = the counter's maximum, at most one
+// operation stricter than needed).
+template <int NB>
+__device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sbuf,
+                                         const LaneCtx& C, const FastConst& K) {
+    constexpr uint32_t T = T_FWD * 4;
+    const uint32_t m12 = sbuf + C.w * (uint32_t)(wt(1, 2, 6) * 4);  // uniform
+    const uint32_t mloc = sbuf + C.w * WS * 4;                      // uniform: own region
+    v4i lo, hi;
+    tw_load<T + TW1 * 4>(lo, hi, C.zero, lds);
+    lds_wait<0>(lo, hi);
+    fwd_pass8(x0, lo, hi, K);
+    if constexpr (NB == 1) {  // the other wavefront has finished reading this buffer
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
     }
+    store_rows<1, 2, 0>(x0, m12, lds);
+    fwd_pass8(x1, lo, hi, K);
+    store_rows<1, 2, 1>(x1, m12, lds);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    tw_load<T + TW2 * 4>(lo, hi, C.a2, lds);
+    gather_rows<1, 2, 0>(x0, sbuf + C.f12, lds);
+    gather_rows<1, 2, 1>(x1, sbuf + C.f12, lds);
+    lds_wait<8>(x0, lo, hi);
+    fwd_pass8(x0, lo, hi, K);
+    store_rows<2, 3, 0>(x0, mloc, lds);
+    gather_rows<2, 3, 0>(x0, sbuf + C.f23, lds);
+    lds_wait<15>(x1);
+    fwd_pass8(x1, lo, hi, K);
+    tw_load<T + TW3 * 4>(lo, hi, C.a3, lds);
+    store_rows<2, 3, 1>(x1, mloc, lds);
+    gather_rows<2, 3, 1>(x1, sbuf + C.f23, lds);
+    lds_wait<15>(x0, lo, hi);
+    fwd_pass8(x0, lo, hi, K);
+    store_rows<3, 4, 0>(x0, mloc, lds);
+    gather_rows<3, 4, 0>(x0, sbuf + C.f34, lds);
+    lds_wait<15>(x1);
+    fwd_pass8(x1, lo, hi, K);
+    tw_load<T + TW4 * 4>(lo, C.a4, lds);
+    store_rows<3, 4, 1>(x1, mloc, lds);
+    gather_rows<3, 4, 1>(x1, sbuf + C.f34, lds);
+    lds_wait<15>(x0, lo);
+    fwd_pass1(x0, lo, K);
+    lds_wait<0>(x1);
+    fwd_pass1(x1, lo, K);
 }
 
-// forward transform of two polynomials, L1 -> L4 (one cross-wave exchange)
-__device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], int32_t* buf, const int32_t* psi,
-                                         uint32_t t, const FastConst& K) {
-    fwd_pass<true>(x0, psi, 1, 0, K);
-    fwd_pass<true>(x1, psi, 1, 0, K);
-    __syncthreads();  // the other wavefront has finished reading buf
-    lds_store<1>(buf, x0, t);
-    lds_store<1>(buf + PFN, x1, t);
+// Inverse transform of two polynomials (no N^-1: folded into the BSK), L4 -> L1.
+// sloc = buffer of the last forward exchange (wave-local steps), sx = the other buffer.
+template <int NB>
+__device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sloc,
+                                         uint32_t sx, const LaneCtx& C, const FastConst& K) {
+    constexpr uint32_t T = T_INV * 4;
+    const uint32_t mloc = sloc + C.w * WS * 4;
+    const uint32_t m21 = sx + C.w * (uint32_t)(wt(2, 1, 9) * 4);
+    v4i lo, hi;
+    tw_load<T + TW4 * 4>(lo, C.a4, lds);
+    lds_wait<0>(x0, lo);
+    inv_pass1(x0, lo, K);
+    store_rows<4, 3, 0>(x0, mloc, lds);
+    gather_rows<4, 3, 0>(x0, sloc + C.f43, lds);
+    inv_pass1(x1, lo, K);
+    tw_load<T + TW3 * 4>(lo, hi, C.a3, lds);
+    store_rows<4, 3, 1>(x1, mloc, lds);
+    gather_rows<4, 3, 1>(x1, sloc + C.f43, lds);
+    lds_wait<15>(x0, lo, hi);
+    inv_pass8(x0, lo, hi, K);
+    store_rows<3, 2, 0>(x0, mloc, lds);
+    gather_rows<3, 2, 0>(x0, sloc + C.f32, lds);
+    lds_wait<15>(x1);
+    inv_pass8(x1, lo, hi, K);
+    tw_load<T + TW2 * 4>(lo, hi, C.a2, lds);
+    store_rows<3, 2, 1>(x1, mloc, lds);
+    gather_rows<3, 2, 1>(x1, sloc + C.f32, lds);
+    lds_wait<15>(x0, lo, hi);
+    inv_pass8(x0, lo, hi, K);
+    if constexpr (NB == 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    store_rows<2, 1, 0>(x0, m21, lds);
+    lds_wait<0>(x1);
+    inv_pass8(x1, lo, hi, K);
+    store_rows<2, 1, 1>(x1, m21, lds);
+    tw_load<T + TW1 * 4>(lo, hi, C.zero, lds);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    lds_load<2>(buf, x0, t);
-    lds_load<2>(buf + PFN, x1, t);
-    fwd_pass<true>(x0, psi, 8, t >> 4, K);
-    fwd_pass<true>(x1, psi, 8, t >> 4, K);
-    wave_sync();
-    lds_store<2>(buf, x0, t);
-    lds_store<2>(buf + PFN, x1, t);
-    wave_sync();
-    lds_load<3>(buf, x0, t);
-    lds_load<3>(buf + PFN, x1, t);
-    fwd_pass<true>(x0, psi, 64, t >> 1, K);
-    fwd_pass<true>(x1, psi, 64, t >> 1, K);
-    wave_sync();
-    lds_store<3>(buf, x0, t);
-    lds_store<3>(buf + PFN, x1, t);
-    wave_sync();
-    lds_load<4>(buf, x0, t);
-    lds_load<4>(buf + PFN, x1, t);
-    fwd_pass<false>(x0, psi, 128, t, K);
-    fwd_pass<false>(x1, psi, 128, t, K);
-}
-
-// inverse transform of two polynomials (no N^-1: folded into the BSK), L4 -> L1
-__device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], int32_t* buf, const int32_t* ipsi,
-                                         uint32_t t, const FastConst& K) {
-    inv_pass<false>(x0, ipsi, 128, t, K);
-    inv_pass<false>(x1, ipsi, 128, t, K);
-    wave_sync();
-    lds_store<4>(buf, x0, t);
-    lds_store<4>(buf + PFN, x1, t);
-    wave_sync();
-    lds_load<3>(buf, x0, t);
-    lds_load<3>(buf + PFN, x1, t);
-    inv_pass<true>(x0, ipsi, 64, t >> 1, K);
-    inv_pass<true>(x1, ipsi, 64, t >> 1, K);
-    wave_sync();
-    lds_store<3>(buf, x0, t);
-    lds_store<3>(buf + PFN, x1, t);
-    wave_sync();
-    lds_load<2>(buf, x0, t);
-    lds_load<2>(buf + PFN, x1, t);
-    inv_pass<true>(x0, ipsi, 8, t >> 4, K);
-    inv_pass<true>(x1, ipsi, 8, t >> 4, K);
-    wave_sync();
-    lds_store<2>(buf, x0, t);  // own half (b9 = wavefront)
-    lds_store<2>(buf + PFN, x1, t);
-    __syncthreads();
-    lds_load<1>(buf, x0, t);
-    lds_load<1>(buf + PFN, x1, t);
-    inv_pass<true>(x0, ipsi, 1, 0, K);
-    inv_pass<true>(x1, ipsi, 1, 0, K);
+    gather_rows<2, 1, 0>(x0, sx + C.f21, lds);
+    gather_rows<2, 1, 1>(x1, sx + C.f21, lds);
+    lds_wait<8>(x0, lo, hi);
+    inv_pass8(x0, lo, hi, K);
+    lds_wait<0>(x1);
+    inv_pass8(x1, lo, hi, K);
 }
 
 // MINW: minimum waves per SIMD requested from the register allocator.
 // ACC64: exact 64-bit sums over all 8 rows, one reduction per output (32 more VGPRs);
 //        otherwise every digit's row pair is reduced into a 32-bit sum.
 // CTS: ciphertexts per workgroup (a workgroup barrier then spans 2*CTS wavefronts).
-template <int MINW, bool ACC64, int CTS>
+// PF: BSK groups (of 4) whose loads are issued before the digit's forward NTT, so their
+//     latency hides behind it (16 VGPRs each); the rest are loaded when the MAC starts.
+// EXP: timing experiments (results invalid): 1 one BSK slice, 2 no BSK loads.
+// NB: exchange buffers per ciphertext (2: alternate, 1: smaller LDS footprint, more barriers).
+template <int MINW, bool ACC64, int CTS, int EXP = 0, int PF = 0, int NB = 2>
 __global__ void __launch_bounds__(TPC * CTS, MINW)
 k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                     const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -253,19 +416,27 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
     const uint32_t cl = __builtin_amdgcn_readfirstlane(tid / TPC), t = tid % TPC;
     const uint32_t ct = blockIdx.x * CTS + cl;
     const bool active = ct < B;
-    int32_t* buf = lds + T_WORDS + cl * BUF_WORDS;
-    const int32_t* psi = lds + T_PSI;
-    const int32_t* ipsi = lds + T_IPSI;
-    const char* mono = reinterpret_cast<const char*>(lds + T_MONO);
+    const uint32_t ctbase = (T_WORDS + cl * NB * XBUF) * 4;  // bytes, uniform
+
+    LaneCtx C;
+    C.w = __builtin_amdgcn_readfirstlane(t >> 6);
+    C.f12 = ld_lane<1, 2>(t), C.f23 = ld_lane<2, 3>(t), C.f34 = ld_lane<3, 4>(t);
+    C.f43 = ld_lane<4, 3>(t), C.f32 = ld_lane<3, 2>(t), C.f21 = ld_lane<2, 1>(t);
+    const uint32_t w6 = t >> 6;
+    C.a2 = ((((t >> 3) & 3) | (w6 << 2)) * 32);            // block i >> 7 in L2
+    C.a3 = (((t & 31) | (w6 << 5)) * 32);                  // block i >> 4 in L3
+    const uint32_t nslot = ((t >> 5) & 1) | ((t & 31) << 1) | (w6 << 6);  // i >> 3 in L4
+    C.a4 = nslot * 16;
+    C.zero = 0;
 
     uint64_t* g = acc_io + (size_t)(active ? ct : 0) * 2 * FN;
     const uint32_t Qh = (uint32_t)K.Q >> 1;
-    int32_t acc[2][8];  // centred canonical, [-(Q>>1)-1, Q>>1)
+    int32_t acc[2][8];  // L1, centred canonical, [-(Q>>1)-1, Q>>1)
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const uint64_t v0 = active ? g[p * FN + ix1(t, r)] : 0;
+            const uint64_t v0 = active ? g[p * FN + elem<1>(t, r)] : 0;
             const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
             acc[p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
         }
@@ -273,9 +444,9 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
 
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * (2 * FDG2 * 2 * FN * 4)), 0x00020000);
-    const uint32_t voff = t * 32;  // 8 consecutive words per lane in L4
-    // slot exponent of L4 slot 8t + r: e = 256 bitrev3(r) + et, et = 2 bitrev7(t) + 1
-    const uint32_t et = 2 * (__builtin_bitreverse32(t) >> 25) + 1;
+    const uint32_t voff = nslot * 32;  // 8 consecutive slots per lane in L4
+    // slot exponent of L4 slot 8 nslot + r: e = 256 bitrev3(r) + et, et = 2 bitrev7(nslot) + 1
+    const uint32_t et = 2 * (__builtin_bitreverse32(nslot) >> 25) + 1;
     const uint64_t* ap = a + (size_t)(active ? ct : 0) * n;
     const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;  // 2N = 2^11
     for (uint32_t i = 0; i < n; ++i) {
@@ -296,9 +467,12 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
                 }
 
         // BSK rows through a buffer resource: lane offset in a VGPR, row offset in an SGPR
-        const uint32_t round_off = i * (2 * FDG2 * 2 * FN * 4);
+        const uint32_t round_off = EXP == 1 ? 0u : i * (2 * FDG2 * 2 * FN * 4);
+        // five cross-wavefront exchanges per round alternate between the two buffers
+        const uint32_t par = NB == 2 ? (i & 1) : 0;
 #pragma unroll
         for (uint32_t l = 0; l < FDIG; ++l) {
+            const uint32_t sbuf = ctbase + ((par + l) & (NB - 1)) * XBUF * 4;
             // signed digit l of the centred c (rgsw-acc.cpp:83-109, carries included):
             //   d_l = (c + 64 (1 + 128 + ... + 128^(l-1))) >> 7l,  digit = sext7(d_l);
             //   the top digit |d_3| <= 33 is its own sext7, so one v_bfe_i32 serves all four
@@ -309,36 +483,50 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
                 x0[r] = __builtin_amdgcn_sbfe(acc[0][r] + kl, FLOGG * l, FLOGG);
                 x1[r] = __builtin_amdgcn_sbfe(acc[1][r] + kl, FLOGG * l, FLOGG);
             }
-            ntt_fwd2(x0, x1, buf, psi + opaque_zero(), t, K);
-            // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l)
+            // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l); group g = (key k, poly j)
+            v4i pw[4][4];
+            auto issue = [&](int g) {
+                const int k = g >> 1, j = g & 1;
+                const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;      // uniform
+                const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;  // uniform
+                if constexpr (EXP >= 2) {
+                    pw[g][0] = v4i{(int)s0, (int)s1, 3, 4};
+                    pw[g][1] = pw[g][0] + 1, pw[g][2] = pw[g][0] + 2, pw[g][3] = pw[g][0] + 3;
+                } else {
+                    pw[g][0] = ld_bsk(rsrc, voff, s0), pw[g][1] = ld_bsk(rsrc, voff + 16, s0);
+                    pw[g][2] = ld_bsk(rsrc, voff, s1), pw[g][3] = ld_bsk(rsrc, voff + 16, s1);
+                }
+            };
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+            for (int g = 0; g < PF; ++g) issue(g);
+            __builtin_amdgcn_sched_barrier(0);
+            ntt_fwd2<NB>(x0, x1, lds, sbuf, C, K);
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;      // uniform
-                    const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;  // uniform
-                    // one (key, poly) group of BSK words at a time: bounds the staging registers
-                    __builtin_amdgcn_sched_barrier(0);
-                    const v4i a0 = ld_bsk(rsrc, voff, s0), a1 = ld_bsk(rsrc, voff + 16, s0);
-                    const v4i b0 = ld_bsk(rsrc, voff, s1), b1 = ld_bsk(rsrc, voff + 16, s1);
-                    const int32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                    const int32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            for (int g = 0; g < 4; ++g) {
+                const int k = g >> 1, j = g & 1;
+                // groups not prefetched: one at a time, which bounds the staging registers
+                __builtin_amdgcn_sched_barrier(0);
+                if (g >= PF) issue(g);
+                const v4i a0 = pw[g][0], a1 = pw[g][1], b0 = pw[g][2], b1 = pw[g][3];
+                const int32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+                const int32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        if constexpr (ACC64) {
-                            s[k][j][r] = (int64_t)x0[r] * w0[r] + s[k][j][r];
-                            s[k][j][r] = (int64_t)x1[r] * w1[r] + s[k][j][r];
-                        } else {
-                            const int64_t T = (int64_t)x0[r] * w0[r] + (int64_t)x1[r] * w1[r];
-                            s32[k][j][r] += sredc(T, K);
-                        }
+                for (int r = 0; r < 8; ++r) {
+                    if constexpr (ACC64) {
+                        s[k][j][r] = (int64_t)x0[r] * w0[r] + s[k][j][r];
+                        s[k][j][r] = (int64_t)x1[r] * w1[r] + s[k][j][r];
+                    } else {
+                        const int64_t T = (int64_t)x0[r] * w0[r] + (int64_t)x1[r] * w1[r];
+                        s32[k][j][r] += sredc(T, K);
                     }
                 }
+            }
         }
 
         // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1)
         const uint32_t b4 = (et * ai) << 2;       // byte offsets into the 2N-entry table
         const uint32_t st4 = (ai << 10) & 8191;   // 256 * ai * 4 mod 8192
+        const char* mono = reinterpret_cast<const char*>(lds + T_MONO);
         int32_t S0[8], S1[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -356,7 +544,9 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
             S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
             S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
         }
-        ntt_inv2(S0, S1, buf, ipsi + opaque_zero(), t, K);
+        ntt_inv2<NB>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
+                     ctbase + ((par + FDIG) & (NB - 1)) * XBUF * 4,
+                      C, K);
         // acc <- centred canonical (acc + S): u = acc + S + (Q>>1) + 1 + 4Q in (0, 8Q)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -372,7 +562,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
         // acc0 transposed (X -> X^-1, poly.cpp:762-770): out[(N-k) mod N] = -acc0[k]
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const uint32_t k = ix1(t, r);
+            const uint32_t k = elem<1>(t, r);
             const uint32_t v = (uint32_t)(acc[0][r] < 0 ? acc[0][r] + K.Q : acc[0][r]);
             const uint32_t v1 = (uint32_t)(acc[1][r] < 0 ? acc[1][r] + K.Q : acc[1][r]);
             g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
@@ -381,7 +571,8 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
     }
 }
 
-// generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies
+// generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies, twiddles
+// packed per pass (see the table-block comment above)
 __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t words, const uint32_t* __restrict__ psi,
                             const uint32_t* __restrict__ ipsi, const uint32_t* __restrict__ mono,
                             int32_t* __restrict__ out) {
@@ -391,9 +582,24 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
         return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
     };
     if (idx < words) out[T_WORDS + idx] = mont(bsk[idx]);
-    if (idx < FN) {
-        out[T_PSI + idx] = mont(psi[idx]);
-        out[T_IPSI + idx] = mont(ipsi[idx]);
+    if (idx < TW_WORDS) {
+        // which packed entry is idx?
+        uint32_t m, c, e;
+        if (idx < TW2) m = 1, c = 0, e = idx;
+        else if (idx < TW3) m = 8, c = (idx - TW2) >> 3, e = (idx - TW2) & 7;
+        else if (idx < TW4) m = 64, c = (idx - TW3) >> 3, e = (idx - TW3) & 7;
+        else m = 0, c = 0, e = 0;
+        int32_t f = 0, iv = 0;
+        if (m == 0) {
+            f = mont(psi[512 + idx - TW4]);
+            iv = mont(ipsi[512 + idx - TW4]);
+        } else if (e < 7) {
+            const uint32_t k = e == 0 ? m + c : e < 3 ? 2 * m + 2 * c + (e - 1) : 4 * m + 4 * c + (e - 3);
+            f = mont(psi[k]);
+            iv = mont(ipsi[k]);
+        }
+        out[T_FWD + idx] = f;
+        out[T_INV + idx] = iv;
     }
     if (idx < 2 * FN) out[T_MONO + idx] = mont(mono[idx]);
 }
@@ -441,9 +647,9 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         const char* e = std::getenv("TFHE_FAST_VARIANT");
         return e ? std::atoi(e) : 0;
     }();
-    auto launch = [&](auto kern, int cts) {
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts));
-        hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts), s, K, P.n,
+    auto launch = [&](auto kern, int cts, int nb = 2) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts, nb));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts, nb), s, K, P.n,
                            loga, tabs, bsk, a, acc, (uint32_t)B);
     };
     switch (variant) {
@@ -451,7 +657,20 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 2: launch(k_blind_rotate_fast<3, true, 1>, 1); break;
         case 3: launch(k_blind_rotate_fast<2, true, 2>, 2); break;
         case 4: launch(k_blind_rotate_fast<3, false, 1>, 1); break;
-        default: launch(k_blind_rotate_fast<3, true, 2>, 2); break;
+        case 9: launch(k_blind_rotate_fast<3, true, 2, 1>, 2); break;  // timing experiment: one BSK slice
+        case 10: launch(k_blind_rotate_fast<3, true, 2, 2>, 2); break; // timing experiment: no BSK loads
+        case 13: launch(k_blind_rotate_fast<2, true, 2, 0, 4>, 2); break;
+        case 14: launch(k_blind_rotate_fast<3, false, 2, 0, 4>, 2); break;
+        case 15: launch(k_blind_rotate_fast<3, true, 2, 0, 2>, 2); break;
+        case 16: launch(k_blind_rotate_fast<2, true, 2, 0, 2>, 2); break;
+        case 17: launch(k_blind_rotate_fast<4, false, 2, 0, 0, 1>, 2, 1); break;
+        case 18: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1); break;
+        case 19: launch(k_blind_rotate_fast<4, true, 2, 0, 0, 1>, 2, 1); break;
+        case 20: launch(k_blind_rotate_fast<3, true, 2, 0, 0, 1>, 2, 1); break;
+        case 21: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 2>, 2, 2); break;
+        // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
+        // row sums, half of each digit's BSK prefetched behind its forward NTT
+        default: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1); break;
     }
     return hipGetLastError();
 }
