@@ -54,11 +54,13 @@ constexpr int TPC = 128;  // threads per ciphertext
 
 // Table block (int32 words, centred Montgomery form).  Twiddles are packed per radix-8
 // pass so that a lane fetches the 7 twiddles of its block with two ds_read_b128:
-//   TW1[8]        pass on (b9 b8 b7), one block
-//   TW2[8][8]     pass on (b6 b5 b4), block c = i >> 7
-//   TW3[64][8]    pass on (b3 b2 b1), block c = i >> 4
-//   TW4[512]      single stage on b0: psi[512 + (i >> 1)]
-// block c of a pass with stride m holds psi[m+c], psi[2m+2c], psi[2m+2c+1], psi[4m+4c .. +3], 0.
+//   TW1  [lo 4][hi 4]           pass on (b9 b8 b7), one block
+//   TW2  [lo 8][4] [hi 8][4]    pass on (b6 b5 b4), block c = i >> 7
+//   TW3  [lo 64][4] [hi 64][4]  pass on (b3 b2 b1), block c = i >> 4
+//   TW4  [128 lanes][4]         single stage on b0: psi[512 + (i >> 1)], in L4 lane order
+// block c of a pass with stride m: lo = psi[m+c], psi[2m+2c], psi[2m+2c+1], psi[4m+4c],
+// hi = psi[4m+4c+1 .. +3], 0.  Separate lo/hi arrays and the lane-ordered TW4 keep every
+// 16-lane ds_read_b128 group on one 256-byte bank row (no conflicts).
 // Forward (psi) and inverse (psi^-1) sets, then mono[2N] = psi^k - 1.
 constexpr uint32_t TW1 = 0, TW2 = 8, TW3 = 72, TW4 = 584, TW_WORDS = 1096;
 constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS = 2 * TW_WORDS + 2 * FN;
@@ -196,11 +198,11 @@ __device__ __forceinline__ void gather_rows(int32_t (&x)[8], uint32_t base, cons
         : "memory");
 }
 // packed twiddles of one block: two ds_read_b128 (one for the single-stage pass)
-template <uint32_t OFF>
+template <uint32_t OFF, uint32_t NBLK>
 __device__ __forceinline__ void tw_load(v4i& lo, v4i& hi, uint32_t addr, const int32_t* lds) {
     asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b128 %1, %2 offset:%5"
                  : "=&v"(lo), "=&v"(hi)
-                 : "v"(addr), "s"(lds), "i"(OFF), "i"(OFF + 16)
+                 : "v"(addr), "s"(lds), "i"(OFF), "i"(OFF + NBLK * 16)
                  : "memory");
 }
 template <uint32_t OFF>
@@ -310,7 +312,7 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
     const uint32_t m12 = sbuf + C.w * (uint32_t)(wt(1, 2, 6) * 4);  // uniform
     const uint32_t mloc = sbuf + C.w * WS * 4;                      // uniform: own region
     v4i lo, hi;
-    tw_load<T + TW1 * 4>(lo, hi, C.zero, lds);
+    tw_load<T + TW1 * 4, 1>(lo, hi, C.zero, lds);
     lds_wait<0>(lo, hi);
     fwd_pass8(x0, lo, hi, K);
     if constexpr (NB == 1) {  // the other wavefront has finished reading this buffer
@@ -322,7 +324,7 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
     store_rows<1, 2, 1>(x1, m12, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    tw_load<T + TW2 * 4>(lo, hi, C.a2, lds);
+    tw_load<T + TW2 * 4, 8>(lo, hi, C.a2, lds);
     gather_rows<1, 2, 0>(x0, sbuf + C.f12, lds);
     gather_rows<1, 2, 1>(x1, sbuf + C.f12, lds);
     lds_wait<8>(x0, lo, hi);
@@ -331,7 +333,7 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
     gather_rows<2, 3, 0>(x0, sbuf + C.f23, lds);
     lds_wait<15>(x1);
     fwd_pass8(x1, lo, hi, K);
-    tw_load<T + TW3 * 4>(lo, hi, C.a3, lds);
+    tw_load<T + TW3 * 4, 64>(lo, hi, C.a3, lds);
     store_rows<2, 3, 1>(x1, mloc, lds);
     gather_rows<2, 3, 1>(x1, sbuf + C.f23, lds);
     lds_wait<15>(x0, lo, hi);
@@ -364,7 +366,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     store_rows<4, 3, 0>(x0, mloc, lds);
     gather_rows<4, 3, 0>(x0, sloc + C.f43, lds);
     inv_pass1(x1, lo, K);
-    tw_load<T + TW3 * 4>(lo, hi, C.a3, lds);
+    tw_load<T + TW3 * 4, 64>(lo, hi, C.a3, lds);
     store_rows<4, 3, 1>(x1, mloc, lds);
     gather_rows<4, 3, 1>(x1, sloc + C.f43, lds);
     lds_wait<15>(x0, lo, hi);
@@ -373,7 +375,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     gather_rows<3, 2, 0>(x0, sloc + C.f32, lds);
     lds_wait<15>(x1);
     inv_pass8(x1, lo, hi, K);
-    tw_load<T + TW2 * 4>(lo, hi, C.a2, lds);
+    tw_load<T + TW2 * 4, 8>(lo, hi, C.a2, lds);
     store_rows<3, 2, 1>(x1, mloc, lds);
     gather_rows<3, 2, 1>(x1, sloc + C.f32, lds);
     lds_wait<15>(x0, lo, hi);
@@ -386,7 +388,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     lds_wait<0>(x1);
     inv_pass8(x1, lo, hi, K);
     store_rows<2, 1, 1>(x1, m21, lds);
-    tw_load<T + TW1 * 4>(lo, hi, C.zero, lds);
+    tw_load<T + TW1 * 4, 1>(lo, hi, C.zero, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     gather_rows<2, 1, 0>(x0, sx + C.f21, lds);
@@ -423,10 +425,10 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
     C.f12 = ld_lane<1, 2>(t), C.f23 = ld_lane<2, 3>(t), C.f34 = ld_lane<3, 4>(t);
     C.f43 = ld_lane<4, 3>(t), C.f32 = ld_lane<3, 2>(t), C.f21 = ld_lane<2, 1>(t);
     const uint32_t w6 = t >> 6;
-    C.a2 = ((((t >> 3) & 3) | (w6 << 2)) * 32);            // block i >> 7 in L2
-    C.a3 = (((t & 31) | (w6 << 5)) * 32);                  // block i >> 4 in L3
+    C.a2 = ((((t >> 3) & 3) | (w6 << 2)) * 16);            // block i >> 7 in L2
+    C.a3 = (((t & 31) | (w6 << 5)) * 16);                  // block i >> 4 in L3
     const uint32_t nslot = ((t >> 5) & 1) | ((t & 31) << 1) | (w6 << 6);  // i >> 3 in L4
-    C.a4 = nslot * 16;
+    C.a4 = t * 16;                                          // TW4 is stored in lane order
     C.zero = 0;
 
     uint64_t* g = acc_io + (size_t)(active ? ct : 0) * 2 * FN;
@@ -583,23 +585,24 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
     };
     if (idx < words) out[T_WORDS + idx] = mont(bsk[idx]);
     if (idx < TW_WORDS) {
-        // which packed entry is idx?
-        uint32_t m, c, e;
-        if (idx < TW2) m = 1, c = 0, e = idx;
-        else if (idx < TW3) m = 8, c = (idx - TW2) >> 3, e = (idx - TW2) & 7;
-        else if (idx < TW4) m = 64, c = (idx - TW3) >> 3, e = (idx - TW3) & 7;
-        else m = 0, c = 0, e = 0;
-        int32_t f = 0, iv = 0;
-        if (m == 0) {
-            f = mont(psi[512 + idx - TW4]);
-            iv = mont(ipsi[512 + idx - TW4]);
-        } else if (e < 7) {
-            const uint32_t k = e == 0 ? m + c : e < 3 ? 2 * m + 2 * c + (e - 1) : 4 * m + 4 * c + (e - 3);
-            f = mont(psi[k]);
-            iv = mont(ipsi[k]);
+        // which packed entry is idx?  e = position within the block (0..3 lo, 4..7 hi)
+        uint32_t k = 0;
+        bool zero = false;
+        if (idx < TW4) {
+            uint32_t m, nblk, j;
+            if (idx < TW2) m = 1, nblk = 1, j = idx;
+            else if (idx < TW3) m = 8, nblk = 8, j = idx - TW2;
+            else m = 64, nblk = 64, j = idx - TW3;
+            const uint32_t hi = j >= 4 * nblk, c = (j % (4 * nblk)) >> 2, e = (hi ? 4 : 0) + (j & 3);
+            zero = e == 7;
+            k = e == 0 ? m + c : e < 3 ? 2 * m + 2 * c + (e - 1) : 4 * m + 4 * c + (e - 3);
+        } else {
+            const uint32_t j = idx - TW4, t = j >> 2, q = j & 3;
+            const uint32_t nslot = ((t >> 5) & 1) | ((t & 31) << 1) | ((t >> 6) << 6);
+            k = 512 + 4 * nslot + q;
         }
-        out[T_FWD + idx] = f;
-        out[T_INV + idx] = iv;
+        out[T_FWD + idx] = zero ? 0 : mont(psi[k]);
+        out[T_INV + idx] = zero ? 0 : mont(ipsi[k]);
     }
     if (idx < 2 * FN) out[T_MONO + idx] = mont(mono[idx]);
 }
