@@ -17,8 +17,10 @@ Extra JSON fields:
                 stream; algorithmic bytes per SURVEY.md 8(d) (B_alg = BSK key
                 stream per bootstrap + KS gather + LWE I/O, no cross-ciphertext
                 reuse); traffic from rocprofv3 PMC if --pmc-json is given.
-  valu          the real bound: modular multiplies/s vs the measured gfx950
-                Shoup-modmul peak (profiles/r01_valu_rates.txt).
+  valu          the real bound (integer VALU issue): modular
+                multiplies/s, and the VALU issue fraction = PMC-measured VALU
+                instructions x 4 cycles (wave64 integer multiply/add issue,
+                profiles/r01_valu_rates.txt) / (SIMDs x clock x kernel time).
   cpu_baseline  the C oracle (oracle/tfhe_oracle.c, OpenMP) on a bounded sample
                 of the same workload on this host's cores (rank 0, N=1 only).
 """
@@ -37,7 +39,8 @@ sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
 
 MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
-MODMUL_PEAK = 7.66e12              # measured Shoup u32 modmul/s, profiles/r01_valu_rates.txt
+VALU_CYCLES = 4                    # cycles per wave64 VALU instruction (mul/mad class; profiles/r01_valu_rates.txt)
+CLOCK_HZ = 2.4e9                   # MI355X peak engine clock
 
 
 def parse():
@@ -218,12 +221,15 @@ def main():
     br_ms = e0.elapsed_time(e1) / args.kernel_reps
     balg, bsk_bytes = b_alg_per_bootstrap(p)
     achieved = balg * B / (br_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, valu_insts = None, None
     if os.path.exists(args.pmc_json):
         try:
-            traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(args.pmc_json))
+            if pmc.get("units_per_launch") == B:
+                traffic = pmc.get("hbm_bytes_per_launch")
+                valu_insts = pmc.get("sq_insts_valu_per_launch")
         except Exception:
-            traffic = None
+            traffic = valu_insts = None
     mm = modmuls_per_bootstrap(p)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
@@ -232,9 +238,14 @@ def main():
                 "note": "B_alg per SURVEY.md 8(d): key-stream bytes with no cross-ciphertext reuse; frac > 1 means "
                         "the 64 MiB BSK is re-served from L2/MALL across the batch. The kernel is VALU-bound: "
                         "see 'valu'."}
-    valu = {"modmul_per_bootstrap": mm, "achieved_modmul_per_s": round(mm * B / (br_ms * 1e-3), 1),
-            "peak_modmul_per_s": MODMUL_PEAK,
-            "frac": round(mm * B / (br_ms * 1e-3) / MODMUL_PEAK, 3)}
+    simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+    valu = {"bound": "valu-int", "modmul_per_bootstrap": mm,
+            "achieved_modmul_per_s": round(mm * B / (br_ms * 1e-3), 1),
+            "valu_instr_per_launch": valu_insts,
+            "issue_frac": None if valu_insts is None else
+            round(valu_insts * VALU_CYCLES / (simds * CLOCK_HZ * br_ms * 1e-3), 3),
+            "note": "issue_frac = PMC SQ_INSTS_VALU x 4 cycles / (4 SIMDs/CU x CUs x 2.4 GHz x kernel time), "
+                    "from " + os.path.relpath(args.pmc_json, ROOT)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

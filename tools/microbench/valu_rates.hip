@@ -158,6 +158,28 @@ __global__ void k_modmul_shoup(uint32_t* out, int iters, uint32_t seed) {
     for (int k = 0; k < 8; ++k) s ^= x[k];
     out[t] = s;
 }
+// signed Montgomery (R = 2^32) as in blind_rotate_fast.hip: v_mad_i64_i32, v_mul_lo_u32, v_mad_i64_i32
+__global__ void k_modmul_smont(int32_t* out, int iters, uint32_t seed) {
+    int32_t t = threadIdx.x + blockIdx.x * blockDim.x;
+    const int32_t Q = 134215681, nQ = -Q, w = 12345677;
+    uint32_t inv = 1;
+    for (int it = 0; it < 5; ++it) inv *= 2u - (uint32_t)Q * inv;
+    int32_t x[8];
+    for (int k = 0; k < 8; ++k) x[k] = (int32_t)((seed + t * 8 + k) % (uint32_t)Q) - Q / 2;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t T = (int64_t)x[k] * w;
+                const int32_t m = (int32_t)((uint32_t)T * inv);
+                x[k] = (int32_t)(((int64_t)m * nQ + T) >> 32);
+            }
+    }
+    int32_t s = 0;
+    for (int k = 0; k < 8; ++k) s ^= x[k];
+    out[t] = s;
+}
 __global__ void k_modmul_barrett(uint32_t* out, int iters, uint32_t seed) {
     uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
     const uint32_t Q = 134215681u;
@@ -245,6 +267,7 @@ int main() {
     // whole modmuls: rate reported as modmul/s (lane), fraction vs fp32 lane rate = 1/slots
     run<uint32_t>("modmul_shoup_u32", k_modmul_shoup, ops, peak);
     run<uint32_t>("modmul_barrett_u32", k_modmul_barrett, ops, peak);
+    run<int32_t>("modmul_smont_i32", k_modmul_smont, ops, peak);
     run<double>("modmul_f64_centred", k_modmul_f64, ops, peak);
     return 0;
 }

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSV output for one kernel into per-launch HBM bytes.
 
-Usage: pmc_summary.py KERNEL_SUBSTRING FETCH_DIR WRITE_DIR OUT_JSON
+Usage: pmc_summary.py KERNEL_SUBSTRING FETCH_DIR WRITE_DIR OUT_JSON [MIX_DIR]
+MIX_DIR (optional): a pass with SQ_INSTS_VALU / SQ_INSTS_LDS / SQ_WAVES, recorded per launch
+(bench.py turns SQ_INSTS_VALU into the VALU issue fraction).
 FETCH_SIZE/WRITE_SIZE are KiB (TCC_EA0_RDREQ/WRREQ based).  Per
 MI355X_MICROARCH.md 'HBM', gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide
 (16 B/lane) coalesced stream; other access widths are uncalibrated, so both the
@@ -30,11 +32,18 @@ def main():
     kname, fdir, wdir, out = sys.argv[1:5]
     fetch, nf = per_launch(rows(fdir), kname, "FETCH_SIZE")
     write, nw = per_launch(rows(wdir), kname, "WRITE_SIZE")
-    res = {"kernel": kname, "launches": [nf, nw], "fetch_kib_raw": fetch, "write_kib": write}
+    res = {"kernel": kname, "launches": [nf, nw], "fetch_kib_raw": fetch, "write_kib": write,
+           "units_per_launch": int(os.environ.get("PMC_UNITS", "8192"))}  # bench.py's default batch
     if fetch is not None and write is not None:
         res["hbm_bytes_per_launch_raw"] = (fetch + write) * 1024
         res["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
         res["correction"] = "read side x2 per MI355X_MICROARCH.md HBM section (wide-stream calibration)"
+    if len(sys.argv) > 5:
+        mix = rows(sys.argv[5])
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_LDS_BANK_CONFLICT"):
+            v, _ = per_launch(mix, kname, c)
+            if v is not None:
+                res[c.lower() + "_per_launch"] = v
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
