@@ -671,6 +671,7 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 19: launch(k_blind_rotate_fast<4, true, 2, 0, 0, 1>, 2, 1); break;
         case 20: launch(k_blind_rotate_fast<3, true, 2, 0, 0, 1>, 2, 1); break;
         case 21: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 2>, 2, 2); break;
+        case 22: launch(k_blind_rotate_fast<3, true, 1, 0, 2, 1>, 1, 1); break;
         // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
         // row sums, half of each digit's BSK prefetched behind its forward NTT
         default: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1); break;
