@@ -98,8 +98,13 @@ struct Scratch {
     uint64_t* ext = nullptr;  // [cap][N+1]
     uint64_t* lwe[6] = {};    // [cap][n+1] each
     size_t cap = 0;
+    uint64_t* io = nullptr;   // host-array staging: in1 | in2 | out
+    size_t io_words = 0;
 };
 
+// A device holds two (stream, scratch) lanes: host-array calls alternate sub-batches
+// between them so PCIe copies of one overlap the kernels of the other.  Device-pointer
+// entry points use lane 0 (or the caller's stream).
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
@@ -107,6 +112,8 @@ struct Device {
     void* bsk_fast = nullptr;
     Scratch sc;
     DevTables tables{};
+    hipStream_t stream2 = nullptr;  // lane 1
+    Scratch sc2;
 };
 
 }  // namespace
@@ -266,11 +273,16 @@ void free_device(Device& d) {
     if (d.stream) hipStreamSynchronize(d.stream);
     hipFree(d.arena);
     hipFree(d.bsk_fast);
-    hipFree(d.sc.acc);
-    hipFree(d.sc.a);
-    hipFree(d.sc.ext);
-    for (auto* p : d.sc.lwe) hipFree(p);
+    if (d.stream2) hipStreamSynchronize(d.stream2);
+    for (Scratch* sc : {&d.sc, &d.sc2}) {
+        hipFree(sc->acc);
+        hipFree(sc->a);
+        hipFree(sc->ext);
+        for (auto* p : sc->lwe) hipFree(p);
+        hipFree(sc->io);
+    }
     if (d.stream) hipStreamDestroy(d.stream);
+    if (d.stream2) hipStreamDestroy(d.stream2);
     d = Device{};
     d.id = -1;
 }
@@ -283,12 +295,24 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     hipFree(d.sc.a);
     hipFree(d.sc.ext);
     for (auto*& q : d.sc.lwe) hipFree(q), q = nullptr;
+    uint64_t* io = d.sc.io;
+    const size_t io_words = d.sc.io_words;
     d.sc = Scratch{};
+    d.sc.io = io, d.sc.io_words = io_words;
     HCHECK(hipMalloc(&d.sc.acc, cap * 2 * p.N * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.a, cap * p.n * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.ext, cap * (p.N + 1) * sizeof(uint64_t)));
     for (auto*& q : d.sc.lwe) HCHECK(hipMalloc(&q, cap * (p.n + 1) * sizeof(uint64_t)));
     d.sc.cap = cap;
+    return TFHE_OK;
+}
+
+tfhe_status ensure_io(Device& d, size_t words) {
+    if (words <= d.sc.io_words) return TFHE_OK;
+    hipFree(d.sc.io);
+    d.sc.io = nullptr, d.sc.io_words = 0;
+    HCHECK(hipMalloc(&d.sc.io, words * sizeof(uint64_t)));
+    d.sc.io_words = words;
     return TFHE_OK;
 }
 
@@ -502,38 +526,62 @@ tfhe_status for_each_shard(tfhe_ctx* c, size_t B, F&& body) {
     return TFHE_OK;
 }
 
-// Generic chunked runner: in-arrays are [B][in_words] (up to 2), out [B][out_words].
+// Host-array runner: in-arrays are [B][in_words] (up to 2), out [B][out_words].  Each
+// device's shard is cut into sub-batches that alternate between the device's two lanes:
+// sub-batch k's H2D copy and kernels are queued on its lane before the host waits for
+// sub-batch k-1's D2H, so the PCIe traffic of one overlaps the kernels of the other.
+// op(lane, in1, in2, out, count, index of the first ciphertext).
+constexpr size_t kMinSub = 1536;  // below this a sub-batch no longer fills the GPU
 template <typename Op>
 tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
                           uint64_t* out, size_t wo, Op&& op) {
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        const size_t chunk = std::min(cnt, c->max_chunk);
-        SCHECK(ensure_scratch(c, d, chunk));
-        // staging buffers for inputs/outputs live in lwe[...] slots reserved by the caller's op
-        uint64_t *din1 = nullptr, *din2 = nullptr, *dout = nullptr;
-        const size_t need1 = chunk * w1 * 8, need2 = chunk * w2 * 8, needo = chunk * wo * 8;
-        HCHECK(hipMalloc(&din1, std::max<size_t>(need1, 8)));
-        if (in2) HCHECK(hipMalloc(&din2, std::max<size_t>(need2, 8)));
-        HCHECK(hipMalloc(&dout, std::max<size_t>(needo, 8)));
+        static const size_t max_parts = [] {
+            const char* e = std::getenv("TFHE_HOST_PARTS");
+            return e ? std::max(1, std::atoi(e)) : 1;  // measured: splitting loses more kernel efficiency than it hides
+        }();
+        const size_t parts = cnt >= 2 * kMinSub ? std::min<size_t>(max_parts, cnt / kMinSub) : 1;
+        const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
+        Device lane[2] = {d, d};
+        lane[1].stream = d.stream2, lane[1].sc = d.sc2;
+        const int nl = parts > 1 ? 2 : 1;
+        const size_t w_in2 = in2 ? w2 : 0;
         tfhe_status st = TFHE_OK;
-        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
-            const size_t b = std::min(chunk, lo + cnt - off);
-            if (hipMemcpyAsync(din1, in1 + off * w1, b * w1 * 8, hipMemcpyHostToDevice, d.stream) != hipSuccess ||
-                (in2 && hipMemcpyAsync(din2, in2 + off * w2, b * w2 * 8, hipMemcpyHostToDevice, d.stream) !=
+        for (int l = 0; l < nl && st == TFHE_OK; ++l) {
+            st = ensure_scratch(c, lane[l], sub);
+            if (st == TFHE_OK) st = ensure_io(lane[l], sub * (w1 + w_in2 + wo));
+        }
+        d.sc = lane[0].sc;  // keep what was (re)allocated
+        d.sc2 = lane[1].sc;
+        if (st != TFHE_OK) return st;
+        auto d2h = [&](int l, size_t off, size_t b) -> tfhe_status {
+            const uint64_t* dout = lane[l].sc.io + sub * (w1 + w_in2);
+            if (hipMemcpyAsync(out + off * wo, dout, b * wo * 8, hipMemcpyDeviceToHost, lane[l].stream) != hipSuccess ||
+                hipStreamSynchronize(lane[l].stream) != hipSuccess)
+                return fail(TFHE_ERR_DEVICE, std::string("D2H/sync failed: ") + hipGetErrorString(hipGetLastError()));
+            return TFHE_OK;
+        };
+        size_t prev_off = 0, prev_b = 0;
+        int prev_l = -1;
+        for (size_t k = 0, off = lo; off < lo + cnt && st == TFHE_OK; ++k, off += sub) {
+            const int l = (int)(k % nl);
+            const size_t b = std::min(sub, lo + cnt - off);
+            Device& L = lane[l];
+            uint64_t *din1 = L.sc.io, *din2 = in2 ? L.sc.io + sub * w1 : nullptr, *dout = L.sc.io + sub * (w1 + w_in2);
+            if (hipMemcpyAsync(din1, in1 + off * w1, b * w1 * 8, hipMemcpyHostToDevice, L.stream) != hipSuccess ||
+                (in2 && hipMemcpyAsync(din2, in2 + off * w2, b * w2 * 8, hipMemcpyHostToDevice, L.stream) !=
                             hipSuccess)) {
                 st = fail(TFHE_ERR_DEVICE, "H2D copy failed");
                 break;
             }
-            st = op(d, din1, din2, dout, b);
+            st = op(L, din1, din2, dout, b, off);
             if (st != TFHE_OK) break;
-            if (hipMemcpyAsync(out + off * wo, dout, b * wo * 8, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
-                hipStreamSynchronize(d.stream) != hipSuccess)
-                st = fail(TFHE_ERR_DEVICE, std::string("D2H/sync failed: ") + hipGetErrorString(hipGetLastError()));
+            if (prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
+            prev_l = l, prev_off = off, prev_b = b;
         }
+        if (st == TFHE_OK && prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
         hipStreamSynchronize(d.stream);
-        hipFree(din1);
-        hipFree(din2);
-        hipFree(dout);
+        if (d.stream2) hipStreamSynchronize(d.stream2);
         return st;
     });
 }
@@ -620,6 +668,8 @@ tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk
         Device& d = c->devs[g];
         HCHECK(hipSetDevice(d.id));
         HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+        HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
         HCHECK(hipMalloc(&d.arena, bytes));
         if (g == 0) {
             HCHECK(hipMemcpy(d.arena, img.data(), bytes, hipMemcpyHostToDevice));
@@ -644,6 +694,7 @@ tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, cons
     d.id = device;
     HCHECK(hipSetDevice(device));
     HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
     HCHECK(hipMalloc(&d.arena, bytes));
     HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
     SCHECK(finish_device(c.get(), d));
@@ -718,7 +769,7 @@ tfhe_status tfhe_mkm_switch(tfhe_ctx* c, size_t B, const uint64_t* ct_ext, uint6
     if (!ct_ext || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
     const tfhe_params& p = c->p;
     return run_lwe_batch(c, B, ct_ext, p.N + 1, nullptr, 0, out, p.n + 1,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                              return dev_mkm(c, d, i1, fmod, o, b);
                          });
 }
@@ -744,7 +795,7 @@ tfhe_status tfhe_eval_bin_gate(tfhe_ctx* c, int gate, size_t B, const uint64_t* 
     if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
     const size_t w = c->p.n + 1;
     return run_lwe_batch(c, B, ct1, w, ct2, w, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b) {
+                         [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
                              return dev_gate(c, d, gate, i1, i2, q, o, b);
                          });
 }
@@ -773,34 +824,27 @@ tfhe_status tfhe_eval_func(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t q
     const int prop = check_input_function(lut, q, q);
     const size_t w = c->p.n + 1;
     const uint64_t stride = per_ct_lut ? q : 0;
-    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        uint64_t* d_lut = nullptr;
-        const size_t lut_words = per_ct_lut ? cnt * q : q;
-        HCHECK(hipMalloc(&d_lut, lut_words * 8));
-        HCHECK(hipMemcpy(d_lut, lut + (per_ct_lut ? lo * q : 0), lut_words * 8, hipMemcpyHostToDevice));
-        const size_t chunk = std::min(cnt, c->max_chunk);
-        tfhe_status st = ensure_scratch(c, d, chunk);
-        uint64_t *din = nullptr, *dout = nullptr;
-        if (st == TFHE_OK && (hipMalloc(&din, chunk * w * 8) != hipSuccess || hipMalloc(&dout, chunk * w * 8) != hipSuccess))
-            st = fail(TFHE_ERR_OUT_OF_MEMORY, "staging allocation failed");
-        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
-            const size_t b = std::min(chunk, lo + cnt - off);
-            if (hipMemcpyAsync(din, ct + off * w, b * w * 8, hipMemcpyHostToDevice, d.stream) != hipSuccess) {
-                st = fail(TFHE_ERR_DEVICE, "H2D failed");
-                break;
-            }
-            st = dev_func(c, d, prop, din, q, d_lut + (per_ct_lut ? (off - lo) * q : 0), stride, dout, b);
-            if (st != TFHE_OK) break;
-            if (hipMemcpyAsync(out + off * w, dout, b * w * 8, hipMemcpyDeviceToHost, d.stream) != hipSuccess ||
-                hipStreamSynchronize(d.stream) != hipSuccess)
-                st = fail(TFHE_ERR_DEVICE, "D2H/sync failed");
-        }
-        hipStreamSynchronize(d.stream);
-        hipFree(din);
-        hipFree(dout);
-        hipFree(d_lut);
-        return st;
-    });
+    // LUTs go to every device once (all of them when per ciphertext), then the batch runs
+    // through the pipelined host-array runner
+    const size_t D = c->devs.size();
+    std::vector<uint64_t*> d_lut(D, nullptr);
+    const size_t lut_words = per_ct_lut ? B * q : q;
+    tfhe_status st = TFHE_OK;
+    for (size_t g = 0; g < D && st == TFHE_OK; ++g) {
+        if (hipSetDevice(c->devs[g].id) != hipSuccess || hipMalloc(&d_lut[g], lut_words * 8) != hipSuccess ||
+            hipMemcpy(d_lut[g], lut, lut_words * 8, hipMemcpyHostToDevice) != hipSuccess)
+            st = fail(TFHE_ERR_OUT_OF_MEMORY, "LUT upload failed");
+    }
+    if (st == TFHE_OK)
+        st = run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                           [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t off) {
+                               size_t g = 0;
+                               while (c->devs[g].id != d.id) ++g;
+                               return dev_func(c, d, prop, i1, q, d_lut[g] + (per_ct_lut ? off * q : 0), stride, o, b);
+                           });
+    for (size_t g = 0; g < D; ++g)
+        if (d_lut[g]) hipSetDevice(c->devs[g].id), hipFree(d_lut[g]);
+    return st;
 }
 
 tfhe_status tfhe_eval_floor(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint32_t roundbits,
@@ -810,7 +854,7 @@ tfhe_status tfhe_eval_floor(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t 
     if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
     const size_t w = c->p.n + 1;
     return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                              return dev_floor(c, d, i1, mod, roundbits, o, b);
                          });
 }
@@ -821,7 +865,7 @@ tfhe_status tfhe_eval_sign(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t m
     if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
     const size_t w = c->p.n + 1;
     return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b) {
+                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                              return dev_sign(c, d, i1, mod, o, b);
                          });
 }

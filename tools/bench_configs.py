@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Throughput of the other SURVEY.md 8(d) configurations on one MI355X (C3, C4, C5a, C5b).
+
+bench.py measures the headline C2 (STD128 NAND, inputs resident in HBM).  This script
+times the host-array entry points (EvalFunc / EvalBinGate / EvalSign: PCIe transfers
+included) with synthetic keys and random ciphertexts, counting bootstraps with the
+engine's own counter (tfhe_info.bootstraps).  One JSON line per configuration.
+Usage: python3 tools/bench_configs.py [C3 C4 C5a C5b] [--reps 2]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["C3", "C4", "C5a", "C5b"])
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    import tfhe_amd
+    from tfhe_amd import capi
+
+    for name in args.configs:
+        if name == "C2host":  # the headline workload through the host-array API (PCIe included)
+            p = capi.params_from_set("STD128")
+            B, op = 8192, "EvalBinGate(NAND)"
+        elif name == "C3":      # STD128 arbFunc logQ=12 throw=1, EvalFunc with an arbitrary LUT, B=4096
+            p = capi.params_from_logq("STD128", True, 12, 0, 0, 1)
+            B, op = 4096, "EvalFunc(x^3 mod 8)"
+        elif name == "C4":    # STD192 NAND (8192 per GPU of the 65536-gate, 8-GPU config)
+            p = capi.params_from_set("STD192")
+            B, op = 8192, "EvalBinGate(NAND)"
+        elif name == "C5a":   # STD128Q EvalSign, ciphertext modulus 2^23, B=1024
+            p = capi.params_from_set("STD128Q")
+            B, op = 1024, "EvalSign(Qin=2^23)"
+        elif name == "C5b":   # STD128 logQ=23 throw=1 EvalSign, ciphertext modulus 2^23, B=1024
+            p = capi.params_from_logq("STD128", False, 23, 0, 0, 1)
+            B, op = 1024, "EvalSign(Qin=2^23)"
+        else:
+            raise SystemExit(f"unknown config {name}")
+        rs = np.random.default_rng(1)
+        t0 = time.perf_counter()
+        bsk = rs.integers(0, p.Q, p.bsk_words(), dtype=np.uint64)
+        ksk = rs.integers(0, p.qKS, p.ksk_words(), dtype=np.uint64)
+        ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+        del bsk, ksk
+        setup_s = time.perf_counter() - t0
+        qin = 1 << 23
+        if name == "C3":
+            ct = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+            lut = np.array([(x ** 3) % 8 for x in range(8)] * (p.q // 8), dtype=np.uint64)
+            call = lambda: ctx.EvalFunc(ct, lut)
+        elif name in ("C4", "C2host"):
+            c1 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+            c2 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+            call = lambda: ctx.EvalBinGate("NAND", c1, c2)
+        else:
+            ct = rs.integers(0, qin, (B, p.n + 1), dtype=np.uint64)
+            call = lambda: ctx.EvalSign(ct, qin)
+        call()  # warm-up
+        b0 = ctx.info().bootstraps
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            call()
+        dt = time.perf_counter() - t0
+        nb = ctx.info().bootstraps - b0
+        info = ctx.info()
+        print(json.dumps({
+            "config": name, "op": op, "batch": B, "params": {"n": p.n, "N": p.N, "Q": p.Q, "dG2": p.dG2,
+                                                              "baseG": p.baseG, "qKS": p.qKS},
+            "kernel": "fast" if info.word_bits == 32 and p.N == 1024 else "generic",
+            "bootstraps_per_call": nb // args.reps, "bootstraps_per_s": round(nb / dt, 1),
+            "calls_per_s": round(args.reps / dt, 3), "note": "host-array API, PCIe transfers included",
+            "setup_s": round(setup_s, 1)}), flush=True)
+        ctx.GPUClean()
+
+
+if __name__ == "__main__":
+    main()
