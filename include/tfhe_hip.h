@@ -152,6 +152,13 @@ tfhe_status tfhe_mkm_switch_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct
 tfhe_status tfhe_export_key_image(tfhe_ctx* ctx, void* d_dst, size_t bytes, void* stream);
 tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, const void* d_src, size_t bytes,
                                       int device);
+/* The same image as a file (cache the packed layout on disk; replaces
+ * BTKeyLoad + GPUSetup's host conversion, binfhecontext.h:208-220, bootstrapping.cu:874-1083):
+ * header {magic "TFHEKIMG", ABI version, tfhe_params, image bytes, FNV-1a 64 of the image}
+ * followed by the image.  Loading checks magic, version, parameters, size and checksum
+ * before touching the device. */
+tfhe_status tfhe_save_key_image(tfhe_ctx* ctx, const char* path);
+tfhe_status tfhe_setup_from_key_file(tfhe_ctx** out, const tfhe_params* p, const char* path, int device);
 
 /* ---- introspection ---- */
 tfhe_status tfhe_get_info(tfhe_ctx* ctx, tfhe_info* out);

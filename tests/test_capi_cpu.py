@@ -65,3 +65,18 @@ def test_errors_without_setup(capi):
     bad.Q = 1000  # not prime / not 1 mod 2N
     assert lib.tfhe_params_finish(ctypes.byref(bad)) == 1
     assert lib.tfhe_host_selftest(ctypes.byref(bad)) == 1
+
+
+def test_key_file_rejected_before_device_use(tmp_path):
+    """tfhe_setup_from_key_file validates the header (magic, ABI, parameters, size,
+    checksum) before any device call, so these checks run without a GPU."""
+    import tfhe_amd
+    from tfhe_amd import capi
+
+    p = capi.params_from_set("TOY")
+    bad = tmp_path / "bad.kimg"
+    bad.write_bytes(b"NOTAKEY!" + b"\0" * 200)
+    with pytest.raises(capi.TfheError, match="not a key image"):
+        tfhe_amd.BinFHEContextHIP.from_key_file(p, str(bad))
+    with pytest.raises(capi.TfheError, match="cannot open"):
+        tfhe_amd.BinFHEContextHIP.from_key_file(p, str(tmp_path / "missing.kimg"))

@@ -228,3 +228,78 @@ def test_device_gate_entry_matches_host_entry(std128):
     ctx.EvalBinGateDevice("NAND", 10, d1.data_ptr(), d2.data_ptr(), do.data_ptr(), stream=s.cuda_stream)
     s.synchronize()
     assert np.array_equal(do.cpu().numpy().astype(np.uint64), ctx.EvalBinGate("NAND", c1, c2))
+
+
+# ---------------------------------------------------------------- batch shapes and edge values
+@pytest.mark.parametrize("B", [1, 2, 3, 130])
+def test_gate_batch_sizes(std128, B):
+    """Odd batches leave the fast kernel's last workgroup half idle; B=1 is the scalar API."""
+    op, cp, ctx, orc = std128["op"], std128["cp"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(100 + B)
+    c1 = random_cts(rs, B, cp.n, cp.q)
+    c2 = random_cts(rs, B, cp.n, cp.q)
+    assert np.array_equal(ctx.EvalBinGate("AND", c1, c2), orc.eval_bin_gate("AND", c1, c2))
+
+
+def test_eval_acc_boundary_values(std128):
+    """Accumulator coefficients at the centring boundaries (0, Q>>1, (Q>>1)+-1, Q-1), where a
+    wrong canonical/centred representative would change the digit decomposition."""
+    op, ctx, orc = std128["op"], std128["ctx"], std128["orc"]
+    Q, h = int(op.Q), int(op.Q) >> 1
+    edge = np.array([0, 1, h - 1, h, h + 1, Q - 2, Q - 1], dtype=np.uint64)
+    rs = np.random.default_rng(3)
+    B = 3
+    acc = edge[rs.integers(0, len(edge), (B, 2, op.N))]
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+
+
+def test_batch_above_chunk_size(std128):
+    """A batch larger than the 65536-ciphertext chunk (the reference's max_bootstapping_num)
+    spans two device chunks; sampled ciphertexts on both sides equal the oracle."""
+    if std128["path"] != "fast":
+        pytest.skip("one kernel is enough for the chunking logic")
+    op, cp, ctx, orc = std128["op"], std128["cp"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(9)
+    B = 65536 + 5
+    c1 = random_cts(rs, B, cp.n, cp.q)
+    c2 = random_cts(rs, B, cp.n, cp.q)
+    out = ctx.EvalBinGate("OR", c1, c2)
+    idx = [0, 1, 65535, 65536, B - 1]
+    assert np.array_equal(out[idx], orc.eval_bin_gate("OR", c1[idx], c2[idx]))
+
+
+def test_std128_opt_uses_fast_kernel_exactly(capi, oracle):
+    """STD128_OPT (n=502) runs on the specialised kernel too: blind rotation parity with
+    random keys (validity is irrelevant for bit-exactness)."""
+    op = oracle.params_from_set("STD128_OPT")
+    cp = capi.params_from_set("STD128_OPT")
+    rs = np.random.default_rng(4)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    B = 3
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+    c1 = random_cts(rs, 4, cp.n, cp.q)
+    c2 = random_cts(rs, 4, cp.n, cp.q)
+    assert np.array_equal(ctx.EvalBinGate("NOR", c1, c2), orc.eval_bin_gate("NOR", c1, c2))
+    ctx.GPUClean()
+    orc.close()
+
+
+def test_key_file_roundtrip(std128, capi, tmp_path):
+    """save_key_image -> from_key_file (the on-disk cache of the packed layout) gives an
+    identical engine; a wrong parameter set is refused."""
+    ctx, cp = std128["ctx"], std128["cp"]
+    path = str(tmp_path / "std128.kimg")
+    ctx.save_key_image(path)
+    ctx2 = capi.BinFHEContextHIP.from_key_file(cp, path)
+    rs = np.random.default_rng(21)
+    c1 = random_cts(rs, 7, cp.n, cp.q)
+    c2 = random_cts(rs, 7, cp.n, cp.q)
+    assert np.array_equal(ctx.EvalBinGate("XNOR", c1, c2), ctx2.EvalBinGate("XNOR", c1, c2))
+    ctx2.GPUClean()
+    with pytest.raises(capi.TfheError, match="parameters differ"):
+        capi.BinFHEContextHIP.from_key_file(capi.params_from_set("STD128_OPT"), path)

@@ -567,6 +567,11 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             const int l = (int)(k % nl);
             const size_t b = std::min(sub, lo + cnt - off);
             Device& L = lane[l];
+            if (prev_l == l) {  // one lane: its previous output must leave before its buffers are reused
+                st = d2h(prev_l, prev_off, prev_b);
+                prev_l = -1;
+                if (st != TFHE_OK) break;
+            }
             uint64_t *din1 = L.sc.io, *din2 = in2 ? L.sc.io + sub * w1 : nullptr, *dout = L.sc.io + sub * (w1 + w_in2);
             if (hipMemcpyAsync(din1, in1 + off * w1, b * w1 * 8, hipMemcpyHostToDevice, L.stream) != hipSuccess ||
                 (in2 && hipMemcpyAsync(din2, in2 + off * w2, b * w2 * 8, hipMemcpyHostToDevice, L.stream) !=
@@ -697,6 +702,83 @@ tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, cons
     HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
     HCHECK(hipMalloc(&d.arena, bytes));
     HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
+    SCHECK(finish_device(c.get(), d));
+    *out = c.release();
+    return TFHE_OK;
+}
+
+namespace {
+struct KeyFileHeader {
+    char magic[8];  // "TFHEKIMG"
+    uint32_t abi;
+    uint32_t reserved;
+    tfhe_params params;
+    uint64_t bytes;
+    uint64_t fnv;
+};
+uint64_t fnv1a64(const unsigned char* p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
+}  // namespace
+
+tfhe_status tfhe_save_key_image(tfhe_ctx* c, const char* path) {
+    SCHECK(check_ctx(c));
+    if (!path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null path");
+    std::vector<unsigned char> img(c->layout.total);
+    HCHECK(hipSetDevice(c->devs[0].id));
+    HCHECK(hipStreamSynchronize(c->devs[0].stream));
+    HCHECK(hipMemcpy(img.data(), c->devs[0].arena, img.size(), hipMemcpyDeviceToHost));
+    KeyFileHeader hdr{};
+    std::memcpy(hdr.magic, "TFHEKIMG", 8);
+    hdr.abi = (uint32_t)tfhe_abi_version();
+    hdr.params = c->p;
+    hdr.bytes = img.size();
+    hdr.fnv = fnv1a64(img.data(), img.size());
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
+    const bool ok = std::fwrite(&hdr, sizeof(hdr), 1, f) == 1 && std::fwrite(img.data(), 1, img.size(), f) == img.size();
+    if (std::fclose(f) != 0 || !ok) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("write failed: ") + path);
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_setup_from_key_file(tfhe_ctx** out, const tfhe_params* p, const char* path, int device) {
+    if (!out || !p || !path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    tfhe_params want = *p;
+    std::string err;
+    if (params_finish(&want, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
+    KeyFileHeader hdr{};
+    std::vector<unsigned char> img;
+    tfhe_status st = TFHE_OK;
+    if (std::fread(&hdr, sizeof(hdr), 1, f) != 1 || std::memcmp(hdr.magic, "TFHEKIMG", 8) != 0)
+        st = fail(TFHE_ERR_INVALID_ARGUMENT, "not a key image file");
+    else if (hdr.abi != (uint32_t)tfhe_abi_version())
+        st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image written by another ABI version");
+    else if (std::memcmp(&hdr.params, &want, sizeof(want)) != 0)
+        st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image parameters differ from the requested ones");
+    else {
+        img.resize(hdr.bytes);
+        if (std::fread(img.data(), 1, img.size(), f) != img.size())
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "truncated key image file");
+        else if (fnv1a64(img.data(), img.size()) != hdr.fnv)
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image checksum mismatch");
+    }
+    std::fclose(f);
+    if (st != TFHE_OK) return st;
+    std::unique_ptr<tfhe_ctx> c;
+    SCHECK(create_ctx(&want, 1, c));
+    if (img.size() != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+    Device& d = c->devs[0];
+    d.id = device;
+    HCHECK(hipSetDevice(device));
+    HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    HCHECK(hipMalloc(&d.arena, img.size()));
+    HCHECK(hipMemcpy(d.arena, img.data(), img.size(), hipMemcpyHostToDevice));
     SCHECK(finish_device(c.get(), d));
     *out = c.release();
     return TFHE_OK;

@@ -77,6 +77,8 @@ _SIGS = {
     "tfhe_mkm_switch_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
     "tfhe_export_key_image": ([VP, VP, SZ, VP], C.c_int),
     "tfhe_setup_from_key_image": ([C.POINTER(VP), P, VP, SZ, C.c_int], C.c_int),
+    "tfhe_save_key_image": ([VP, C.c_char_p], C.c_int),
+    "tfhe_setup_from_key_file": ([C.POINTER(VP), P, C.c_char_p, C.c_int], C.c_int),
     "tfhe_get_info": ([VP, C.POINTER(Info)], C.c_int),
     "tfhe_host_selftest": ([P], C.c_int),
 }

@@ -4,6 +4,7 @@ over the C-ABI.  Ciphertexts are numpy uint64 arrays of shape [B, n+1]
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -39,6 +40,17 @@ class BinFHEContextHIP:
         check(lib().tfhe_setup_from_key_image(C.byref(ctx._h), C.byref(params), C.c_void_p(d_src), nbytes, device),
               "tfhe_setup_from_key_image")
         return ctx
+
+    @classmethod
+    def from_key_file(cls, params: Params, path: str, device: int = 0):
+        """Adopt a key image saved by save_key_image (no host key conversion)."""
+        ctx = cls(params)
+        check(lib().tfhe_setup_from_key_file(C.byref(ctx._h), C.byref(params), os.fsencode(path), device),
+              "tfhe_setup_from_key_file")
+        return ctx
+
+    def save_key_image(self, path: str):
+        check(lib().tfhe_save_key_image(self._h, os.fsencode(path)), "tfhe_save_key_image")
 
     def export_key_image(self, d_dst: int, nbytes: int, stream: int = 0):
         check(lib().tfhe_export_key_image(self._h, C.c_void_p(d_dst), nbytes, C.c_void_p(stream)),
