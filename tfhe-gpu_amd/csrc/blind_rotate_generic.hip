@@ -11,6 +11,8 @@
 //   acc_j += INTT(S_j)
 // acc stays in coefficient form, so the kernel input/output is the reference's
 // EvalAcc_CUDA coefficient form (acc0 transposed on exit, bootstrapping.cu:675-686).
+#include <cstdlib>
+
 #include "device_math.hpp"
 #include "kernels.hpp"
 
@@ -148,11 +150,232 @@ k_blind_rotate_generic(BRParams P, const W* __restrict__ psi, const W* __restric
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Register-resident variant for N in {1024, 2048} (k_blind_rotate_gen2).
+// The accumulator and the external-product sums live in registers: thread t owns
+// coefficients / NTT slots x = t + 256 k (k < CN = N / 256), so the decomposition, the
+// MAC (coalesced BSK reads) and the accumulator update need no LDS.  Only the current
+// digit's two polynomials pass through LDS for the transforms (2N words), so a workgroup
+// needs 16-32 KiB instead of (2 + dG2) N words: several workgroups share a CU.  Digits
+// come from the centred accumulator in closed form (see blind_rotate_fast.hip):
+//   d_l = (c + (B/2)(B^l - 1)/(B - 1)) >> (l logG),  digit_l = sext_logG(d_l)
+// which equals SignedDigitDecompose (rgsw-acc.cpp:83-109) digit by digit, thrown
+// digits included.  Transforms are radix-4 LDS stages (one barrier per two stages).
+// ---------------------------------------------------------------------------
+
+// CT stages m and 2m fused: a0=x[j], a1=x[j+h], a2=x[j+2h], a3=x[j+3h], h = len/2
+template <typename W>
+__device__ __forceinline__ void lds_ntt_fwd_r4(W* buf, uint32_t N, uint32_t logN, W Q, const W* __restrict__ psi,
+                                               const W* __restrict__ psi_sh) {
+    uint32_t m = 1, loglen = logN - 1;  // stage with m blocks has half-length len = 2^loglen
+    while (m < N) {
+        if (m * 2 < N) {  // radix-4 unit: stages m (len) and 2m (len/2)
+            const uint32_t lh = loglen - 1, h = 1u << lh, units = N >> 2;
+            for (uint32_t u = threadIdx.x; u < 2 * units; u += blockDim.x) {
+                const uint32_t poly = u >= units, uu = u - poly * units;
+                const uint32_t i = uu >> lh, jj = uu & (h - 1);       // block of stage m, offset in quarter
+                W* a = buf + (size_t)poly * N + ((size_t)i << (loglen + 1)) + jj;
+                const W w = psi[m + i], ws = psi_sh[m + i];
+                const W w1 = psi[2 * m + 2 * i], w1s = psi_sh[2 * m + 2 * i];
+                const W w2 = psi[2 * m + 2 * i + 1], w2s = psi_sh[2 * m + 2 * i + 1];
+                W a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
+                W v = shoup<W>(a2, w, ws, Q);
+                a2 = subm<W>(a0, v, Q), a0 = addm<W>(a0, v, Q);
+                v = shoup<W>(a3, w, ws, Q);
+                a3 = subm<W>(a1, v, Q), a1 = addm<W>(a1, v, Q);
+                v = shoup<W>(a1, w1, w1s, Q);
+                a[h] = subm<W>(a0, v, Q), a[0] = addm<W>(a0, v, Q);
+                v = shoup<W>(a3, w2, w2s, Q);
+                a[3 * h] = subm<W>(a2, v, Q), a[2 * h] = addm<W>(a2, v, Q);
+            }
+            m <<= 2;
+            loglen -= 2;
+        } else {  // last single stage
+            const uint32_t half = N >> 1;
+            for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
+                const uint32_t poly = b >= half, bb = b - poly * half;
+                W* a = buf + (size_t)poly * N + 2 * bb;
+                const W v = shoup<W>(a[1], psi[m + bb], psi_sh[m + bb], Q);
+                const W u0 = a[0];
+                a[0] = addm<W>(u0, v, Q), a[1] = subm<W>(u0, v, Q);
+            }
+            m <<= 1;
+        }
+        __syncthreads();
+    }
+}
+
+// GS inverse (no N^-1), stages fused in pairs from the small blocks up
+template <typename W>
+__device__ __forceinline__ void lds_ntt_inv_r4(W* buf, uint32_t N, uint32_t logN, W Q, const W* __restrict__ ipsi,
+                                               const W* __restrict__ ipsi_sh) {
+    uint32_t m = N >> 1, loglen = 0;  // stage with m blocks, half-length 2^loglen
+    if (logN & 1) {  // odd number of stages: the single stage first
+        const uint32_t half = N >> 1;
+        for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
+            const uint32_t poly = b >= half, bb = b - poly * half;
+            W* a = buf + (size_t)poly * N + 2 * bb;
+            const W u0 = a[0], u1 = a[1];
+            a[0] = addm<W>(u0, u1, Q);
+            a[1] = shoup<W>(subm<W>(u0, u1, Q), ipsi[m + bb], ipsi_sh[m + bb], Q);
+        }
+        __syncthreads();
+        m >>= 1;
+        loglen = 1;
+    }
+    while (m > 1) {  // stages m (half-length h) then m/2 (half-length 2h)
+        const uint32_t lh = loglen, h = 1u << lh, units = N >> 2;
+        for (uint32_t u = threadIdx.x; u < 2 * units; u += blockDim.x) {
+            const uint32_t poly = u >= units, uu = u - poly * units;
+            const uint32_t i = uu >> lh, jj = uu & (h - 1);  // block of stage m/2
+            W* a = buf + (size_t)poly * N + ((size_t)i << (lh + 2)) + jj;
+            const W w1 = ipsi[m + 2 * i], w1s = ipsi_sh[m + 2 * i];
+            const W w2 = ipsi[m + 2 * i + 1], w2s = ipsi_sh[m + 2 * i + 1];
+            const W w = ipsi[(m >> 1) + i], ws = ipsi_sh[(m >> 1) + i];
+            W a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
+            W s0 = addm<W>(a0, a1, Q), d0 = shoup<W>(subm<W>(a0, a1, Q), w1, w1s, Q);
+            W s1 = addm<W>(a2, a3, Q), d1 = shoup<W>(subm<W>(a2, a3, Q), w2, w2s, Q);
+            a[0] = addm<W>(s0, s1, Q);
+            a[2 * h] = shoup<W>(subm<W>(s0, s1, Q), w, ws, Q);
+            a[h] = addm<W>(d0, d1, Q);
+            a[3 * h] = shoup<W>(subm<W>(d0, d1, Q), w, ws, Q);
+        }
+        __syncthreads();
+        m >>= 2;
+        loglen += 2;
+    }
+}
+
+template <typename W, int CN>
+__global__ void __launch_bounds__(GEN_THREADS, 2)
+k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__ psi_sh, const W* __restrict__ ipsi,
+                    const W* __restrict__ ipsi_sh, const W* __restrict__ mono, const W* __restrict__ mono_sh,
+                    const uint32_t* __restrict__ eidx, const W* __restrict__ bsk, const W* __restrict__ bsk_sh,
+                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = GEN_THREADS * CN;
+    W* buf = reinterpret_cast<W*>(smem);  // [2][N]: the current digit of both polynomials
+    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const W Q = (W)P.Q, r1 = (W)P.r1;
+    const uint64_t Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
+    const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
+    const uint64_t scale = (uint64_t)twoN / amod;
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+
+    W acc[2][CN];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) acc[p][k] = (W)g[p * N + t + GEN_THREADS * k];
+
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        W A[2][2][CN];  // A_kj per owned slot, lazily reduced (< 2 dG2 Q)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) A[kk][j][k] = 0;
+        const W* ek = bsk + (size_t)i * round_words;
+        const W* eks = bsk_sh + (size_t)i * round_words;
+        for (uint32_t l = 0; l < P.digits; ++l) {
+            const uint32_t lt = l + P.thr;  // digit index including the thrown ones
+            const uint32_t shift = lt * logG;
+            // (B/2)(B^lt - 1)/(B - 1) = (B/2)(1 + B + ... + B^(lt-1))
+            int64_t K = 0;
+            for (uint32_t z = 0; z < lt; ++z) K = (K << logG) + Bh;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const uint64_t v = (uint64_t)acc[p][k];
+                    const int64_t c = v < Qhalf ? (int64_t)v : (int64_t)v - Qs;
+                    const int64_t d = (c + K) >> shift;
+                    int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    if (r < 0) r += Qs;
+                    buf[p * N + t + GEN_THREADS * k] = (W)r;
+                }
+            __syncthreads();
+            lds_ntt_fwd_r4<W>(buf, N, P.logN, Q, psi, psi_sh);
+            // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both output polynomials
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const uint32_t x = t + GEN_THREADS * k;
+                const W d0 = buf[x], d1 = buf[N + x];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
+                        const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
+                        A[kk][j][k] += shoup_lazy<W>(d0, ek[o0], eks[o0], Q) + shoup_lazy<W>(d1, ek[o1], eks[o1], Q);
+                    }
+            }
+            __syncthreads();  // buf is rewritten by the next digit
+        }
+        // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1) into buf, then INTT
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint32_t x = t + GEN_THREADS * k;
+            const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
+            const W mp = mono[ip], mps = mono_sh[ip], mn = mono[in], mns = mono_sh[in];
+            const W A00 = reduce_full<W>(A[0][0][k], r1, Q), A01 = reduce_full<W>(A[0][1][k], r1, Q);
+            const W A10 = reduce_full<W>(A[1][0][k], r1, Q), A11 = reduce_full<W>(A[1][1][k], r1, Q);
+            buf[x] = addm<W>(shoup<W>(A00, mp, mps, Q), shoup<W>(A10, mn, mns, Q), Q);
+            buf[N + x] = addm<W>(shoup<W>(A01, mp, mps, Q), shoup<W>(A11, mn, mns, Q), Q);
+        }
+        __syncthreads();
+        lds_ntt_inv_r4<W>(buf, N, P.logN, Q, ipsi, ipsi_sh);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) acc[p][k] = addm<W>(acc[p][k], buf[p * N + t + GEN_THREADS * k], Q);
+        __syncthreads();  // buf is rewritten by the next round
+    }
+    // acc0 -> transpose (X -> X^-1, poly.cpp:762-770) through LDS, reduced values
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) buf[p * N + t + GEN_THREADS * k] = acc[p][k];
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += GEN_THREADS) {
+        const W v = buf[k == 0 ? 0 : N - k];
+        g[k] = (uint64_t)(k == 0 ? v : (v == 0 ? (W)0 : (W)(Q - v)));
+        g[N + k] = (uint64_t)buf[N + k];
+    }
+}
+
 hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const DevTables& T, const void* bsk,
                                        const void* bsk_sh, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B,
                                        hipStream_t s) {
     if (B == 0) return hipSuccess;
     const size_t wb = word_bits == 32 ? 4 : 8;
+    static const bool v1 = [] {
+        const char* e = std::getenv("TFHE_GENERIC_V1");
+        return e && e[0] == '1';
+    }();
+    if (!v1 && (P.N == 1024 || P.N == 2048)) {
+        const size_t lds2 = (size_t)2 * P.N * wb;
+        dim3 grid((unsigned)B), block(GEN_THREADS);
+        auto go = [&](auto kern, auto tag) {
+            using W = decltype(tag);
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+            hipLaunchKernelGGL(kern, grid, block, lds2, s, P, (const W*)T.psi, (const W*)T.psi_sh, (const W*)T.ipsi,
+                               (const W*)T.ipsi_sh, (const W*)T.mono, (const W*)T.mono_sh, T.eidx, (const W*)bsk,
+                               (const W*)bsk_sh, a, amod, acc);
+        };
+        if (word_bits == 32)
+            P.N == 1024 ? go(k_blind_rotate_gen2<uint32_t, 4>, uint32_t{}) : go(k_blind_rotate_gen2<uint32_t, 8>, uint32_t{});
+        else
+            P.N == 1024 ? go(k_blind_rotate_gen2<uint64_t, 4>, uint64_t{}) : go(k_blind_rotate_gen2<uint64_t, 8>, uint64_t{});
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)(2 + P.dG2) * P.N * wb;
     if (lds > 160 * 1024) return hipErrorNotSupported;
     dim3 grid((unsigned)B), block(GEN_THREADS);
