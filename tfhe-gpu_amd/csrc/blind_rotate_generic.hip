@@ -164,10 +164,26 @@ k_blind_rotate_generic(BRParams P, const W* __restrict__ psi, const W* __restric
 // digits included.  Transforms are radix-4 LDS stages (one barrier per two stages).
 // ---------------------------------------------------------------------------
 
+// Lazy (Harvey) butterflies: forward values stay in [0, 4Q), inverse values in [0, 2Q)
+// (4Q < 2^W: Q < 2^30 for u32 words, Q < 2^58 for u64), one conditional subtraction each.
+template <typename W>
+__device__ __forceinline__ void ct_lazy(W& x, W& y, W w, W ws, W Q2, W Q) {
+    const W u = csub<W>(x, Q2), v = shoup_lazy<W>(y, w, ws, Q);
+    x = u + v;
+    y = u + Q2 - v;
+}
+template <typename W>
+__device__ __forceinline__ void gs_lazy(W& x, W& y, W w, W ws, W Q2, W Q) {
+    const W u = x, v = y;
+    x = csub<W>(u + v, Q2);
+    y = shoup_lazy<W>(u + Q2 - v, w, ws, Q);
+}
+
 // CT stages m and 2m fused: a0=x[j], a1=x[j+h], a2=x[j+2h], a3=x[j+3h], h = len/2
 template <typename W>
 __device__ __forceinline__ void lds_ntt_fwd_r4(W* buf, uint32_t N, uint32_t logN, W Q, const W* __restrict__ psi,
                                                const W* __restrict__ psi_sh) {
+    const W Q2 = 2 * Q;
     uint32_t m = 1, loglen = logN - 1;  // stage with m blocks has half-length len = 2^loglen
     while (m < N) {
         if (m * 2 < N) {  // radix-4 unit: stages m (len) and 2m (len/2)
@@ -180,14 +196,11 @@ __device__ __forceinline__ void lds_ntt_fwd_r4(W* buf, uint32_t N, uint32_t logN
                 const W w1 = psi[2 * m + 2 * i], w1s = psi_sh[2 * m + 2 * i];
                 const W w2 = psi[2 * m + 2 * i + 1], w2s = psi_sh[2 * m + 2 * i + 1];
                 W a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
-                W v = shoup<W>(a2, w, ws, Q);
-                a2 = subm<W>(a0, v, Q), a0 = addm<W>(a0, v, Q);
-                v = shoup<W>(a3, w, ws, Q);
-                a3 = subm<W>(a1, v, Q), a1 = addm<W>(a1, v, Q);
-                v = shoup<W>(a1, w1, w1s, Q);
-                a[h] = subm<W>(a0, v, Q), a[0] = addm<W>(a0, v, Q);
-                v = shoup<W>(a3, w2, w2s, Q);
-                a[3 * h] = subm<W>(a2, v, Q), a[2 * h] = addm<W>(a2, v, Q);
+                ct_lazy<W>(a0, a2, w, ws, Q2, Q);
+                ct_lazy<W>(a1, a3, w, ws, Q2, Q);
+                ct_lazy<W>(a0, a1, w1, w1s, Q2, Q);
+                ct_lazy<W>(a2, a3, w2, w2s, Q2, Q);
+                a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
             }
             m <<= 2;
             loglen -= 2;
@@ -196,9 +209,9 @@ __device__ __forceinline__ void lds_ntt_fwd_r4(W* buf, uint32_t N, uint32_t logN
             for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
                 const uint32_t poly = b >= half, bb = b - poly * half;
                 W* a = buf + (size_t)poly * N + 2 * bb;
-                const W v = shoup<W>(a[1], psi[m + bb], psi_sh[m + bb], Q);
-                const W u0 = a[0];
-                a[0] = addm<W>(u0, v, Q), a[1] = subm<W>(u0, v, Q);
+                W a0 = a[0], a1 = a[1];
+                ct_lazy<W>(a0, a1, psi[m + bb], psi_sh[m + bb], Q2, Q);
+                a[0] = a0, a[1] = a1;
             }
             m <<= 1;
         }
@@ -206,19 +219,21 @@ __device__ __forceinline__ void lds_ntt_fwd_r4(W* buf, uint32_t N, uint32_t logN
     }
 }
 
-// GS inverse (no N^-1), stages fused in pairs from the small blocks up
+// GS inverse (no N^-1), stages fused in pairs from the small blocks up; inputs and
+// outputs in [0, 2Q)
 template <typename W>
 __device__ __forceinline__ void lds_ntt_inv_r4(W* buf, uint32_t N, uint32_t logN, W Q, const W* __restrict__ ipsi,
                                                const W* __restrict__ ipsi_sh) {
+    const W Q2 = 2 * Q;
     uint32_t m = N >> 1, loglen = 0;  // stage with m blocks, half-length 2^loglen
     if (logN & 1) {  // odd number of stages: the single stage first
         const uint32_t half = N >> 1;
         for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
             const uint32_t poly = b >= half, bb = b - poly * half;
             W* a = buf + (size_t)poly * N + 2 * bb;
-            const W u0 = a[0], u1 = a[1];
-            a[0] = addm<W>(u0, u1, Q);
-            a[1] = shoup<W>(subm<W>(u0, u1, Q), ipsi[m + bb], ipsi_sh[m + bb], Q);
+            W a0 = a[0], a1 = a[1];
+            gs_lazy<W>(a0, a1, ipsi[m + bb], ipsi_sh[m + bb], Q2, Q);
+            a[0] = a0, a[1] = a1;
         }
         __syncthreads();
         m >>= 1;
@@ -234,12 +249,11 @@ __device__ __forceinline__ void lds_ntt_inv_r4(W* buf, uint32_t N, uint32_t logN
             const W w2 = ipsi[m + 2 * i + 1], w2s = ipsi_sh[m + 2 * i + 1];
             const W w = ipsi[(m >> 1) + i], ws = ipsi_sh[(m >> 1) + i];
             W a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
-            W s0 = addm<W>(a0, a1, Q), d0 = shoup<W>(subm<W>(a0, a1, Q), w1, w1s, Q);
-            W s1 = addm<W>(a2, a3, Q), d1 = shoup<W>(subm<W>(a2, a3, Q), w2, w2s, Q);
-            a[0] = addm<W>(s0, s1, Q);
-            a[2 * h] = shoup<W>(subm<W>(s0, s1, Q), w, ws, Q);
-            a[h] = addm<W>(d0, d1, Q);
-            a[3 * h] = shoup<W>(subm<W>(d0, d1, Q), w, ws, Q);
+            gs_lazy<W>(a0, a1, w1, w1s, Q2, Q);
+            gs_lazy<W>(a2, a3, w2, w2s, Q2, Q);
+            gs_lazy<W>(a0, a2, w, ws, Q2, Q);
+            gs_lazy<W>(a1, a3, w, ws, Q2, Q);
+            a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
         }
         __syncthreads();
         m >>= 2;
@@ -335,7 +349,8 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int k = 0; k < CN; ++k) acc[p][k] = addm<W>(acc[p][k], buf[p * N + t + GEN_THREADS * k], Q);
+            for (int k = 0; k < CN; ++k)  // inverse outputs are in [0, 2Q)
+                acc[p][k] = csub<W>(csub<W>(acc[p][k] + buf[p * N + t + GEN_THREADS * k], 2 * Q), Q);
         __syncthreads();  // buf is rewritten by the next round
     }
     // acc0 -> transpose (X -> X^-1, poly.cpp:762-770) through LDS, reduced values
