@@ -303,3 +303,27 @@ def test_key_file_roundtrip(std128, capi, tmp_path):
     ctx2.GPUClean()
     with pytest.raises(capi.TfheError, match="parameters differ"):
         capi.BinFHEContextHIP.from_key_file(capi.params_from_set("STD128_OPT"), path)
+
+
+@pytest.mark.parametrize("path", ["f64", "generic"])
+def test_std192_blind_rotation_parity(capi, oracle, path):
+    """STD192 (Q = 2^37 - 2^17 + 1, N = 2048) runs on the exact-FP64 kernel by default and
+    on the u64 generic kernel with TFHE_FORCE_GENERIC=1; both equal the oracle."""
+    op = oracle.params_from_set("STD192")
+    cp = capi.params_from_set("STD192")
+    rs = np.random.default_rng(5)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    if path == "generic":
+        os.environ["TFHE_FORCE_GENERIC"] = "1"
+    try:
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    finally:
+        os.environ.pop("TFHE_FORCE_GENERIC", None)
+    B = 2
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    acc[1, :, :4] = [0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1]
+    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+    ctx.GPUClean()
+    orc.close()

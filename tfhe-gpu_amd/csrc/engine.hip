@@ -110,6 +110,7 @@ struct Device {
     hipStream_t stream = nullptr;
     unsigned char* arena = nullptr;
     void* bsk_fast = nullptr;
+    void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
     Scratch sc;
     DevTables tables{};
     hipStream_t stream2 = nullptr;  // lane 1
@@ -123,6 +124,7 @@ struct tfhe_ctx {
     int word_bits = 64;
     int ksk_bits = 64;
     bool use_fast = false;
+    bool use_f64 = false;
     BRParams br{};
     KSParams ks{};
     ArenaLayout layout{};
@@ -159,6 +161,7 @@ tfhe_status init_derived(tfhe_ctx* c) {
     c->ks.n_pad = (uint32_t)c->layout.n_pad;
     const char* force = std::getenv("TFHE_FORCE_GENERIC");
     c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
+    c->use_f64 = f64_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
         return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
     if (p.baseKS > 256) return fail(TFHE_ERR_UNSUPPORTED, "baseKS > 256 not supported");
@@ -264,6 +267,11 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
         HCHECK(launch_pack_bsk_fast(c->br, d.tables, d.arena + c->layout.bsk, d.bsk_fast, d.stream));
         HCHECK(hipStreamSynchronize(d.stream));
     }
+    if (c->use_f64) {
+        HCHECK(hipMalloc(&d.keys_f64, bsk_f64_bytes(c->br)));
+        HCHECK(launch_pack_bsk_f64(c->br, d.tables, d.arena + c->layout.bsk, d.keys_f64, d.stream));
+        HCHECK(hipStreamSynchronize(d.stream));
+    }
     return TFHE_OK;
 }
 
@@ -273,6 +281,7 @@ void free_device(Device& d) {
     if (d.stream) hipStreamSynchronize(d.stream);
     hipFree(d.arena);
     hipFree(d.bsk_fast);
+    hipFree(d.keys_f64);
     if (d.stream2) hipStreamSynchronize(d.stream2);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
@@ -324,6 +333,8 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     const ArenaLayout& L = c->layout;
     if (c->use_fast && (amod & (amod - 1)) == 0) {
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
+    } else if (c->use_f64) {
+        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, a, amod, acc, B, d.stream));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
                                            amod, acc, B, d.stream));
@@ -806,7 +817,8 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
     if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
     out->num_devices = (int)c->devs.size();
     out->word_bits = c->word_bits;
-    out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0);
+    out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0) +
+                            (c->use_f64 ? bsk_f64_bytes(c->br) : 0);
     out->ksk_device_bytes = c->layout.total - c->layout.ksk;
     out->bootstraps = c->bootstraps.load();
     out->key_image_bytes = c->layout.total;

@@ -43,6 +43,14 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
                                 hipStream_t s);
 size_t bsk_fast_bytes(const BRParams& P);
 
+// Exact-FP64 blind rotation for 2^32 <= Q < 2^40 (STD192 class): keys/tables as centred
+// doubles derived on device from the generic (u64) arena.
+bool f64_path_supported(const BRParams& P, int word_bits);
+size_t bsk_f64_bytes(const BRParams& P);
+hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
+hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, const uint64_t* a,
+                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
 //   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.
 //   kska: [N][baseKS][dKS][n_pad] (A part, rows padded to 16 bytes), kskb: [N][baseKS][dKS] (B),
