@@ -305,12 +305,13 @@ def test_key_file_roundtrip(std128, capi, tmp_path):
         capi.BinFHEContextHIP.from_key_file(capi.params_from_set("STD128_OPT"), path)
 
 
-@pytest.mark.parametrize("path", ["f64", "generic"])
-def test_std192_blind_rotation_parity(capi, oracle, path):
-    """STD192 (Q = 2^37 - 2^17 + 1, N = 2048) runs on the exact-FP64 kernel by default and
-    on the u64 generic kernel with TFHE_FORCE_GENERIC=1; both equal the oracle."""
-    op = oracle.params_from_set("STD192")
-    cp = capi.params_from_set("STD192")
+@pytest.mark.parametrize("pset,path", [("STD192", "f64"), ("STD192", "generic"), ("STD128Q", "f64")])
+def test_n2048_blind_rotation_parity(capi, oracle, pset, path):
+    """STD192 (Q = 2^37 - 2^17 + 1) and STD128Q (Q = 2^50 - 2^14 + 1, the reducing variant),
+    N = 2048, run on the exact-FP64 kernel by default and on the u64 generic kernel with
+    TFHE_FORCE_GENERIC=1; all equal the oracle, including accumulator boundary values."""
+    op = oracle.params_from_set(pset)
+    cp = capi.params_from_set(pset)
     rs = np.random.default_rng(5)
     bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)

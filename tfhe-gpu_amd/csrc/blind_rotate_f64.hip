@@ -1,5 +1,5 @@
 // blind_rotate_f64.hip -- CGGI blind rotation in exact FP64 integer arithmetic for
-// 2^32 <= Q < 2^40 (STD192, STD192_OPT, STD192Q, STD192Q_OPT; N = 1024 or 2048).
+// 2^32 <= Q < 2^50 (STD192(_OPT), STD192Q(_OPT), STD128Q(_OPT); N = 1024 or 2048).
 //
 // Same math as the generic kernel (rgsw-acc-cggi.cpp:246-307, rgsw-acc.cpp:57-111), but
 // every NTT-domain value is an integer held exactly in a double, so a modular product is
@@ -7,9 +7,11 @@
 // twiddles need no Shoup companions:
 //     h = a*b (rounded), l = fma(a, b, -h)          a*b = h + l exactly
 //     q = rint(h / Q),   r = fma(-q, Q, h) + l      r = a*b - qQ exactly, |r| <~ Q/2
-// Exactness holds while |a*b| < 2^96 and every sum stays below 2^53: with Q < 2^40 the
-// forward transform grows by < Q/2 per stage (< 6Q after 11), the inverse transform
-// doubles per stage from |S| < 1.1Q (< 2^51 after 11) and needs no reduction at all.
+// Exactness holds while |a*b| < 2^102 and every sum stays below 2^53.  Q < 2^40 (RED =
+// false): the forward transform grows by < Q/2 per stage (< 6Q after 11), the inverse
+// doubles per stage from |S| < 1.1Q (< 2^51 after 11); no reduction at all.  Q < 2^50
+// (RED = true, STD128Q class): every radix-4 unit reduces its outputs to |x| <~ Q/2
+// (x - rint(x/Q) Q, three instructions), which keeps all values below 4Q < 2^52.
 // Keys and tables are centred (|x| <= Q/2).  The accumulator stays in int64 registers
 // (canonical [0, Q)) for the closed-form digit decomposition of the generic v2 kernel.
 #include <cmath>
@@ -35,7 +37,12 @@ __device__ __forceinline__ double fmodmul(double a, double b, const F64Const& K)
     return __dadd_rn(__fma_rn(-q, K.Q, h), l);
 }
 
-// CT stages m and 2m fused (radix-4 units), no reductions
+__device__ __forceinline__ double fred(double x, const F64Const& K) {
+    return __fma_rn(-__builtin_rint(__dmul_rn(x, K.Qinv)), K.Q, x);
+}
+
+// CT stages m and 2m fused (radix-4 units); RED: reduce the unit's outputs
+template <bool RED>
 __device__ __forceinline__ void f64_ntt_fwd(double* buf, uint32_t N, uint32_t logN, const double* psi,
                                             const F64Const& K) {
     uint32_t m = 1, loglen = logN - 1;
@@ -53,9 +60,11 @@ __device__ __forceinline__ void f64_ntt_fwd(double* buf, uint32_t N, uint32_t lo
                 v = fmodmul(a3, w, K);
                 a3 = __dsub_rn(a1, v), a1 = __dadd_rn(a1, v);
                 v = fmodmul(a1, w1, K);
-                a[h] = __dsub_rn(a0, v), a[0] = __dadd_rn(a0, v);
+                a1 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
                 v = fmodmul(a3, w2, K);
-                a[3 * h] = __dsub_rn(a2, v), a[2 * h] = __dadd_rn(a2, v);
+                a3 = __dsub_rn(a2, v), a2 = __dadd_rn(a2, v);
+                if constexpr (RED) a0 = fred(a0, K), a1 = fred(a1, K), a2 = fred(a2, K), a3 = fred(a3, K);
+                a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
             }
             m <<= 2;
             loglen -= 2;
@@ -65,7 +74,8 @@ __device__ __forceinline__ void f64_ntt_fwd(double* buf, uint32_t N, uint32_t lo
                 const uint32_t poly = b >= half, bb = b - poly * half;
                 double* a = buf + (size_t)poly * N + 2 * bb;
                 const double v = fmodmul(a[1], psi[m + bb], K), u0 = a[0];
-                a[0] = __dadd_rn(u0, v), a[1] = __dsub_rn(u0, v);
+                a[0] = RED ? fred(__dadd_rn(u0, v), K) : __dadd_rn(u0, v);
+                a[1] = RED ? fred(__dsub_rn(u0, v), K) : __dsub_rn(u0, v);
             }
             m <<= 1;
         }
@@ -73,7 +83,8 @@ __device__ __forceinline__ void f64_ntt_fwd(double* buf, uint32_t N, uint32_t lo
     }
 }
 
-// GS inverse without N^-1 (folded into the BSK), no reductions
+// GS inverse without N^-1 (folded into the BSK); RED: reduce the doubling outputs
+template <bool RED>
 __device__ __forceinline__ void f64_ntt_inv(double* buf, uint32_t N, uint32_t logN, const double* ipsi,
                                             const F64Const& K) {
     uint32_t m = N >> 1, loglen = 0;
@@ -83,7 +94,7 @@ __device__ __forceinline__ void f64_ntt_inv(double* buf, uint32_t N, uint32_t lo
             const uint32_t poly = b >= half, bb = b - poly * half;
             double* a = buf + (size_t)poly * N + 2 * bb;
             const double u0 = a[0], u1 = a[1];
-            a[0] = __dadd_rn(u0, u1);
+            a[0] = RED ? fred(__dadd_rn(u0, u1), K) : __dadd_rn(u0, u1);
             a[1] = fmodmul(__dsub_rn(u0, u1), ipsi[m + bb], K);
         }
         __syncthreads();
@@ -100,9 +111,9 @@ __device__ __forceinline__ void f64_ntt_inv(double* buf, uint32_t N, uint32_t lo
             const double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
             const double s0 = __dadd_rn(a0, a1), d0 = fmodmul(__dsub_rn(a0, a1), w1, K);
             const double s1 = __dadd_rn(a2, a3), d1 = fmodmul(__dsub_rn(a2, a3), w2, K);
-            a[0] = __dadd_rn(s0, s1);
+            a[0] = RED ? fred(__dadd_rn(s0, s1), K) : __dadd_rn(s0, s1);
             a[2 * h] = fmodmul(__dsub_rn(s0, s1), w, K);
-            a[h] = __dadd_rn(d0, d1);
+            a[h] = RED ? fred(__dadd_rn(d0, d1), K) : __dadd_rn(d0, d1);
             a[3 * h] = fmodmul(__dsub_rn(d0, d1), w, K);
         }
         __syncthreads();
@@ -119,7 +130,7 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 }
 
 // table block (doubles): psi[N] ipsi[N] mono[2N], then the BSK [n][2][dG2][2][N]
-template <int CN>
+template <int CN, bool RED>
 __global__ void __launch_bounds__(F64_THREADS, 2)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -175,7 +186,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     buf[p * N + t + F64_THREADS * k] = (double)r;
                 }
             __syncthreads();
-            f64_ntt_fwd(buf, N, P.logN, psi, K);
+            f64_ntt_fwd<RED>(buf, N, P.logN, psi, K);
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
                 const uint32_t x = t + F64_THREADS * k;
@@ -200,7 +211,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             buf[N + x] = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
         }
         __syncthreads();
-        f64_ntt_inv(buf, N, P.logN, ipsi, K);
+        f64_ntt_inv<RED>(buf, N, P.logN, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -239,7 +250,7 @@ __global__ void k_pack_f64(uint64_t Q, uint32_t N, const uint64_t* __restrict__ 
 }  // namespace
 
 bool f64_path_supported(const BRParams& P, int word_bits) {
-    return word_bits == 64 && P.Q >= (1ull << 32) && P.Q < (1ull << 40) && (P.N == 1024 || P.N == 2048) &&
+    return word_bits == 64 && P.Q >= (1ull << 32) && P.Q < (1ull << 50) && (P.N == 1024 || P.N == 2048) &&
            P.logG <= 32 && P.n > 0;
 }
 
@@ -266,8 +277,9 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(F64_THREADS), lds, s, P, K, (const double*)keys, T.eidx, a,
                            amod, acc);
     };
-    if (P.N == 1024) go(k_blind_rotate_f64<4>);
-    else go(k_blind_rotate_f64<8>);
+    const bool red = P.Q >= (1ull << 40);
+    if (P.N == 1024) red ? go(k_blind_rotate_f64<4, true>) : go(k_blind_rotate_f64<4, false>);
+    else red ? go(k_blind_rotate_f64<8, true>) : go(k_blind_rotate_f64<8, false>);
     return hipGetLastError();
 }
 
