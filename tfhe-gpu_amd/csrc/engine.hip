@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -115,7 +116,11 @@ struct Device {
     DevTables tables{};
     hipStream_t stream2 = nullptr;  // lane 1
     Scratch sc2;
+    void* pin[2] = {};               // pinned staging blocks for the host-array API
+    hipEvent_t pin_ev[2] = {};       // last DMA that used each block
 };
+
+constexpr size_t kStageBytes = (size_t)8 << 20;
 
 }  // namespace
 
@@ -289,6 +294,10 @@ void free_device(Device& d) {
         hipFree(sc->ext);
         for (auto* p : sc->lwe) hipFree(p);
         hipFree(sc->io);
+    }
+    for (int k = 0; k < 2; ++k) {
+        if (d.pin_ev[k]) hipEventSynchronize(d.pin_ev[k]), hipEventDestroy(d.pin_ev[k]);
+        if (d.pin[k]) hipHostFree(d.pin[k]);
     }
     if (d.stream) hipStreamDestroy(d.stream);
     if (d.stream2) hipStreamDestroy(d.stream2);
@@ -537,6 +546,51 @@ tfhe_status for_each_shard(tfhe_ctx* c, size_t B, F&& body) {
     return TFHE_OK;
 }
 
+// Host <-> device copies through two pinned 8 MiB blocks: the host copy pool fills (or
+// drains) block k+1 while the DMA engine moves block k.  Pageable hipMemcpyAsync stages
+// through the runtime's buffers with one host thread; this path is ~2x faster.
+tfhe_status ensure_pinned(Device& d) {
+    for (int k = 0; k < 2; ++k) {
+        if (!d.pin[k]) HCHECK(hipHostMalloc(&d.pin[k], kStageBytes, hipHostMallocDefault));
+        if (!d.pin_ev[k]) HCHECK(hipEventCreateWithFlags(&d.pin_ev[k], hipEventDisableTiming));
+    }
+    return TFHE_OK;
+}
+tfhe_status h2d_staged(Device& d, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    SCHECK(ensure_pinned(d));
+    for (size_t off = 0, k = 0; off < bytes; off += kStageBytes, ++k) {
+        const int slot = (int)(k & 1);
+        const size_t blk = std::min(kStageBytes, bytes - off);
+        HCHECK(hipEventSynchronize(d.pin_ev[slot]));  // the DMA that last read this block is done
+        parallel_memcpy(d.pin[slot], (const char*)src + off, blk);
+        HCHECK(hipMemcpyAsync((char*)dst + off, d.pin[slot], blk, hipMemcpyHostToDevice, s));
+        HCHECK(hipEventRecord(d.pin_ev[slot], s));
+    }
+    return TFHE_OK;
+}
+tfhe_status d2h_staged(Device& d, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    SCHECK(ensure_pinned(d));
+    size_t prev_off = 0, prev_blk = 0;
+    for (size_t off = 0, k = 0;; off += kStageBytes, ++k) {
+        const int slot = (int)(k & 1);
+        const bool more = off < bytes;
+        const size_t blk = more ? std::min(kStageBytes, bytes - off) : 0;
+        if (more) {
+            HCHECK(hipEventSynchronize(d.pin_ev[slot]));
+            HCHECK(hipMemcpyAsync(d.pin[slot], (const char*)src + off, blk, hipMemcpyDeviceToHost, s));
+            HCHECK(hipEventRecord(d.pin_ev[slot], s));
+        }
+        if (k > 0) {  // drain the previous block while this one is in flight
+            const int ps = (int)((k - 1) & 1);
+            HCHECK(hipEventSynchronize(d.pin_ev[ps]));
+            parallel_memcpy((char*)dst + prev_off, d.pin[ps], prev_blk);
+        }
+        if (!more) break;
+        prev_off = off, prev_blk = blk;
+    }
+    return TFHE_OK;
+}
+
 // Host-array runner: in-arrays are [B][in_words] (up to 2), out [B][out_words].  Each
 // device's shard is cut into sub-batches that alternate between the device's two lanes:
 // sub-batch k's H2D copy and kernels are queued on its lane before the host waits for
@@ -567,11 +621,12 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
         if (st != TFHE_OK) return st;
         auto d2h = [&](int l, size_t off, size_t b) -> tfhe_status {
             const uint64_t* dout = lane[l].sc.io + sub * (w1 + w_in2);
-            if (hipMemcpyAsync(out + off * wo, dout, b * wo * 8, hipMemcpyDeviceToHost, lane[l].stream) != hipSuccess ||
-                hipStreamSynchronize(lane[l].stream) != hipSuccess)
-                return fail(TFHE_ERR_DEVICE, std::string("D2H/sync failed: ") + hipGetErrorString(hipGetLastError()));
-            return TFHE_OK;
+            return d2h_staged(d, out + off * wo, dout, b * wo * 8, lane[l].stream);
         };
+        static const bool trace = std::getenv("TFHE_TRACE") != nullptr;
+        auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        const double t0 = trace ? now() : 0;
+        double t_h2d = 0, t_op = 0;
         size_t prev_off = 0, prev_b = 0;
         int prev_l = -1;
         for (size_t k = 0, off = lo; off < lo + cnt && st == TFHE_OK; ++k, off += sub) {
@@ -584,13 +639,12 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
                 if (st != TFHE_OK) break;
             }
             uint64_t *din1 = L.sc.io, *din2 = in2 ? L.sc.io + sub * w1 : nullptr, *dout = L.sc.io + sub * (w1 + w_in2);
-            if (hipMemcpyAsync(din1, in1 + off * w1, b * w1 * 8, hipMemcpyHostToDevice, L.stream) != hipSuccess ||
-                (in2 && hipMemcpyAsync(din2, in2 + off * w2, b * w2 * 8, hipMemcpyHostToDevice, L.stream) !=
-                            hipSuccess)) {
-                st = fail(TFHE_ERR_DEVICE, "H2D copy failed");
-                break;
-            }
+            st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, L.stream);
+            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, L.stream);
+            if (st != TFHE_OK) break;
+            if (trace) hipStreamSynchronize(L.stream), t_h2d = now() - t0;
             st = op(L, din1, din2, dout, b, off);
+            if (trace) hipStreamSynchronize(L.stream), t_op = now() - t0;
             if (st != TFHE_OK) break;
             if (prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
             prev_l = l, prev_off = off, prev_b = b;
@@ -598,6 +652,9 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
         if (st == TFHE_OK && prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
         hipStreamSynchronize(d.stream);
         if (d.stream2) hipStreamSynchronize(d.stream2);
+        if (trace)
+            std::fprintf(stderr, "[tfhe] host batch %zu: h2d done %.2f ms, kernels done %.2f ms, d2h done %.2f ms\n", cnt,
+                         t_h2d, t_op, now() - t0);
         return st;
     });
 }

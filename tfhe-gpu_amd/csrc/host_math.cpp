@@ -5,7 +5,70 @@
 #include <cstring>
 #include <unordered_map>
 
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+
 namespace tfhe {
+
+namespace {
+struct CopyPool {
+    std::mutex call, m;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> workers;
+    unsigned T = 0;
+    uint64_t gen = 0;
+    unsigned pending = 0;
+    char* dst = nullptr;
+    const char* src = nullptr;
+    size_t bytes = 0;
+    CopyPool() {
+        T = host_threads();
+        for (unsigned w = 1; w < T; ++w) workers.emplace_back([this, w] { loop(w); });
+        for (auto& t : workers) t.detach();
+    }
+    void piece(unsigned w) {
+        const size_t per = (bytes + T - 1) / T, lo = std::min(bytes, w * per), hi = std::min(bytes, lo + per);
+        if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+    }
+    void loop(unsigned w) {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+            }
+            piece(w);
+            std::lock_guard<std::mutex> lk(m);
+            if (--pending == 0) done_cv.notify_one();
+        }
+    }
+    void run(void* d, const void* s2, size_t n) {
+        std::lock_guard<std::mutex> one(call);
+        if (T <= 1 || n < (1u << 20)) {
+            std::memcpy(d, s2, n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m);
+            dst = (char*)d, src = (const char*)s2, bytes = n;
+            pending = T - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        piece(0);
+        std::unique_lock<std::mutex> lk(m);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+};
+}  // namespace
+
+void parallel_memcpy(void* dst, const void* src, size_t bytes) {
+    static CopyPool* pool = new CopyPool();  // intentionally leaked: workers are detached
+    pool->run(dst, src, bytes);
+}
+
 
 uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
     uint64_t r = 1 % m;

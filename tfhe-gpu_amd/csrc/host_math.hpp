@@ -44,6 +44,11 @@ void parallel_for(size_t n, F&& f) {
     for (auto& x : th) x.join();
 }
 
+// Persistent worker pool for large host memcpy (pinned staging of the host-array API):
+// creating threads per 8 MiB block would cost as much as the copy.  Thread-safe (one
+// copy at a time); workers are created on first use and live until process exit.
+void parallel_memcpy(void* dst, const void* src, size_t bytes);
+
 using u128 = unsigned __int128;
 
 inline uint64_t mulmod(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)(((u128)a * b) % m); }
