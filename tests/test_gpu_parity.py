@@ -328,3 +328,58 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path):
     assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
     ctx.GPUClean()
     orc.close()
+
+
+def _prime_1_mod(m, bits):
+    """Largest prime p < 2^bits with p = 1 (mod m) (deterministic Miller-Rabin for 64-bit)."""
+    def is_prime(n):
+        if n < 2:
+            return False
+        d, s = n - 1, 0
+        while d % 2 == 0:
+            d //= 2
+            s += 1
+        for a in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+            x = pow(a, d, n)
+            if x in (1, n - 1) or a % n == 0:
+                continue
+            for _ in range(s - 1):
+                x = x * x % n
+                if x == n - 1:
+                    break
+            else:
+                return False
+        return True
+    p = ((1 << bits) - 1) // m * m + 1
+    while not is_prime(p):
+        p -= m
+    return p
+
+
+@pytest.mark.parametrize("bits,baseG_log", [(35, 12), (45, 15)])
+def test_custom_modulus_n1024_f64_parity(capi, oracle, bits, baseG_log):
+    """User-defined parameters (C-ABI tfhe_params_finish) with a 35-bit / 45-bit Q at N=1024
+    exercise the exact-FP64 kernel's N=1024 instances (plain and reducing)."""
+    import ctypes as C
+
+    from tfhe_amd import capi as raw
+
+    cp = capi.params_from_set("STD128")
+    cp.Q = _prime_1_mod(2 * cp.N, bits)
+    cp.baseG = 1 << baseG_log
+    cp.digitsG = cp.dG2 = 0
+    raw.check(raw.lib().tfhe_params_finish(C.byref(cp)), "tfhe_params_finish")
+    op = oracle.params_from_set("STD128")
+    for k in ("Q", "baseG", "digitsG", "dG2", "numDigitsToThrow"):
+        setattr(op, k, getattr(cp, k))
+    op.logG = baseG_log
+    rs = np.random.default_rng(bits)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    B = 3
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+    ctx.GPUClean()
+    orc.close()
