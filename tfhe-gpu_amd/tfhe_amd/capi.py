@@ -10,7 +10,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_amd/
 _ROOT = os.path.dirname(_PKG)
-_LIB = os.path.join(_PKG, "lib", "libtfhe_hip.so")
+_LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
