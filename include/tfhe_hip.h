@@ -8,7 +8,7 @@
  * NativePoly <-> flat u64) is in INTEGRATION.md.
  *
  *   reference symbol                                        entry point
- *   GPUFFTBootstrap::GPUSetup       bootstrapping.cuh:111   tfhe_setup
+ *   GPUFFTBootstrap::GPUSetup       bootstrapping.cuh:111   tfhe_setup_eval (OpenFHE EVALUATION-format BSK) or tfhe_setup
  *   GPUFFTBootstrap::GPUClean       bootstrapping.cuh:116   tfhe_clean
  *   GPUFFTBootstrap::EvalAcc_CUDA   bootstrapping.cuh:126   tfhe_eval_acc
  *   GPUFFTBootstrap::MKMSwitch_CUDA bootstrapping.cuh:135   tfhe_mkm_switch
@@ -111,6 +111,15 @@ tfhe_status tfhe_params_finish(tfhe_params* p);
 /* ---- reference boundary ---- */
 tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
                        int num_gpus);
+/* Same, with the BSK exactly as OpenFHE holds it after KeyGen / BTKeyLoad: EVALUATION
+ * format, (*BSkey)[0][key][i][l][m].GetValues() in [n][2][dG2][2][N] order (rgsw-acc-cggi.cpp:231-236).
+ * Replaces the host INTT the reference runs in GPUSetup_core (bootstrapping.cu:874-1083)
+ * and the shim's SetFormat(COEFFICIENT): the library's NTT uses OpenFHE's root
+ * (RootOfUnity(2N, Q), rgsw-cryptoparameters.h:80, nbtheory.cpp:284-343) and transform
+ * (transformnat-impl.h:196-236, 684-706), so the values are taken as they are.  Entries
+ * must be < Q (TFHE_ERR_INVALID_ARGUMENT otherwise). */
+tfhe_status tfhe_setup_eval(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_eval, const uint64_t* ksk,
+                            int num_gpus);
 tfhe_status tfhe_clean(tfhe_ctx* ctx);
 /* a[B][n] mod a_mod; acc[B][2][N] coefficient in/out; acc0 returned transposed
  * (the callers rely on it: binfhe-base-scheme.cpp:665-671, 1203-1204). */

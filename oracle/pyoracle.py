@@ -70,6 +70,9 @@ def lib():
         L.or_splitmix64.argtypes = [C.POINTER(Rng)]
         L.or_splitmix64.restype = C.c_uint64
         L.or_kat_keys.argtypes = [P, C.POINTER(Rng), u64p, u64p]
+        L.or_root_of_unity.argtypes = [C.c_uint64, C.c_uint32]
+        L.or_root_of_unity.restype = C.c_uint64
+        L.or_openfhe_ntt.argtypes = [C.c_uint64, C.c_uint32, C.c_size_t, u64p, u64p, C.c_int]
         L.or_keygen.argtypes = [P, C.POINTER(Rng), u64p, u64p, u64p]
         L.or_encrypt.argtypes = [P, C.POINTER(Rng), u64p, C.c_int64, C.c_uint64, C.c_uint64, u64p]
         L.or_decrypt.argtypes = [P, u64p, u64p, C.c_uint64, C.c_uint64]
@@ -125,6 +128,19 @@ def keygen(p: Params, rng: Rng):
     ksk = np.empty(nk, dtype=np.uint64)
     lib().or_keygen(C.byref(p), C.byref(rng), sk, bsk, ksk)
     return sk, bsk, ksk
+
+
+def root_of_unity(Q: int, N: int) -> int:
+    """RootOfUnity(2N, Q): the smallest primitive 2N-th root (nbtheory.cpp:284-343)."""
+    return int(lib().or_root_of_unity(Q, N))
+
+
+def openfhe_ntt(Q: int, N: int, polys, inverse: bool = False) -> np.ndarray:
+    """COEFFICIENT <-> OpenFHE EVALUATION format of a stack of N-word polynomials."""
+    a = np.ascontiguousarray(polys, dtype=np.uint64).ravel()
+    out = np.empty_like(a)
+    lib().or_openfhe_ntt(Q, N, a.size // N, a, out, int(inverse))
+    return out
 
 
 def splitmix(rng: Rng, count: int, mod: int) -> np.ndarray:

@@ -267,6 +267,45 @@ static void ntt_inv(const ntt_tab* t, uint64_t* a) {
     for (uint32_t j = 0; j < t->N; ++j) a[j] = mulmod(a[j], t->Ninv, Q);
 }
 
+/* OpenFHE's EVALUATION format (what RingGSWACCKey polynomials hold after BTKeyLoad /
+ * KeyGen, rgsw-acc-cggi.cpp:231-236).
+ * Root: RootOfUnity(2N, Q) (rgsw-cryptoparameters.h:80) = the smallest primitive 2N-th
+ * root of unity, nbtheory.cpp:284-343 (any generator's (Q-1)/2N power, then the minimum
+ * over its odd powers).  Table: Table[bitrev(i)] = root^i (transformnat-impl.h:684-706).
+ * Transform: ForwardTransformToBitReverseInPlace (transformnat-impl.h:196-236), Cooley-Tukey
+ * with omega = Table[m + i] -- the same loop as ntt_fwd above. */
+uint64_t or_root_of_unity(uint64_t Q, uint32_t N) {
+    const uint64_t r = find_psi(Q, N), r2 = mulmod(r, r, Q);
+    uint64_t best = r, x = r;
+    for (uint32_t k = 3; k < 2 * N; k += 2) {
+        x = mulmod(x, r2, Q);
+        if (x < best) best = x;
+    }
+    return best;
+}
+
+void or_openfhe_ntt(uint64_t Q, uint32_t N, size_t polys, const uint64_t* in, uint64_t* out, int inverse) {
+    ntt_tab t;
+    t.N = N;
+    t.logN = ilog2u(N);
+    t.Q = Q;
+    t.Ninv = powmod(N, Q - 2, Q);
+    t.psi_br = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    t.ipsi_br = (uint64_t*)malloc(sizeof(uint64_t) * N);
+    const uint64_t psi = or_root_of_unity(Q, N), ipsi = powmod(psi, Q - 2, Q);
+    for (uint32_t k = 0; k < N; ++k) {
+        t.psi_br[bitrev(k, t.logN)] = powmod(psi, k, Q);
+        t.ipsi_br[bitrev(k, t.logN)] = powmod(ipsi, k, Q);
+    }
+    for (size_t k = 0; k < polys; ++k) {
+        uint64_t* a = out + k * N;
+        for (uint32_t j = 0; j < N; ++j) a[j] = in[k * N + j] % Q;
+        if (inverse) ntt_inv(&t, a); /* InverseTransformFromBitReverseInPlace, incl. N^-1 */
+        else ntt_fwd(&t, a);
+    }
+    ntt_free(&t);
+}
+
 void or_polymul_schoolbook(const or_params* p, const uint64_t* a, const uint64_t* b, uint64_t* c) {
     const uint32_t N = p->N;
     const uint64_t Q = p->Q;

@@ -72,6 +72,11 @@ int or_is_prime(uint64_t x);
 void or_polymul_schoolbook(const or_params* p, const uint64_t* a, const uint64_t* b, uint64_t* c);
 /* same product through the oracle's own NTT */
 void or_polymul_ntt(const or_params* p, const uint64_t* a, const uint64_t* b, uint64_t* c);
+/* OpenFHE EVALUATION format: minimal primitive 2N-th root (nbtheory.cpp:284-343) and the
+ * bit-reversed Cooley-Tukey transform (transformnat-impl.h:196-236, 684-706); `polys`
+ * polynomials of N words, inverse includes the N^-1 scaling. */
+uint64_t or_root_of_unity(uint64_t Q, uint32_t N);
+void or_openfhe_ntt(uint64_t Q, uint32_t N, size_t polys, const uint64_t* in, uint64_t* out, int inverse);
 /* rgsw-acc.cpp:57-111: in [2][N] -> out [dG2][N], row = poly + 2*digit, values mod Q */
 void or_signed_digit_decompose(const or_params* p, const uint64_t* in, uint64_t* out);
 

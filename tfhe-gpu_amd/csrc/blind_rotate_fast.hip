@@ -305,7 +305,7 @@ struct LaneCtx {
 // rows travel through LDS, the other one's radix-8 pass runs.  Wait counts are the LDS
 // operations issued after the awaited ones (15 = the counter's maximum, at most one
 // operation stricter than needed).
-template <int NB>
+template <int NB, bool BAR = true>
 __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sbuf,
                                          const LaneCtx& C, const FastConst& K) {
     constexpr uint32_t T = T_FWD * 4;
@@ -317,13 +317,13 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
     fwd_pass8(x0, lo, hi, K);
     if constexpr (NB == 1) {  // the other wavefront has finished reading this buffer
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (BAR) __syncthreads();
     }
     store_rows<1, 2, 0>(x0, m12, lds);
     fwd_pass8(x1, lo, hi, K);
     store_rows<1, 2, 1>(x1, m12, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (BAR) __syncthreads();
     tw_load<T + TW2 * 4, 8>(lo, hi, C.a2, lds);
     gather_rows<1, 2, 0>(x0, sbuf + C.f12, lds);
     gather_rows<1, 2, 1>(x1, sbuf + C.f12, lds);
@@ -353,7 +353,7 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
 
 // Inverse transform of two polynomials (no N^-1: folded into the BSK), L4 -> L1.
 // sloc = buffer of the last forward exchange (wave-local steps), sx = the other buffer.
-template <int NB>
+template <int NB, bool BAR = true>
 __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sloc,
                                          uint32_t sx, const LaneCtx& C, const FastConst& K) {
     constexpr uint32_t T = T_INV * 4;
@@ -382,7 +382,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     inv_pass8(x0, lo, hi, K);
     if constexpr (NB == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (BAR) __syncthreads();
     }
     store_rows<2, 1, 0>(x0, m21, lds);
     lds_wait<0>(x1);
@@ -390,7 +390,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     store_rows<2, 1, 1>(x1, m21, lds);
     tw_load<T + TW1 * 4, 1>(lo, hi, C.zero, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (BAR) __syncthreads();
     gather_rows<2, 1, 0>(x0, sx + C.f21, lds);
     gather_rows<2, 1, 1>(x1, sx + C.f21, lds);
     lds_wait<8>(x0, lo, hi);
@@ -405,7 +405,8 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
 // CTS: ciphertexts per workgroup (a workgroup barrier then spans 2*CTS wavefronts).
 // PF: BSK groups (of 4) whose loads are issued before the digit's forward NTT, so their
 //     latency hides behind it (16 VGPRs each); the rest are loaded when the MAC starts.
-// EXP: timing experiments (results invalid): 1 one BSK slice, 2 no BSK loads.
+// EXP: timing experiments (results invalid): 1 one BSK slice, 2 no BSK loads, 3 no barriers
+//      inside the transforms, 4 = 2 + 3.
 // NB: exchange buffers per ciphertext (2: alternate, 1: smaller LDS footprint, more barriers).
 template <int MINW, bool ACC64, int CTS, int EXP = 0, int PF = 0, int NB = 2>
 __global__ void __launch_bounds__(TPC * CTS, MINW)
@@ -491,7 +492,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
                 const int k = g >> 1, j = g & 1;
                 const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;      // uniform
                 const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;  // uniform
-                if constexpr (EXP >= 2) {
+                if constexpr (EXP == 2 || EXP == 4) {
                     pw[g][0] = v4i{(int)s0, (int)s1, 3, 4};
                     pw[g][1] = pw[g][0] + 1, pw[g][2] = pw[g][0] + 2, pw[g][3] = pw[g][0] + 3;
                 } else {
@@ -502,7 +503,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
 #pragma unroll
             for (int g = 0; g < PF; ++g) issue(g);
             __builtin_amdgcn_sched_barrier(0);
-            ntt_fwd2<NB>(x0, x1, lds, sbuf, C, K);
+            ntt_fwd2<NB, (EXP < 3)>(x0, x1, lds, sbuf, C, K);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int k = g >> 1, j = g & 1;
@@ -546,7 +547,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
             S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
             S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
         }
-        ntt_inv2<NB>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
+        ntt_inv2<NB, (EXP < 3)>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
                      ctbase + ((par + FDIG) & (NB - 1)) * XBUF * 4,
                       C, K);
         // acc <- centred canonical (acc + S): u = acc + S + (Q>>1) + 1 + 4Q in (0, 8Q)
@@ -671,6 +672,8 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 19: launch(k_blind_rotate_fast<4, true, 2, 0, 0, 1>, 2, 1); break;
         case 20: launch(k_blind_rotate_fast<3, true, 2, 0, 0, 1>, 2, 1); break;
         case 21: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 2>, 2, 2); break;
+        case 23: launch(k_blind_rotate_fast<3, true, 2, 3, 2, 1>, 2, 1); break; // timing: no barriers
+        case 24: launch(k_blind_rotate_fast<3, true, 2, 4, 2, 1>, 2, 1); break; // timing: neither
         case 22: launch(k_blind_rotate_fast<3, true, 1, 0, 2, 1>, 1, 1); break;
         // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
         // row sums, half of each digit's BSK prefetched behind its forward NTT

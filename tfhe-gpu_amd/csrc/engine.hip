@@ -211,14 +211,15 @@ void pack_ksk(std::vector<unsigned char>& img, const ArenaLayout& L, uint32_t n,
 
 // Build the whole key image on the host (one-time, GPUSetup_core's job in the
 // reference, bootstrapping.cu:874-1083).
-tfhe_status build_host_image(tfhe_ctx* c, const uint64_t* bsk_coeff, const uint64_t* ksk,
+tfhe_status build_host_image(tfhe_ctx* c, const uint64_t* bsk, bool bsk_eval, const uint64_t* ksk,
                              std::vector<unsigned char>& img) {
     const tfhe_params& p = c->p;
     const ArenaLayout& L = c->layout;
     img.assign(L.total, 0);
     NttTables t = make_ntt_tables(p.Q, p.N);
     std::vector<uint64_t> bsk_ntt(L.bsk_words);
-    bsk_to_ntt_scaled(p, t, bsk_coeff, bsk_ntt.data());
+    if (!bsk_to_ntt_scaled(p, t, bsk, bsk_eval, bsk_ntt.data()))
+        return fail(TFHE_ERR_INVALID_ARGUMENT, "evaluation-format BSK entry >= Q");
     auto put = [&](auto tag, size_t off, size_t off_sh, const uint64_t* v, size_t count) {
         using W = decltype(tag);
         fill_words<W>(img, off, v, count);
@@ -728,14 +729,15 @@ tfhe_status tfhe_params_finish(tfhe_params* p) {
     return s == TFHE_OK ? s : fail(s, err);
 }
 
-tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
-                       int num_gpus) {
+namespace {
+tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, bool bsk_eval,
+                         const uint64_t* ksk, int num_gpus) {
     if (!out || !bsk_coeff || !ksk) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
     std::unique_ptr<tfhe_ctx> c;
     SCHECK(create_ctx(p, num_gpus, c));
     std::vector<unsigned char> img;
-    SCHECK(build_host_image(c.get(), bsk_coeff, ksk, img));
+    SCHECK(build_host_image(c.get(), bsk_coeff, bsk_eval, ksk, img));
     const size_t bytes = c->layout.total;
     for (size_t g = 0; g < c->devs.size(); ++g) {
         Device& d = c->devs[g];
@@ -754,6 +756,17 @@ tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk
     }
     *out = c.release();
     return TFHE_OK;
+}
+}  // namespace
+
+tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
+                       int num_gpus) {
+    return setup_common(out, p, bsk_coeff, false, ksk, num_gpus);
+}
+
+tfhe_status tfhe_setup_eval(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_eval, const uint64_t* ksk,
+                            int num_gpus) {
+    return setup_common(out, p, bsk_eval, true, ksk, num_gpus);
 }
 
 tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, const void* d_src, size_t bytes,

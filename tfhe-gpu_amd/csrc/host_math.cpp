@@ -1,4 +1,5 @@
 // host_math.cpp -- see host_math.hpp.
+#include <atomic>
 #include "host_math.hpp"
 
 #include <cmath>
@@ -233,12 +234,21 @@ NttTables make_ntt_tables(uint64_t Q, uint32_t N) {
     t.N = N;
     t.logN = ilog2(N);
     t.Q = Q;
+    // psi = RootOfUnity(2N, Q) as OpenFHE picks it (rgsw-cryptoparameters.h:80,
+    // nbtheory.cpp:284-343): the smallest primitive 2N-th root, i.e. the minimum over the
+    // odd powers of any one of them.  With OpenFHE's bit-reversed table and transform
+    // (transformnat-impl.h:196-236, 684-706) the NTT below then IS OpenFHE's EVALUATION
+    // format, so evaluation-format keys need no conversion (tfhe_setup_eval).
+    uint64_t r = 0;
     for (uint64_t g = 2;; ++g) {
-        uint64_t x = powmod(g, (Q - 1) / (2ull * N), Q);
-        if (powmod(x, N, Q) == Q - 1) {
-            t.psi = x;
-            break;
-        }
+        r = powmod(g, (Q - 1) / (2ull * N), Q);
+        if (powmod(r, N, Q) == Q - 1) break;
+    }
+    t.psi = r;
+    const uint64_t r2 = mulmod(r, r, Q);
+    for (uint64_t k = 3, x = r; k < 2ull * N; k += 2) {
+        x = mulmod(x, r2, Q);
+        if (x < t.psi) t.psi = x;
     }
     uint64_t ipsi = powmod(t.psi, Q - 2, Q);
     t.Ninv = powmod(N, Q - 2, Q);
@@ -300,16 +310,25 @@ void host_ntt_inv(const NttTables& t, uint64_t* a, bool scale) {
         for (uint32_t j = 0; j < t.N; ++j) a[j] = mulmod(a[j], t.Ninv, Q);
 }
 
-void bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk_coeff, uint64_t* out) {
+bool bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk, bool eval, uint64_t* out) {
     const size_t polys = (size_t)p.n * 2 * p.dG2 * 2;
     const uint32_t N = p.N;
+    std::atomic<bool> bad{false};
     parallel_for(polys, [&](size_t k) {
         uint64_t* dst = out + (size_t)k * N;
-        const uint64_t* src = bsk_coeff + (size_t)k * N;
+        const uint64_t* src = bsk + (size_t)k * N;
+        if (eval) {  // already OpenFHE's NTT: entries must be reduced (NativePoly values)
+            for (uint32_t x = 0; x < N; ++x) {
+                if (src[x] >= p.Q) bad = true;
+                dst[x] = mulmod(src[x] % p.Q, t.Ninv, p.Q);
+            }
+            return;
+        }
         for (uint32_t x = 0; x < N; ++x) dst[x] = src[x] % p.Q;
         host_ntt_fwd(t, dst);
         for (uint32_t x = 0; x < N; ++x) dst[x] = mulmod(dst[x], t.Ninv, p.Q);
     });
+    return !bad;
 }
 
 }  // namespace tfhe

@@ -91,8 +91,10 @@ NttTables make_ntt_tables(uint64_t Q, uint32_t N);
 void host_ntt_fwd(const NttTables& t, uint64_t* a);
 void host_ntt_inv(const NttTables& t, uint64_t* a, bool scale);
 
-// BSK [n][2][dG2][2][N] coefficient form -> NTT domain, scaled by N^-1 (so the
-// device INTT needs no final scaling), same layout.  OpenMP over polynomials.
-void bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk_coeff, uint64_t* out);
+// BSK [n][2][dG2][2][N] -> NTT domain, scaled by N^-1 (so the device INTT needs no final
+// scaling), same layout; parallel over polynomials.  eval = the input is already in
+// OpenFHE's EVALUATION format (= this NTT, see make_ntt_tables): scaling only, and false is
+// returned when an entry is not reduced mod Q.
+bool bsk_to_ntt_scaled(const tfhe_params& p, const NttTables& t, const uint64_t* bsk, bool eval, uint64_t* out);
 
 }  // namespace tfhe

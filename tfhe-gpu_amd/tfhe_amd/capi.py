@@ -61,6 +61,7 @@ _SIGS = {
     "tfhe_params_from_logq": ([C.c_int, C.c_int, C.c_uint32, C.c_int64, C.c_uint32, C.c_uint32, P], C.c_int),
     "tfhe_params_finish": ([P], C.c_int),
     "tfhe_setup": ([C.POINTER(VP), P, u64p, u64p, C.c_int], C.c_int),
+    "tfhe_setup_eval": ([C.POINTER(VP), P, u64p, u64p, C.c_int], C.c_int),
     "tfhe_clean": ([VP], C.c_int),
     "tfhe_eval_acc": ([VP, SZ, u64p, U64, u64p], C.c_int),
     "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),

@@ -23,7 +23,11 @@ class BinFHEContextHIP:
         self._h = C.c_void_p()
 
     # -- GPUSetup / GPUClean (binfhecontext.cpp:349-365) --
-    def GPUSetup(self, bsk_coeff, ksk, num_gpus: int = 1):
+    def GPUSetup(self, bsk_coeff, ksk, num_gpus: int = 1, bsk_format: str = "coefficient"):
+        """bsk_format "coefficient" (tfhe_setup) or "evaluation": OpenFHE's NTT-domain
+        values as KeyGen/BTKeyLoad leave them (tfhe_setup_eval, no host INTT)."""
+        if bsk_format not in ("coefficient", "evaluation"):
+            raise ValueError("bsk_format must be 'coefficient' or 'evaluation'")
         if self._h:
             self.GPUClean()
         p = self.params
@@ -31,7 +35,8 @@ class BinFHEContextHIP:
         kk = _u64(ksk).ravel()
         if bsk.size != p.bsk_words() or kk.size != p.ksk_words():
             raise ValueError("key sizes do not match the parameters")
-        check(lib().tfhe_setup(C.byref(self._h), C.byref(p), bsk, kk, num_gpus), "tfhe_setup")
+        fn = lib().tfhe_setup if bsk_format == "coefficient" else lib().tfhe_setup_eval
+        check(fn(C.byref(self._h), C.byref(p), bsk, kk, num_gpus), fn.__name__)
         return self
 
     @classmethod
