@@ -16,7 +16,8 @@ ALL_SETS = ["TOY", "MEDIUM", "STD128_AP", "STD128_APOPT", "STD128", "STD128_OPT"
             "STD256", "STD256_OPT", "STD128Q", "STD128Q_OPT", "STD192Q", "STD192Q_OPT", "STD256Q", "STD256Q_OPT",
             "SIGNED_MOD_TEST"]
 TRUTH = {"AND": lambda x, y: x & y, "OR": lambda x, y: x | y, "NAND": lambda x, y: 1 - (x & y),
-         "XOR": lambda x, y: x ^ y}
+         "NOR": lambda x, y: 1 - (x | y), "XOR": lambda x, y: x ^ y, "XNOR": lambda x, y: 1 - (x ^ y),
+         "XOR_FAST": lambda x, y: x ^ y, "XNOR_FAST": lambda x, y: 1 - (x ^ y)}  # UnitTestFHEW.cpp truth tables
 
 
 @pytest.mark.parametrize("name", ALL_SETS)
