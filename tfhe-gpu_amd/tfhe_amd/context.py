@@ -107,6 +107,8 @@ class BinFHEContextHIP:
         ct = _u64(ct)
         m = np.ascontiguousarray(matrix, dtype=np.int64)
         K, cols = m.shape
+        if ct.size != K * (self.params.n + 1):  # lwe-operation.cu:66-69
+            raise ValueError("The number of rows of the matrix must be equal to the number of input ciphertexts.")
         out = np.empty((cols, self.params.n + 1), dtype=np.uint64)
         check(lib().tfhe_ciphertext_mul_matrix(self._h, K, ct.ravel(), cols, m.ravel(), modulus, out.ravel()),
               "tfhe_ciphertext_mul_matrix")
