@@ -105,11 +105,19 @@ def cpu_baseline(p, bsk, ksk, seconds):
     t0 = time.perf_counter()
     orc.eval_bin_gate("NAND", c1, c2)
     dt = time.perf_counter() - t0
+    # the single-thread figure SURVEY 8(d) asks for, on a quarter of the time budget
+    orc.L.or_set_threads(1)
+    B1 = max(1, int(seconds / 4 / max(t_cal, 1e-3)))
+    t0 = time.perf_counter()
+    orc.eval_bin_gate("NAND", c1[:B1], c2[:B1])
+    dt1 = time.perf_counter() - t0
+    orc.L.or_set_threads(threads)
     orc.close()
     return {"value": round(B / dt, 3), "unit": "bootstraps/s", "cores": threads, "kind": "port",
+            "single_thread_value": round(B1 / dt1, 3),
             "sample": f"STD128 EvalBinGate(NAND) on {B} random ciphertext pairs, same synthetic keys; "
                       f"oracle/tfhe_oracle.c (exact u128 CPU restatement, OpenMP one ciphertext per thread); "
-                      f"{dt:.1f} s"}
+                      f"{dt:.1f} s; single thread: {B1} pairs in {dt1:.1f} s"}
 
 
 def p_oracle(pyoracle, p):
@@ -221,15 +229,17 @@ def main():
     br_ms = e0.elapsed_time(e1) / args.kernel_reps
     balg, bsk_bytes = b_alg_per_bootstrap(p)
     achieved = balg * B / (br_ms * 1e-3) / 1e9
-    traffic, valu_insts = None, None
+    traffic, valu_insts, pmc = None, None, {}
     if os.path.exists(args.pmc_json):
         try:
             pmc = json.load(open(args.pmc_json))
             if pmc.get("units_per_launch") == B:
                 traffic = pmc.get("hbm_bytes_per_launch")
                 valu_insts = pmc.get("sq_insts_valu_per_launch")
+            else:
+                pmc = {}
         except Exception:
-            traffic = valu_insts = None
+            traffic, valu_insts, pmc = None, None, {}
     mm = modmuls_per_bootstrap(p)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
@@ -246,6 +256,14 @@ def main():
             round(valu_insts * VALU_CYCLES / (simds * CLOCK_HZ * br_ms * 1e-3), 3),
             "note": "issue_frac = PMC SQ_INSTS_VALU x 4 cycles / (4 SIMDs/CU x CUs x 2.4 GHz x kernel time), "
                     "from " + os.path.relpath(args.pmc_json, ROOT)}
+    act, gui = pmc.get("sq_active_inst_valu_per_launch"), pmc.get("grbm_gui_active_per_launch")
+    if act and gui:
+        # measured in one PMC pass, clock-independent: VALU-executing cycles per SIMD over the
+        # launch's cycles (GRBM_GUI_ACTIVE sums the 8 XCDs; SQ_ACTIVE_INST_VALU is quad-cycles)
+        valu["busy_frac"] = round(act * 4 / simds / (gui / 8), 3)
+        valu["held_clock_ghz"] = round(gui / 8 / (br_ms * 1e-3) / 1e9, 2)
+        valu["note"] += ("; busy_frac = SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8); held_clock_ghz = "
+                         "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass, MI355X_MICROARCH.md 'DVFS give-back')")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSV output for one kernel into per-launch HBM bytes.
 
-Usage: pmc_summary.py KERNEL_SUBSTRING FETCH_DIR WRITE_DIR OUT_JSON [MIX_DIR]
-MIX_DIR (optional): a pass with SQ_INSTS_VALU / SQ_INSTS_LDS / SQ_WAVES, recorded per launch
-(bench.py turns SQ_INSTS_VALU into the VALU issue fraction).
+Usage: pmc_summary.py KERNEL_SUBSTRING FETCH_DIR WRITE_DIR OUT_JSON [MIX_DIR ...]
+MIX_DIR... (optional): passes with SQ_INSTS_VALU / SQ_INSTS_LDS / SQ_WAVES and SQ_ACTIVE_INST_VALU /
+GRBM_GUI_ACTIVE, recorded per launch (bench.py turns them into the VALU issue fraction, the measured
+VALU-busy fraction and the clock the chip held).
 FETCH_SIZE/WRITE_SIZE are KiB (TCC_EA0_RDREQ/WRREQ based).  Per
 MI355X_MICROARCH.md 'HBM', gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide
 (16 B/lane) coalesced stream; other access widths are uncalibrated, so both the
@@ -38,9 +39,10 @@ def main():
         res["hbm_bytes_per_launch_raw"] = (fetch + write) * 1024
         res["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
         res["correction"] = "read side x2 per MI355X_MICROARCH.md HBM section (wide-stream calibration)"
-    if len(sys.argv) > 5:
-        mix = rows(sys.argv[5])
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_LDS_BANK_CONFLICT"):
+    for d in sys.argv[5:]:
+        mix = rows(d)
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_VALU",
+                  "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
             v, _ = per_launch(mix, kname, c)
             if v is not None:
                 res[c.lower() + "_per_launch"] = v
