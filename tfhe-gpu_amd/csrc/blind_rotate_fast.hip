@@ -73,6 +73,7 @@ constexpr size_t lds_bytes(int cts, int nb) { return (size_t)(T_WORDS + cts * nb
 struct FastConst {
     int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x
     uint32_t Q2, Q4, h1, kacc;  // 2Q, 4Q, (Q>>1)+1, (Q>>1)+1+4Q
+    int32_t ninv;               // N^-1 (centred Montgomery form)
 };
 
 __device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
@@ -574,17 +575,272 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_blind_rotate_fast2: the same round with one digit's transforms eliminated.
+//
+// The signed digits satisfy c = d_0 + 2^7 d_1 + 2^14 d_2 + 2^21 d_3 exactly (rgsw-acc.cpp:83-109
+// with thr = 0: the top digit is the remainder, |d_3| <= 33), so in the NTT domain
+//     D_3 = 2^-21 (NTT(c) - D_0 - 2^7 D_1 - 2^14 D_2)            (mod Q).
+// Substituting into the external product, for key k, column j, polynomial p:
+//     sum_l D_{p,l} W[2l+p]  =  sum_{l<3} D_{p,l} (W[2l+p] - 2^(7l-21) W[6+p])  +  C_p 2^-21 N W[6+p]
+// with C_p = N^-1 NTT(c_p).  k_pack_fast folds both into the key rows (same BSK size), and
+// the kernel keeps C (the accumulator in the NTT domain) next to its coefficient form:
+// C <- C + S each round, where S is the round's NTT-domain increment (the BSK carries N^-1).
+// Six forward transforms per round instead of eight; the product mod Q is unchanged, so the
+// output is bit-identical to the eight-transform round.
+//
+// C lives in LDS (2 polynomials x 2 halves x 128 lanes x 16 bytes per ciphertext, conflict-
+// free ds_read/write_b128) and is reduced every 8 rounds (|C| < 5.2Q, tools/bounds_fast.py).
+// The round starts with the C "digit" (no transform), whose key rows were fetched during the
+// previous round's inverse transform (PFA groups, when the row sums are dead).
+//
+// MROT: monomial table stored at f(e) = (e >> 6) | ((e & 63) << 5), so the lanes of a gather
+// spread over banks by e's top bits (the plain table is 32-way conflicted when 32 | a').
+// With b = e_t a' mod 2N and e = b + 256 c a', f(e)*4 = (((b >> 4) & 0x70) + 16 c a') & 0x70 | F(b).
+constexpr uint32_t CW = 2 * FN;  // words of C per ciphertext
+constexpr size_t lds_bytes2(int cts) { return (size_t)(T_WORDS + cts * (XBUF + CW)) * 4; }
+
+template <int MINW, int PF, int PFA, bool MROT>
+__global__ void __launch_bounds__(TPC * 2, MINW)
+k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
+                     const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
+                     uint32_t B) {
+    constexpr int CTS = 2;
+    extern __shared__ __align__(16) int32_t lds[];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < T_WORDS; k += TPC * CTS) lds[k] = tabs[k];
+    const uint32_t cl = __builtin_amdgcn_readfirstlane(tid / TPC), t = tid % TPC;
+    const uint32_t ct = blockIdx.x * CTS + cl;
+    const bool active = ct < B;
+    const uint32_t sbuf = (T_WORDS + cl * XBUF) * 4;  // exchange buffer (bytes, uniform)
+    v4i* cv = reinterpret_cast<v4i*>(lds + T_WORDS + CTS * XBUF + cl * CW) + t;  // C: cv[(2p + h) * 128]
+
+    LaneCtx C;
+    C.w = __builtin_amdgcn_readfirstlane(t >> 6);
+    C.f12 = ld_lane<1, 2>(t), C.f23 = ld_lane<2, 3>(t), C.f34 = ld_lane<3, 4>(t);
+    C.f43 = ld_lane<4, 3>(t), C.f32 = ld_lane<3, 2>(t), C.f21 = ld_lane<2, 1>(t);
+    const uint32_t w6 = t >> 6;
+    C.a2 = ((((t >> 3) & 3) | (w6 << 2)) * 16);
+    C.a3 = (((t & 31) | (w6 << 5)) * 16);
+    const uint32_t nslot = ((t >> 5) & 1) | ((t & 31) << 1) | (w6 << 6);
+    C.a4 = t * 16;
+    C.zero = 0;
+
+    uint64_t* g = acc_io + (size_t)(active ? ct : 0) * 2 * FN;
+    const uint32_t Qh = (uint32_t)K.Q >> 1;
+    int32_t acc[2][8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint64_t v0 = active ? g[p * FN + elem<1>(t, r)] : 0;
+            const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
+            acc[p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
+        }
+    __syncthreads();
+
+    // C = N^-1 NTT(acc), in the MAC layout
+    {
+        int32_t x0[8], x1[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x0[r] = acc[0][r], x1[r] = acc[1][r];
+        ntt_fwd2<1>(x0, x1, lds, sbuf, C, K);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) x0[r] = smul(x0[r], K.ninv, K), x1[r] = smul(x1[r], K.ninv, K);
+        cv[0] = v4i{x0[0], x0[1], x0[2], x0[3]};
+        cv[128] = v4i{x0[4], x0[5], x0[6], x0[7]};
+        cv[256] = v4i{x1[0], x1[1], x1[2], x1[3]};
+        cv[384] = v4i{x1[4], x1[5], x1[6], x1[7]};
+    }
+
+    constexpr uint32_t ROWB = 2 * FDG2 * 2 * FN * 4;  // key bytes per round
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * ROWB), 0x00020000);
+    const uint32_t voff = nslot * 32;
+    const uint32_t et = 2 * (__builtin_bitreverse32(nslot) >> 25) + 1;
+    const uint64_t* ap = a + (size_t)(active ? ct : 0) * n;
+    const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;
+
+    // rows 2l (poly 0) and 2l+1 (poly 1) of group g = (key k, column j); l = 3: the C rows
+    auto issue = [&](v4i (&pw)[4], uint32_t round_off, int l, int gi) {
+        const int k = gi >> 1, j = gi & 1;
+        const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;
+        const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;
+        pw[0] = ld_bsk(rsrc, voff, s0), pw[1] = ld_bsk(rsrc, voff + 16, s0);
+        pw[2] = ld_bsk(rsrc, voff, s1), pw[3] = ld_bsk(rsrc, voff + 16, s1);
+    };
+    auto mac = [&](int64_t (&s)[2][2][8], const int32_t (&x0)[8], const int32_t (&x1)[8], const v4i (&pw)[4],
+                   int gi) {
+        const int k = gi >> 1, j = gi & 1;
+        const int32_t w0[8] = {pw[0].x, pw[0].y, pw[0].z, pw[0].w, pw[1].x, pw[1].y, pw[1].z, pw[1].w};
+        const int32_t w1[8] = {pw[2].x, pw[2].y, pw[2].z, pw[2].w, pw[3].x, pw[3].y, pw[3].z, pw[3].w};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            s[k][j][r] = (int64_t)x0[r] * w0[r] + s[k][j][r];
+            s[k][j][r] = (int64_t)x1[r] * w1[r] + s[k][j][r];
+        }
+    };
+
+    v4i pa[4][4];  // C rows of the current round
+#pragma unroll
+    for (int gi = 0; gi < PFA; ++gi) issue(pa[gi], 0, 3, gi);
+
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t ar = active ? (uint32_t)(ap[i] & amask) : 0;
+        const uint32_t ai = ((amask + 1 - ar) & amask) << ashift;
+        const uint32_t round_off = i * ROWB;
+
+        int64_t s[2][2][8];
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) s[k][j][r] = 0;
+
+        // the C "digit": no transform
+        {
+            const v4i c00 = cv[0], c01 = cv[128], c10 = cv[256], c11 = cv[384];
+            const int32_t x0[8] = {c00.x, c00.y, c00.z, c00.w, c01.x, c01.y, c01.z, c01.w};
+            const int32_t x1[8] = {c10.x, c10.y, c10.z, c10.w, c11.x, c11.y, c11.z, c11.w};
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (gi >= PFA) issue(pa[gi], round_off, 3, gi);
+                mac(s, x0, x1, pa[gi], gi);
+            }
+        }
+#pragma unroll
+        for (uint32_t l = 0; l < FDIG - 1; ++l) {
+            const int32_t kl = (int32_t)(((1u << (FLOGG * l)) - 1) / ((1u << FLOGG) - 1)) << (FLOGG - 1);
+            int32_t x0[8], x1[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                x0[r] = __builtin_amdgcn_sbfe(acc[0][r] + kl, FLOGG * l, FLOGG);
+                x1[r] = __builtin_amdgcn_sbfe(acc[1][r] + kl, FLOGG * l, FLOGG);
+            }
+            v4i pw[4][4];
+#pragma unroll
+            for (int gi = 0; gi < PF; ++gi) issue(pw[gi], round_off, l, gi);
+            __builtin_amdgcn_sched_barrier(0);
+            ntt_fwd2<1>(x0, x1, lds, sbuf, C, K);
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (gi >= PF) issue(pw[gi], round_off, l, gi);
+                mac(s, x0, x1, pw[gi], gi);
+            }
+        }
+
+        // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1)
+        const char* mono = reinterpret_cast<const char*>(lds + T_MONO);
+        int32_t S0[8], S1[8];
+        uint32_t bp, bn, F4p, F4n;
+        if constexpr (MROT) {
+            bp = (et * ai) & 2047;
+            bn = (0u - bp) & 2047;
+            F4p = ((bp >> 4) & 0xC) | ((bp & 63) << 7);
+            F4n = ((bn >> 4) & 0xC) | ((bn & 63) << 7);
+            bp = (bp >> 4) & 0x70;
+            bn = (bn >> 4) & 0x70;
+        } else {
+            bp = (et * ai) << 2;  // byte offsets into the 2N-entry table
+        }
+        const uint32_t st4 = (ai << 10) & 8191;  // 256 * ai * 4 mod 8192
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint32_t c = __builtin_bitreverse32((uint32_t)r) >> 29;
+            uint32_t op, on;
+            if constexpr (MROT) {
+                const uint32_t cs = c * 16 * ai;  // uniform
+                op = ((bp + cs) & 0x70) | F4p;
+                on = ((bn - cs) & 0x70) | F4n;
+            } else {
+                const uint32_t e4 = bp + c * st4;
+                op = e4 & 8188;
+                on = (0u - e4) & 8188;
+            }
+            const int32_t mp = *reinterpret_cast<const int32_t*>(mono + op);
+            const int32_t mn = *reinterpret_cast<const int32_t*>(mono + on);
+            const int32_t A00 = sredc(s[0][0][r], K), A01 = sredc(s[0][1][r], K);
+            const int32_t A10 = sredc(s[1][0][r], K), A11 = sredc(s[1][1][r], K);
+            S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
+            S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
+        }
+        // C <- C + S, reduced every 8 rounds
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const v4i c00 = cv[0], c01 = cv[128], c10 = cv[256], c11 = cv[384];
+            int32_t y0[8] = {c00.x, c00.y, c00.z, c00.w, c01.x, c01.y, c01.z, c01.w};
+            int32_t y1[8] = {c10.x, c10.y, c10.z, c10.w, c11.x, c11.y, c11.z, c11.w};
+#pragma unroll
+            for (int r = 0; r < 8; ++r) y0[r] += S0[r], y1[r] += S1[r];
+            if ((i & 7) == 7) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) y0[r] = smul(y0[r], K.rM, K), y1[r] = smul(y1[r], K.rM, K);
+            }
+            cv[0] = v4i{y0[0], y0[1], y0[2], y0[3]};
+            cv[128] = v4i{y0[4], y0[5], y0[6], y0[7]};
+            cv[256] = v4i{y1[0], y1[1], y1[2], y1[3]};
+            cv[384] = v4i{y1[4], y1[5], y1[6], y1[7]};
+        }
+        // next round's C rows (the last round re-fetches its own: no loads past the key)
+        const uint32_t next_off = (i + 1 < n ? i + 1 : i) * ROWB;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int gi = 0; gi < PFA; ++gi) issue(pa[gi], next_off, 3, gi);
+        __builtin_amdgcn_sched_barrier(0);
+        ntt_inv2<1>(S0, S1, lds, sbuf, sbuf, C, K);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            uint32_t u0 = (uint32_t)(acc[0][r] + S0[r]) + K.kacc;
+            uint32_t u1 = (uint32_t)(acc[1][r] + S1[r]) + K.kacc;
+            u0 = csub32(csub32(csub32(u0, K.Q4), K.Q2), (uint32_t)K.Q);
+            u1 = csub32(csub32(csub32(u1, K.Q4), K.Q2), (uint32_t)K.Q);
+            acc[0][r] = (int32_t)(u0 - K.h1);
+            acc[1][r] = (int32_t)(u1 - K.h1);
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint32_t k = elem<1>(t, r);
+            const uint32_t v = (uint32_t)(acc[0][r] < 0 ? acc[0][r] + K.Q : acc[0][r]);
+            const uint32_t v1 = (uint32_t)(acc[1][r] < 0 ? acc[1][r] + K.Q : acc[1][r]);
+            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
+            g[FN + k] = v1;
+        }
+    }
+}
+
 // generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies, twiddles
 // packed per pass (see the table-block comment above)
+// PackMode: which kernel the copy is for (k_blind_rotate_fast: plain rows and table;
+// k_blind_rotate_fast2: digit-3-eliminated rows (hc[l] = 2^(7l-21), hc[3] = N 2^-21 mod Q)
+// and/or the rotated monomial table).
+struct PackMode {
+    uint32_t horner, mrot;
+    uint32_t hc[4];
+};
 __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t words, const uint32_t* __restrict__ psi,
                             const uint32_t* __restrict__ ipsi, const uint32_t* __restrict__ mono,
-                            int32_t* __restrict__ out) {
+                            int32_t* __restrict__ out, PackMode M) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     auto mont = [Q](uint32_t v) {
         const uint32_t m = (uint32_t)(((uint64_t)v << 32) % Q);
         return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
     };
-    if (idx < words) out[T_WORDS + idx] = mont(bsk[idx]);
+    if (idx < words) {
+        uint32_t v = bsk[idx];
+        if (M.horner) {
+            // idx = (((i * 2 + k) * 8 + row) * 2 + j) * N + slot; row = 2l + p
+            const uint32_t row = (uint32_t)((idx / (2 * FN)) % FDG2), l = row >> 1, p = row & 1;
+            const size_t i6 = idx + ((size_t)(6 + p) - row) * 2 * FN;  // row 6 + p, same k, j, slot
+            const uint64_t w6 = (uint64_t)(bsk[i6] % Q) * M.hc[l] % Q;
+            v = l < 3 ? (uint32_t)(((uint64_t)(v % Q) + Q - w6) % Q) : (uint32_t)w6;
+        }
+        out[T_WORDS + idx] = mont(v);
+    }
     if (idx < TW_WORDS) {
         // which packed entry is idx?  e = position within the block (0..3 lo, 4..7 hi)
         uint32_t k = 0;
@@ -605,7 +861,10 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
         out[T_FWD + idx] = zero ? 0 : mont(psi[k]);
         out[T_INV + idx] = zero ? 0 : mont(ipsi[k]);
     }
-    if (idx < 2 * FN) out[T_MONO + idx] = mont(mono[idx]);
+    if (idx < 2 * FN) {
+        const uint32_t e = (uint32_t)idx;
+        out[T_MONO + (M.mrot ? (e >> 6) | ((e & 63) << 5) : e)] = mont(mono[idx]);
+    }
 }
 
 }  // namespace
@@ -617,12 +876,43 @@ bool fast_path_supported(const BRParams& P, int word_bits) {
 
 size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * FN + T_WORDS) * 4; }
 
+namespace {
+// TFHE_FAST_VARIANT selects the kernel build (A/B experiments); < 30: k_blind_rotate_fast
+// (plain key rows and monomial table), >= 30: k_blind_rotate_fast2.
+constexpr int kDefaultVariant = 34;
+int fast_variant() {
+    static const int v = [] {
+        const char* e = std::getenv("TFHE_FAST_VARIANT");
+        return e && e[0] ? std::atoi(e) : kDefaultVariant;
+    }();
+    return v;
+}
+uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
+    uint64_t r = 1 % m;
+    for (b %= m; e; e >>= 1, b = (unsigned __int128)b * b % m)
+        if (e & 1) r = (unsigned __int128)r * b % m;
+    return r;
+}
+int32_t mont_centred(uint64_t v, uint32_t Q) {
+    const uint32_t m = (uint32_t)(((unsigned __int128)(v % Q) << 32) % Q);
+    return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+}
+}  // namespace
+
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s) {
     const size_t words = (size_t)P.n * 2 * FDG2 * 2 * FN;
+    PackMode M{};
+    if (fast_variant() >= 30) {
+        M.horner = 1;
+        M.mrot = 1;
+        const uint64_t Q = P.Q, i21 = powmod(2, Q - 1 - 21, Q);  // 2^-21 (Q prime)
+        for (int l = 0; l < 3; ++l) M.hc[l] = (uint32_t)((unsigned __int128)powmod(2, 7 * l, Q) * i21 % Q);
+        M.hc[3] = (uint32_t)((unsigned __int128)FN * i21 % Q);
+    }
     hipLaunchKernelGGL(k_pack_fast, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint32_t)P.Q,
                        (const uint32_t*)bsk, words, (const uint32_t*)T.psi, (const uint32_t*)T.ipsi,
-                       (const uint32_t*)T.mono, (int32_t*)bsk_fast);
+                       (const uint32_t*)T.mono, (int32_t*)bsk_fast, M);
     return hipGetLastError();
 }
 
@@ -645,18 +935,29 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     K.Q4 = 4 * Q;
     K.h1 = (Q >> 1) + 1;
     K.kacc = K.h1 + 4 * Q;
+    K.ninv = mont_centred(Q - (Q - 1) / FN, Q);  // N (Q-1)/N = -1 mod Q
     const int32_t* tabs = (const int32_t*)bsk_fast;
     const int32_t* bsk = tabs + T_WORDS;
-    static const int variant = [] {
-        const char* e = std::getenv("TFHE_FAST_VARIANT");
-        return e ? std::atoi(e) : 0;
-    }();
+    const int variant = fast_variant();
     auto launch = [&](auto kern, int cts, int nb = 2) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts, nb));
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts, nb), s, K, P.n,
                            loga, tabs, bsk, a, acc, (uint32_t)B);
     };
+    auto launch2 = [&](auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes2(2));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(TPC * 2), lds_bytes2(2), s, K, P.n, loga, tabs,
+                           bsk, a, acc, (uint32_t)B);
+    };
     switch (variant) {
+        // k_blind_rotate_fast2 <MINW, PF, PFA, MROT>
+        case 30: launch2(k_blind_rotate_fast2<3, 2, 4, true>); break;
+        case 31: launch2(k_blind_rotate_fast2<3, 2, 2, true>); break;
+        case 32: launch2(k_blind_rotate_fast2<3, 2, 0, true>); break;
+        case 33: launch2(k_blind_rotate_fast2<3, 0, 4, true>); break;
+        case 34: launch2(k_blind_rotate_fast2<3, 1, 4, true>); break;
+        case 35: launch2(k_blind_rotate_fast2<3, 1, 2, true>); break;
+        case 36: launch2(k_blind_rotate_fast2<3, 0, 2, true>); break;
         case 1: launch(k_blind_rotate_fast<3, false, 2>, 2); break;
         case 2: launch(k_blind_rotate_fast<3, true, 1>, 1); break;
         case 3: launch(k_blind_rotate_fast<2, true, 2>, 2); break;
@@ -677,7 +978,10 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 22: launch(k_blind_rotate_fast<3, true, 1, 0, 2, 1>, 1, 1); break;
         // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
         // row sums, half of each digit's BSK prefetched behind its forward NTT
-        default: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1); break;
+        default:
+            if (variant >= 30) launch2(k_blind_rotate_fast2<3, 1, 4, true>);  // = 34
+            else launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1);
+            break;
     }
     return hipGetLastError();
 }

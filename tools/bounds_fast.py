@@ -32,11 +32,23 @@ B = 64
 for s in range(10):
     B = chk32(B + smul(B, f"fwd stage {s}"), f"fwd stage {s} out")
 Bf = B
+# k_blind_rotate_fast2: C = N^-1 NTT(acc) from the centred accumulator (|acc| <= Q/2), then
+# C <- C + S per round, reduced (smul by R mod Q) every 8 rounds; C enters the row sums as a
+# digit, so it must stay within the forward-output bound used there.
+B = Qh + 1
+for s in range(10):
+    B = chk32(B + smul(B, f"acc fwd stage {s}"), f"acc fwd stage {s} out")
+C0 = smul(B, "C init (x N^-1)")
 # external product
 A64 = sredc(8 * Bf * Qh, "ACC64 row sum")
 A32 = 4 * sredc(2 * Bf * Qh, "ACC32 pair")
 A = max(A64, A32)
 S = sredc(2 * A * Qh, "monomial product")
+Cmax = C0
+for rnd in range(8):
+    Cmax = chk32(Cmax + S, "C + S")
+Cred = smul(Cmax, "C reduction")
+assert max(C0, Cred) + 7 * S <= Bf, "C used as a digit exceeds the forward bound"
 
 
 def gs(u, v, red=False, what=""):
@@ -67,4 +79,4 @@ lo = -h1 - Sout + h1 + 4 * Q
 hi = Qh + Sout + h1 + 4 * Q
 assert 0 < lo and hi < 8 * Q, "acc update out of (0, 8Q)"
 print(f"Q={Q}: fwd out {Bf / Q:.3f}Q, ACC64 A {A64 / Q:.3f}Q, ACC32 A {A32 / Q:.3f}Q, "
-      f"S {S / Q:.3f}Q, inverse out {Sout / Q:.3f}Q, acc update in [{lo / Q:.2f}Q, {hi / Q:.2f}Q)  OK")
+      f"S {S / Q:.3f}Q, C <= {(max(C0, Cred) + 7 * S) / Q:.3f}Q (pre-reduction {Cmax / Q:.3f}Q), inverse out {Sout / Q:.3f}Q, acc update in [{lo / Q:.2f}Q, {hi / Q:.2f}Q)  OK")
