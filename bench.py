@@ -261,7 +261,8 @@ def main():
         # measured in one PMC pass, clock-independent: VALU-executing cycles per SIMD over the
         # launch's cycles (GRBM_GUI_ACTIVE sums the 8 XCDs; SQ_ACTIVE_INST_VALU is quad-cycles)
         valu["busy_frac"] = round(act * 4 / simds / (gui / 8), 3)
-        valu["held_clock_ghz"] = round(gui / 8 / (br_ms * 1e-3) / 1e9, 2)
+        pass_ns = pmc.get("gui_pass_kernel_ns_per_launch")  # the GUI pass's own dispatch time
+        valu["held_clock_ghz"] = round(gui / 8 / (pass_ns * 1e-9 if pass_ns else br_ms * 1e-3) / 1e9, 2)
         valu["note"] += ("; busy_frac = SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8); held_clock_ghz = "
                          "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass, MI355X_MICROARCH.md 'DVFS give-back')")
 

@@ -69,6 +69,8 @@ constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS =
 // (NB = 1: one buffer and an extra barrier before each cross-wavefront store)
 constexpr uint32_t PS = 576, WS = 2 * PS, XBUF = 2 * WS;
 constexpr size_t lds_bytes(int cts, int nb) { return (size_t)(T_WORDS + cts * nb * XBUF) * 4; }
+// the fast key buffer: [T_WORDS tables][4-wave kernel tables (blind_rotate_fast4.hip)][key rows]
+constexpr uint32_t T4W = 4776, TB_WORDS = T_WORDS + T4W;
 
 struct FastConst {
     int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x
@@ -306,7 +308,9 @@ struct LaneCtx {
 // rows travel through LDS, the other one's radix-8 pass runs.  Wait counts are the LDS
 // operations issued after the awaited ones (15 = the counter's maximum, at most one
 // operation stricter than needed).
-template <int NB, bool BAR = true>
+// BAR bit 0: barrier before the cross-wavefront stores (NB = 1), bit 1: after them
+// (timing experiments clear them; results are then invalid)
+template <int NB, int BAR = 3>
 __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sbuf,
                                          const LaneCtx& C, const FastConst& K) {
     constexpr uint32_t T = T_FWD * 4;
@@ -318,13 +322,13 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
     fwd_pass8(x0, lo, hi, K);
     if constexpr (NB == 1) {  // the other wavefront has finished reading this buffer
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (BAR) __syncthreads();
+        if constexpr (BAR & 1) __syncthreads();
     }
     store_rows<1, 2, 0>(x0, m12, lds);
     fwd_pass8(x1, lo, hi, K);
     store_rows<1, 2, 1>(x1, m12, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (BAR) __syncthreads();
+    if constexpr (BAR & 2) __syncthreads();
     tw_load<T + TW2 * 4, 8>(lo, hi, C.a2, lds);
     gather_rows<1, 2, 0>(x0, sbuf + C.f12, lds);
     gather_rows<1, 2, 1>(x1, sbuf + C.f12, lds);
@@ -354,7 +358,7 @@ __device__ __forceinline__ void ntt_fwd2(int32_t (&x0)[8], int32_t (&x1)[8], con
 
 // Inverse transform of two polynomials (no N^-1: folded into the BSK), L4 -> L1.
 // sloc = buffer of the last forward exchange (wave-local steps), sx = the other buffer.
-template <int NB, bool BAR = true>
+template <int NB, int BAR = 3>
 __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], const int32_t* lds, uint32_t sloc,
                                          uint32_t sx, const LaneCtx& C, const FastConst& K) {
     constexpr uint32_t T = T_INV * 4;
@@ -383,7 +387,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     inv_pass8(x0, lo, hi, K);
     if constexpr (NB == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (BAR) __syncthreads();
+        if constexpr (BAR & 1) __syncthreads();
     }
     store_rows<2, 1, 0>(x0, m21, lds);
     lds_wait<0>(x1);
@@ -391,7 +395,7 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     store_rows<2, 1, 1>(x1, m21, lds);
     tw_load<T + TW1 * 4, 1>(lo, hi, C.zero, lds);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (BAR) __syncthreads();
+    if constexpr (BAR & 2) __syncthreads();
     gather_rows<2, 1, 0>(x0, sx + C.f21, lds);
     gather_rows<2, 1, 1>(x1, sx + C.f21, lds);
     lds_wait<8>(x0, lo, hi);
@@ -504,7 +508,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
 #pragma unroll
             for (int g = 0; g < PF; ++g) issue(g);
             __builtin_amdgcn_sched_barrier(0);
-            ntt_fwd2<NB, (EXP < 3)>(x0, x1, lds, sbuf, C, K);
+            ntt_fwd2<NB, (EXP < 3 ? 3 : 0)>(x0, x1, lds, sbuf, C, K);
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int k = g >> 1, j = g & 1;
@@ -548,7 +552,7 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
             S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
             S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
         }
-        ntt_inv2<NB, (EXP < 3)>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
+        ntt_inv2<NB, (EXP < 3 ? 3 : 0)>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
                      ctbase + ((par + FDIG) & (NB - 1)) * XBUF * 4,
                       C, K);
         // acc <- centred canonical (acc + S): u = acc + S + (Q>>1) + 1 + 4Q in (0, 8Q)
@@ -598,9 +602,15 @@ k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __res
 // spread over banks by e's top bits (the plain table is 32-way conflicted when 32 | a').
 // With b = e_t a' mod 2N and e = b + 256 c a', f(e)*4 = (((b >> 4) & 0x70) + 16 c a') & 0x70 | F(b).
 constexpr uint32_t CW = 2 * FN;  // words of C per ciphertext
-constexpr size_t lds_bytes2(int cts) { return (size_t)(T_WORDS + cts * (XBUF + CW)) * 4; }
+constexpr size_t lds_bytes2(int cts, int nb) { return (size_t)(T_WORDS + cts * (nb * XBUF + CW)) * 4; }
 
-template <int MINW, int PF, int PFA, bool MROT>
+// NB = 2: forward transform l uses exchange buffer l & 1, the inverse keeps the last forward
+// buffer for its wave-local steps and the other for its cross-wavefront step (no barrier
+// before the cross-wavefront stores; 2 x 9 KiB more LDS per ciphertext).
+// DEPTH = 1: a digit's non-prefetched key groups are issued one group ahead of their MAC.
+// EXP (timing experiments, results invalid): 1 no pre-store barriers, 2 no barriers in the
+// transforms, 3 no key loads, 4 = 2 + 3.
+template <int MINW, int PF, int PFA, bool MROT, int NB = 1, int DEPTH = 0, int EXP = 0>
 __global__ void __launch_bounds__(TPC * 2, MINW)
 k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -612,8 +622,9 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     const uint32_t cl = __builtin_amdgcn_readfirstlane(tid / TPC), t = tid % TPC;
     const uint32_t ct = blockIdx.x * CTS + cl;
     const bool active = ct < B;
-    const uint32_t sbuf = (T_WORDS + cl * XBUF) * 4;  // exchange buffer (bytes, uniform)
-    v4i* cv = reinterpret_cast<v4i*>(lds + T_WORDS + CTS * XBUF + cl * CW) + t;  // C: cv[(2p + h) * 128]
+    const uint32_t sbuf = (T_WORDS + cl * NB * XBUF) * 4;  // exchange buffer(s) (bytes, uniform)
+    constexpr uint32_t XB = NB == 2 ? XBUF * 4 : 0;        // bytes to the second buffer
+    v4i* cv = reinterpret_cast<v4i*>(lds + T_WORDS + CTS * NB * XBUF + cl * CW) + t;  // C: cv[(2p + h) * 128]
 
     LaneCtx C;
     C.w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -644,7 +655,7 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         int32_t x0[8], x1[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) x0[r] = acc[0][r], x1[r] = acc[1][r];
-        ntt_fwd2<1>(x0, x1, lds, sbuf, C, K);
+        ntt_fwd2<NB>(x0, x1, lds, sbuf + XB, C, K);
 #pragma unroll
         for (int r = 0; r < 8; ++r) x0[r] = smul(x0[r], K.ninv, K), x1[r] = smul(x1[r], K.ninv, K);
         cv[0] = v4i{x0[0], x0[1], x0[2], x0[3]};
@@ -666,9 +677,14 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         const int k = gi >> 1, j = gi & 1;
         const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;
         const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;
-        pw[0] = ld_bsk(rsrc, voff, s0), pw[1] = ld_bsk(rsrc, voff + 16, s0);
-        pw[2] = ld_bsk(rsrc, voff, s1), pw[3] = ld_bsk(rsrc, voff + 16, s1);
+        if constexpr (EXP >= 3) {
+            pw[0] = v4i{(int)s0, (int)s1, 3, 4}, pw[1] = pw[0] + 1, pw[2] = pw[0] + 2, pw[3] = pw[0] + 3;
+        } else {
+            pw[0] = ld_bsk(rsrc, voff, s0), pw[1] = ld_bsk(rsrc, voff + 16, s0);
+            pw[2] = ld_bsk(rsrc, voff, s1), pw[3] = ld_bsk(rsrc, voff + 16, s1);
+        }
     };
+    constexpr int XBAR = EXP == 1 ? 2 : (EXP == 2 || EXP == 4) ? 0 : 3;
     auto mac = [&](int64_t (&s)[2][2][8], const int32_t (&x0)[8], const int32_t (&x1)[8], const v4i (&pw)[4],
                    int gi) {
         const int k = gi >> 1, j = gi & 1;
@@ -703,10 +719,12 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             const v4i c00 = cv[0], c01 = cv[128], c10 = cv[256], c11 = cv[384];
             const int32_t x0[8] = {c00.x, c00.y, c00.z, c00.w, c01.x, c01.y, c01.z, c01.w};
             const int32_t x1[8] = {c10.x, c10.y, c10.z, c10.w, c11.x, c11.y, c11.z, c11.w};
+            if (DEPTH && PFA == 0) issue(pa[0], round_off, 3, 0);
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi) {
                 __builtin_amdgcn_sched_barrier(0);
-                if (gi >= PFA) issue(pa[gi], round_off, 3, gi);
+                const int q = gi + DEPTH;
+                if (q < 4 && q >= PFA) issue(pa[q], round_off, 3, q);
                 mac(s, x0, x1, pa[gi], gi);
             }
         }
@@ -723,11 +741,13 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 #pragma unroll
             for (int gi = 0; gi < PF; ++gi) issue(pw[gi], round_off, l, gi);
             __builtin_amdgcn_sched_barrier(0);
-            ntt_fwd2<1>(x0, x1, lds, sbuf, C, K);
+            ntt_fwd2<NB, XBAR>(x0, x1, lds, sbuf + (l & 1) * XB, C, K);
+            if (DEPTH && PF == 0) issue(pw[0], round_off, l, 0);
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi) {
                 __builtin_amdgcn_sched_barrier(0);
-                if (gi >= PF) issue(pw[gi], round_off, l, gi);
+                const int q = gi + DEPTH;
+                if (q < 4 && q >= PF) issue(pw[q], round_off, l, q);
                 mac(s, x0, x1, pw[gi], gi);
             }
         }
@@ -790,7 +810,7 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 #pragma unroll
         for (int gi = 0; gi < PFA; ++gi) issue(pa[gi], next_off, 3, gi);
         __builtin_amdgcn_sched_barrier(0);
-        ntt_inv2<1>(S0, S1, lds, sbuf, sbuf, C, K);
+        ntt_inv2<NB, XBAR>(S0, S1, lds, sbuf, sbuf + XB, C, K);  // last forward used buffer 0
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             uint32_t u0 = (uint32_t)(acc[0][r] + S0[r]) + K.kacc;
@@ -839,7 +859,7 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
             const uint64_t w6 = (uint64_t)(bsk[i6] % Q) * M.hc[l] % Q;
             v = l < 3 ? (uint32_t)(((uint64_t)(v % Q) + Q - w6) % Q) : (uint32_t)w6;
         }
-        out[T_WORDS + idx] = mont(v);
+        out[TB_WORDS + idx] = mont(v);
     }
     if (idx < TW_WORDS) {
         // which packed entry is idx?  e = position within the block (0..3 lo, 4..7 hi)
@@ -874,12 +894,13 @@ bool fast_path_supported(const BRParams& P, int word_bits) {
            P.Q < (1ull << 27) && P.n > 0;
 }
 
-size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * FN + T_WORDS) * 4; }
+size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * FN + TB_WORDS) * 4; }
 
 namespace {
 // TFHE_FAST_VARIANT selects the kernel build (A/B experiments); < 30: k_blind_rotate_fast
-// (plain key rows and monomial table), >= 30: k_blind_rotate_fast2.
-constexpr int kDefaultVariant = 34;
+// (plain key rows and monomial table), 30-59: k_blind_rotate_fast2, >= 60 (default):
+// k_blind_rotate_fast4 (blind_rotate_fast4.hip; 59 is its 3-waves/SIMD build).
+constexpr int kDefaultVariant = 60;
 int fast_variant() {
     static const int v = [] {
         const char* e = std::getenv("TFHE_FAST_VARIANT");
@@ -913,7 +934,8 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
     hipLaunchKernelGGL(k_pack_fast, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint32_t)P.Q,
                        (const uint32_t*)bsk, words, (const uint32_t*)T.psi, (const uint32_t*)T.ipsi,
                        (const uint32_t*)T.mono, (int32_t*)bsk_fast, M);
-    return hipGetLastError();
+    if (fast4_table_words() != T4W) return hipErrorInvalidValue;
+    return launch_pack_tables_fast4((uint32_t)P.Q, T, (int32_t*)bsk_fast + T_WORDS, s);
 }
 
 hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const void* bsk_fast, const uint64_t* a,
@@ -937,17 +959,19 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     K.kacc = K.h1 + 4 * Q;
     K.ninv = mont_centred(Q - (Q - 1) / FN, Q);  // N (Q-1)/N = -1 mod Q
     const int32_t* tabs = (const int32_t*)bsk_fast;
-    const int32_t* bsk = tabs + T_WORDS;
+    const int32_t* bsk = tabs + TB_WORDS;
     const int variant = fast_variant();
+    if (variant >= 59)
+        return launch_blind_rotate_fast4(variant, &K, P.n, loga, tabs + T_WORDS, bsk, a, acc, B, s);
     auto launch = [&](auto kern, int cts, int nb = 2) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts, nb));
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts, nb), s, K, P.n,
                            loga, tabs, bsk, a, acc, (uint32_t)B);
     };
-    auto launch2 = [&](auto kern) {
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes2(2));
-        hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(TPC * 2), lds_bytes2(2), s, K, P.n, loga, tabs,
-                           bsk, a, acc, (uint32_t)B);
+    auto launch2 = [&](auto kern, int nb = 1) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes2(2, nb));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(TPC * 2), lds_bytes2(2, nb), s, K, P.n, loga,
+                           tabs, bsk, a, acc, (uint32_t)B);
     };
     switch (variant) {
         // k_blind_rotate_fast2 <MINW, PF, PFA, MROT>
@@ -958,6 +982,17 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         case 34: launch2(k_blind_rotate_fast2<3, 1, 4, true>); break;
         case 35: launch2(k_blind_rotate_fast2<3, 1, 2, true>); break;
         case 36: launch2(k_blind_rotate_fast2<3, 0, 2, true>); break;
+        case 37: launch2(k_blind_rotate_fast2<3, 1, 4, true, 1, 1>); break;
+        case 38: launch2(k_blind_rotate_fast2<3, 0, 4, true, 1, 1>); break;
+        case 39: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1>); break;
+        case 43: launch2(k_blind_rotate_fast2<2, 2, 4, true, 2, 1>, 2); break;
+        case 51: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 1>); break;  // timing only
+        case 52: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 2>); break;  // timing only
+        case 53: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 3>); break;  // timing only
+        case 54: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 4>); break;  // timing only
+        case 40: launch2(k_blind_rotate_fast2<2, 4, 4, true, 2>, 2); break;
+        case 41: launch2(k_blind_rotate_fast2<2, 2, 4, true, 2>, 2); break;
+        case 42: launch2(k_blind_rotate_fast2<2, 4, 4, true, 1>); break;
         case 1: launch(k_blind_rotate_fast<3, false, 2>, 2); break;
         case 2: launch(k_blind_rotate_fast<3, true, 1>, 1); break;
         case 3: launch(k_blind_rotate_fast<2, true, 2>, 2); break;
@@ -979,7 +1014,7 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
         // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
         // row sums, half of each digit's BSK prefetched behind its forward NTT
         default:
-            if (variant >= 30) launch2(k_blind_rotate_fast2<3, 1, 4, true>);  // = 34
+            if (variant >= 30) launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1>);  // = 39
             else launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1);
             break;
     }

@@ -1,0 +1,561 @@
+// blind_rotate_fast4.hip -- STD128-class blind rotation, four wavefronts per ciphertext.
+//
+// Same round as k_blind_rotate_fast2 (blind_rotate_fast.hip: top digit eliminated through the
+// NTT-domain accumulator C, digit-folded key rows, signed Montgomery arithmetic), laid out for
+// four waves per SIMD instead of three:
+//
+//  * 256 lanes per ciphertext (one workgroup), 4 coefficients of each polynomial per lane, so
+//    the per-lane state halves (row sums 32 VGPRs, accumulator 8, C 8) and the kernel fits
+//    128 VGPRs.  A 1024-point transform is five radix-4 register passes over the index-bit
+//    pairs (b9 b8) (b7 b6) (b5 b4) (b3 b2) (b1 b0) with four LDS exchanges; only the last
+//    one crosses wavefronts (one barrier per transform, tools/lds_layouts4.py):
+//        L1 regs (b8 b9)  lanes (b2 b3 b4 b6 b7 b5)  waves (b0 b1)   coefficient order
+//        L2 regs (b6 b7)  lanes (b2 b3 b8 b9 b4 b5)  waves (b0 b1)
+//        L3 regs (b4 b5)  lanes (b2 b3 b6 b8 b9 b7)  waves (b0 b1)
+//        L4 regs (b2 b3)  lanes (b4 b5 b6 b8 b9 b7)  waves (b0 b1)
+//        L5 regs (b0 b1)  lanes (b2 .. b7)           waves (b8 b9)   MAC: lane t owns slots 4t..4t+3
+//    Every exchange stores lane-contiguous rows (ds_write_addtid_b32) and gathers with
+//    conflict-free ds_read_b32; the cross-wavefront exchanges alternate between two areas, so
+//    no barrier is needed before their stores.
+//  * Key rows stream through a ring: while the MAC consumes group g of one digit, group g of
+//    the next digit (or of the next round's C rows) is loaded into the freed registers, so
+//    every row has a whole transform to arrive.
+//  * Twiddles of pass 4 are per-lane constants kept in registers, pass 0's are uniform
+//    (SGPRs), passes 1-3 come from LDS (ds_read_b128).
+//  * Inverse passes on L4 and L2 reduce their second-stage sums (tools/bounds_fast4.py).
+#include "device_math.hpp"
+#include "kernels.hpp"
+
+namespace tfhe {
+namespace f4 {
+
+constexpr uint32_t FN = 1024, FDG2 = 8, FDIG = 4, FLOGG = 7;
+constexpr int TPC = 256;
+
+// Global table block written by k_pack_fast (blind_rotate_fast.hip), int32 centred Montgomery:
+//   pass p >= 1 block c (m = 4^p): [psi[m+c], psi[2m+2c], psi[2m+2c+1], 0]; pass 0 = block 0 of m = 1
+constexpr uint32_t P0F = 0, P1F = 4, P2F = 20, P3F = 84, P4F = 340, PF_END = 1364;
+constexpr uint32_t P0I = PF_END, P1I = P0I + P1F, P4I = P0I + P4F;
+constexpr uint32_t T4_MONO = 2 * PF_END, T4_WORDS = T4_MONO + 2 * FN;
+// LDS (words): pass 1-3 twiddles (fwd, inv), monomials, 4 local regions, 2 cross areas
+constexpr uint32_t L_TW = 0, L_TWI = P4F - P1F, L_MONO = 2 * L_TWI;  // passes 1-3 (fwd, inv)
+// then, for P polynomials per wavefront: 4 local regions of P x LP words, 2 cross areas of P x XP
+constexpr uint32_t LP = 304, XP = 1152, L_CT = L_MONO + 2 * FN;
+constexpr size_t lds_bytes(int P) { return (size_t)(L_CT + 4 * P * LP + 2 * P * XP) * 4; }
+
+struct Lay {
+    int reg[2];
+    int lane[6];
+    int wave[2];
+};
+__host__ __device__ constexpr Lay lay(int L) {
+    return L == 1   ? Lay{{8, 9}, {2, 3, 4, 6, 7, 5}, {0, 1}}
+           : L == 2 ? Lay{{6, 7}, {2, 3, 8, 9, 4, 5}, {0, 1}}
+           : L == 3 ? Lay{{4, 5}, {2, 3, 6, 8, 9, 7}, {0, 1}}
+           : L == 4 ? Lay{{2, 3}, {4, 5, 6, 8, 9, 7}, {0, 1}}
+                    : Lay{{0, 1}, {2, 3, 4, 5, 6, 7}, {8, 9}};
+}
+// (row stride of the writer's register rows, stride of its wavefront blocks; 0 = local)
+__host__ __device__ constexpr int rstride(int A, int B) {
+    return (A == 1 && B == 2) ? 72 : (A == 2 && B == 3) ? 80 : (A == 3 && B == 4) ? 65
+         : (A == 2 && B == 1) ? 68 : (A == 3 && B == 2) ? 68 : (A == 4 && B == 3) ? 65
+         : (A == 4 && B == 5) ? 72 : 64;
+}
+__host__ __device__ constexpr int wstride(int A, int B) { return (A == 4 && B == 5) ? 288 : (A == 5 && B == 4) ? 257 : 0; }
+// LDS words contributed by index bit b in exchange A -> B (its position in the writer's layout)
+__host__ __device__ constexpr int wt(int A, int B, int b) {
+    for (int k = 0; k < 2; ++k)
+        if (lay(A).reg[k] == b) return rstride(A, B) << k;
+    for (int k = 0; k < 6; ++k)
+        if (lay(A).lane[k] == b) return 1 << k;
+    for (int k = 0; k < 2; ++k)
+        if (lay(A).wave[k] == b) return wstride(A, B) << k;
+    return 1 << 24;
+}
+template <int L>
+__device__ __forceinline__ uint32_t elem(uint32_t w, uint32_t lane, uint32_t r) {
+    uint32_t i = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) i |= ((r >> k) & 1) << lay(L).reg[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) i |= ((lane >> k) & 1) << lay(L).lane[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) i |= ((w >> k) & 1) << lay(L).wave[k];
+    return i;
+}
+// writer register r: row offset (words); reader register r: gather offset (words)
+__host__ __device__ constexpr int st_reg(int A, int B, int r) {
+    int o = 0;
+    for (int k = 0; k < 2; ++k)
+        if ((r >> k) & 1) o += wt(A, B, lay(A).reg[k]);
+    return o;
+}
+__host__ __device__ constexpr int ld_reg(int A, int B, int r) {
+    int o = 0;
+    for (int k = 0; k < 2; ++k)
+        if ((r >> k) & 1) o += wt(A, B, lay(B).reg[k]);
+    return o;
+}
+// reader lane/wave part of a gather address (words)
+template <int A, int B>
+__device__ __forceinline__ uint32_t ld_lane(uint32_t w, uint32_t lane) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o += ((lane >> k) & 1) * (uint32_t)wt(A, B, lay(B).lane[k]);
+    if (wstride(A, B) != 0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) o += ((w >> k) & 1) * (uint32_t)wt(A, B, lay(B).wave[k]);
+    }
+    return o;
+}
+// writer wavefront part of a cross-exchange row address (words)
+template <int A, int B>
+__host__ __device__ constexpr uint32_t st_wave(uint32_t w) {
+    uint32_t o = 0;
+    for (int k = 0; k < 2; ++k) o += ((w >> k) & 1) * (uint32_t)wt(A, B, lay(A).wave[k]);
+    return o;
+}
+
+struct FastConst {  // same layout as blind_rotate_fast.hip's
+    int32_t Q, nQ, qinv, rM;
+    uint32_t Q2, Q4, h1, kacc;
+    int32_t ninv;
+};
+__device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
+    const int32_t m = (int32_t)((uint32_t)T * (uint32_t)K.qinv);
+    return (int32_t)(((int64_t)m * K.nQ + T) >> 32);
+}
+__device__ __forceinline__ int32_t smul(int32_t a, int32_t wM, const FastConst& K) { return sredc((int64_t)a * wM, K); }
+__device__ __forceinline__ uint32_t csub32(uint32_t a, uint32_t m) { return min(a, a - m); }
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i ld_bsk(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+
+__device__ __forceinline__ void bfly_ct(int32_t& a, int32_t& b, int32_t w, const FastConst& K) {
+    const int32_t v = smul(b, w, K), u = a;
+    a = u + v;
+    b = u - v;
+}
+template <bool RED = false>
+__device__ __forceinline__ void bfly_gs(int32_t& a, int32_t& b, int32_t w, const FastConst& K) {
+    const int32_t u = a, v = b;
+    a = RED ? smul(u + v, K.rM, K) : u + v;
+    b = smul(u - v, w, K);
+}
+// radix-4 CT pass over register bits (1, 0): w = [psi[m+c], psi[2m+2c], psi[2m+2c+1]]
+__device__ __forceinline__ void fwd4(int32_t (&x)[4], int32_t w1, int32_t w2, int32_t w3, const FastConst& K) {
+    bfly_ct(x[0], x[2], w1, K);
+    bfly_ct(x[1], x[3], w1, K);
+    bfly_ct(x[0], x[1], w2, K);
+    bfly_ct(x[2], x[3], w3, K);
+}
+template <bool RED>
+__device__ __forceinline__ void inv4(int32_t (&x)[4], int32_t w1, int32_t w2, int32_t w3, const FastConst& K) {
+    bfly_gs(x[0], x[1], w2, K);
+    bfly_gs(x[2], x[3], w3, K);
+    bfly_gs<RED>(x[0], x[2], w1, K);
+    bfly_gs<RED>(x[1], x[3], w1, K);
+}
+
+// ---- LDS traffic (inline asm: counted lgkmcnt waits, addtid stores) ----
+// one polynomial's 4 registers as 4 lane-contiguous rows at M0 + OFF
+template <int A, int B, uint32_t OFF>
+__device__ __forceinline__ void store_rows(const int32_t (&x)[4], uint32_t m0, const int32_t* lds) {
+    asm volatile(
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "ds_write_addtid_b32 %0 offset:%6\n\t"
+        "ds_write_addtid_b32 %1 offset:%7\n\t"
+        "ds_write_addtid_b32 %2 offset:%8\n\t"
+        "ds_write_addtid_b32 %3 offset:%9" ::"v"(x[0]),
+        "v"(x[1]), "v"(x[2]), "v"(x[3]), "s"(m0), "s"(lds), "i"((OFF + st_reg(A, B, 0)) * 4),
+        "i"((OFF + st_reg(A, B, 1)) * 4), "i"((OFF + st_reg(A, B, 2)) * 4), "i"((OFF + st_reg(A, B, 3)) * 4)
+        : "memory");
+}
+template <int A, int B, uint32_t OFF>
+__device__ __forceinline__ void gather_rows(int32_t (&x)[4], uint32_t base, const int32_t* lds) {
+    asm volatile(
+        "ds_read_b32 %0, %4 offset:%6\n\t"
+        "ds_read_b32 %1, %4 offset:%7\n\t"
+        "ds_read_b32 %2, %4 offset:%8\n\t"
+        "ds_read_b32 %3, %4 offset:%9"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+        : "v"(base), "s"(lds), "i"((OFF + ld_reg(A, B, 0)) * 4), "i"((OFF + ld_reg(A, B, 1)) * 4),
+          "i"((OFF + ld_reg(A, B, 2)) * 4), "i"((OFF + ld_reg(A, B, 3)) * 4)
+        : "memory");
+}
+template <uint32_t OFF>
+__device__ __forceinline__ void tw_load(v4i& w, uint32_t addr, const int32_t* lds) {
+    asm volatile("ds_read_b128 %0, %1 offset:%3" : "=&v"(w) : "v"(addr), "s"(lds), "i"(OFF * 4) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(int32_t (&x)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(int32_t (&x)[4], v4i& w) {
+    asm volatile("s_waitcnt lgkmcnt(%5)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(w)
+                 : "i"(N)
+                 : "memory");
+}
+__device__ __forceinline__ void lds_drain_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// per-lane constants of the transforms
+struct LaneCtx {
+    uint32_t g12, g23, g34, g45, g54, g43, g32, g21;  // gather bases (bytes; local ones include the region)
+    uint32_t m_loc;                                   // this wavefront's local region (bytes, uniform)
+    uint32_t m45, m54;                                // cross-store wave offsets (bytes, uniform)
+    uint32_t t1, t2, t3;                              // pass 1 / 2 / 3 twiddle block addresses (bytes)
+    int32_t w0f[3], w0i[3];                           // pass 0 (uniform)
+    v4i w4f, w4i;                                     // pass 4 (per lane)
+};
+
+// ---- transforms of P polynomials (P = 2 per ciphertext of the wavefront) ----
+// Every exchange step runs, per polynomial: wait for its gathered rows, its radix-4 pass, its
+// row stores; then (cross steps: drain + barrier) all gathers.  While polynomial p's pass
+// runs, the rows of p+1.. are still in flight: the wait for polynomial p always leaves the
+// 4 (P-1) younger operations outstanding (the gathers of p+1.. plus the stores of ..p-1).
+// EXP (timing experiments, results invalid): bit 0 no barriers, bit 1 no key loads, bit 3 no
+// transforms at all.
+// FOR_P(body): body once per polynomial with a compile-time constant p
+#define FOR_P(...)                                   \
+    {                                                \
+        { constexpr int p = 0; __VA_ARGS__ }         \
+        { constexpr int p = 1; __VA_ARGS__ }         \
+        if constexpr (P > 2) {                       \
+            { constexpr int p = 2; __VA_ARGS__ }     \
+            { constexpr int p = 3; __VA_ARGS__ }     \
+        }                                            \
+    }
+// wait for polynomial p's gathered rows at the end of a transform (no stores follow)
+template <int P, int p>
+constexpr int tail_wait() { return 4 * (P - 1 - p); }
+
+template <uint32_t XA, int P, int EXP = 0>
+__device__ __forceinline__ void ntt_fwd(int32_t (&X)[P][4], const int32_t* lds, const LaneCtx& C, const FastConst& K) {
+    if constexpr ((EXP & 8) != 0) return;
+    constexpr int W = 4 * (P - 1);
+    v4i w;
+    // pass 0 (L1), exchange 1 -> 2
+    FOR_P(fwd4(X[p], C.w0f[0], C.w0f[1], C.w0f[2], K); store_rows<1, 2, p * LP>(X[p], C.m_loc, lds);)
+    tw_load<L_TW>(w, C.t1, lds);
+    FOR_P(gather_rows<1, 2, p * LP>(X[p], C.g12, lds);)
+    // pass 1 (L2), exchange 2 -> 3
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          fwd4(X[p], w.x, w.y, w.z, K); store_rows<2, 3, p * LP>(X[p], C.m_loc, lds);)
+    tw_load<L_TW + 16>(w, C.t2, lds);
+    FOR_P(gather_rows<2, 3, p * LP>(X[p], C.g23, lds);)
+    // pass 2 (L3), exchange 3 -> 4
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          fwd4(X[p], w.x, w.y, w.z, K); store_rows<3, 4, p * LP>(X[p], C.m_loc, lds);)
+    tw_load<L_TW + 80>(w, C.t3, lds);
+    FOR_P(gather_rows<3, 4, p * LP>(X[p], C.g34, lds);)
+    // pass 3 (L4), cross exchange 4 -> 5
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          fwd4(X[p], w.x, w.y, w.z, K);
+          store_rows<4, 5, XA + p * XP>(X[p], C.m45, lds);)
+    if constexpr (!(EXP & 1)) lds_drain_barrier();
+    FOR_P(gather_rows<4, 5, XA + p * XP>(X[p], C.g45, lds);)
+    // pass 4 (L5)
+    FOR_P(lds_wait<tail_wait<P, p>()>(X[p]); fwd4(X[p], C.w4f.x, C.w4f.y, C.w4f.z, K);)
+}
+
+// inverse (N^-1 folded into the keys), L5 -> L1
+template <uint32_t XA, int P, int EXP = 0>
+__device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, const LaneCtx& C, const FastConst& K) {
+    if constexpr ((EXP & 8) != 0) return;
+    constexpr int W = 4 * (P - 1);
+    v4i w;
+    // (b0 b1) (L5), cross exchange 5 -> 4
+    FOR_P(inv4<false>(X[p], C.w4i.x, C.w4i.y, C.w4i.z, K); store_rows<5, 4, XA + p * XP>(X[p], C.m54, lds);)
+    if constexpr (!(EXP & 1)) lds_drain_barrier();
+    tw_load<L_TWI + 80>(w, C.t3, lds);
+    FOR_P(gather_rows<5, 4, XA + p * XP>(X[p], C.g54, lds);)
+    // (b2 b3) (L4, reduced), exchange 4 -> 3
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          inv4<true>(X[p], w.x, w.y, w.z, K);
+          store_rows<4, 3, p * LP>(X[p], C.m_loc, lds);)
+    tw_load<L_TWI + 16>(w, C.t2, lds);
+    FOR_P(gather_rows<4, 3, p * LP>(X[p], C.g43, lds);)
+    // (b4 b5) (L3), exchange 3 -> 2
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          inv4<false>(X[p], w.x, w.y, w.z, K); store_rows<3, 2, p * LP>(X[p], C.m_loc, lds);)
+    tw_load<L_TWI>(w, C.t1, lds);
+    FOR_P(gather_rows<3, 2, p * LP>(X[p], C.g32, lds);)
+    // (b6 b7) (L2, reduced), exchange 2 -> 1
+    FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
+          inv4<true>(X[p], w.x, w.y, w.z, K); store_rows<2, 1, p * LP>(X[p], C.m_loc, lds);)
+    FOR_P(gather_rows<2, 1, p * LP>(X[p], C.g21, lds);)
+    // (b8 b9) (L1)
+    FOR_P(lds_wait<tail_wait<P, p>()>(X[p]); inv4<false>(X[p], C.w0i[0], C.w0i[1], C.w0i[2], K);)
+}
+
+// NCT ciphertexts per wavefront (the same slots of each): every key row loaded feeds NCT
+// ciphertexts, halving the vector-memory traffic per bootstrap at NCT = 2.
+template <int MINW, int NCT = 1, int EXP = 0>
+__global__ void __launch_bounds__(TPC, MINW)
+k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
+                     const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
+                     uint32_t B) {
+    constexpr int P = 2 * NCT;
+    extern __shared__ __align__(16) int32_t lds[];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < L_TWI; k += TPC) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
+    for (uint32_t k = tid; k < 2 * FN; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    constexpr uint32_t LOCW = P * LP, XAW = P * XP;       // local region per wave, cross area (words)
+    constexpr uint32_t XA0 = 4 * LOCW, XA1 = XA0 + XAW;  // cross areas, relative to L_CT
+
+    LaneCtx C;
+    C.m_loc = (L_CT + w * LOCW) * 4;
+    C.g12 = C.m_loc + ld_lane<1, 2>(w, lane) * 4, C.g23 = C.m_loc + ld_lane<2, 3>(w, lane) * 4;
+    C.g34 = C.m_loc + ld_lane<3, 4>(w, lane) * 4, C.g43 = C.m_loc + ld_lane<4, 3>(w, lane) * 4;
+    C.g32 = C.m_loc + ld_lane<3, 2>(w, lane) * 4, C.g21 = C.m_loc + ld_lane<2, 1>(w, lane) * 4;
+    C.g45 = (L_CT + ld_lane<4, 5>(w, lane)) * 4, C.g54 = (L_CT + ld_lane<5, 4>(w, lane)) * 4;
+    C.m45 = (L_CT + st_wave<4, 5>(w)) * 4, C.m54 = (L_CT + st_wave<5, 4>(w)) * 4;
+    C.t1 = (elem<2>(w, lane, 0) >> 8) * 16, C.t2 = (elem<3>(w, lane, 0) >> 6) * 16;
+    C.t3 = (elem<4>(w, lane, 0) >> 4) * 16;
+    const v4i* tv = reinterpret_cast<const v4i*>(tabs);
+    C.w4f = tv[P4F / 4 + tid], C.w4i = tv[P4I / 4 + tid];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) C.w0f[k] = tabs[P0F + k], C.w0i[k] = tabs[P0I + k];
+
+    const uint32_t Qh = (uint32_t)K.Q >> 1;
+    int32_t acc[NCT][2][4];  // L1, centred canonical
+#pragma unroll
+    for (int q = 0; q < NCT; ++q) {
+        const uint32_t ct = blockIdx.x * NCT + q;
+        const uint64_t* g = acc_io + (size_t)(ct < B ? ct : 0) * 2 * FN;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t v0 = ct < B ? g[p * FN + elem<1>(w, lane, r)] : 0;
+                const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
+                acc[q][p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
+            }
+    }
+    __syncthreads();
+
+    // C = N^-1 NTT(acc) in L5
+    int32_t Cp[P][4];
+#pragma unroll
+    for (int q = 0; q < NCT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][1][r];
+    ntt_fwd<XA1, P, EXP>(Cp, lds, C, K);
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cp[p][r] = smul(Cp[p][r], K.ninv, K);
+
+    constexpr uint32_t ROWB = 2 * FDG2 * 2 * FN * 4;  // key bytes per round
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * ROWB), 0x00020000);
+    const uint32_t voff = tid * 16;  // 4 consecutive slots per lane
+    const uint32_t et = 2 * (__builtin_bitreverse32(tid) >> 24) + 1;  // slot 4t + r: e = 512 bitrev2(r) + et
+    const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;
+
+    // group gi = (key k, column j) of digit l (l = 3: the C rows): rows 2l (poly 0), 2l + 1 (poly 1)
+    auto issue = [&](v4i (&pw)[2], uint32_t round_off, int l, int gi) {
+        const int k = gi >> 1, j = gi & 1;
+        if constexpr ((EXP & 2) != 0) {
+            pw[0] = v4i{(int)round_off, l, gi, 4}, pw[1] = pw[0] + 1;
+            return;
+        }
+        pw[0] = ld_bsk(rsrc, voff, round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4);
+        pw[1] = ld_bsk(rsrc, voff, round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4);
+    };
+    auto mac = [&](int64_t (&s)[NCT][2][2][4], const int32_t (&X)[P][4], const v4i (&pw)[2], int gi) {
+        const int k = gi >> 1, j = gi & 1;
+        const int32_t w0[4] = {pw[0].x, pw[0].y, pw[0].z, pw[0].w};
+        const int32_t w1[4] = {pw[1].x, pw[1].y, pw[1].z, pw[1].w};
+#pragma unroll
+        for (int q = 0; q < NCT; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s[q][k][j][r] = (int64_t)X[2 * q][r] * w0[r] + s[q][k][j][r];
+                s[q][k][j][r] = (int64_t)X[2 * q + 1][r] * w1[r] + s[q][k][j][r];
+            }
+    };
+
+    v4i pw[4][2];  // key ring: the rows of the digit being consumed / about to be
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) issue(pw[gi], 0, 3, gi);
+
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t round_off = i * ROWB;
+        uint32_t ai[NCT];  // a'_i = ((amod - a_i) mod amod) * (2N / amod)  (rgsw-acc-cggi.cpp:153)
+#pragma unroll
+        for (int q = 0; q < NCT; ++q) {
+            const uint32_t ct = blockIdx.x * NCT + q;
+            const uint32_t ar = ct < B ? (uint32_t)(a[(size_t)ct * n + i] & amask) : 0;
+            ai[q] = __builtin_amdgcn_readfirstlane(((amask + 1 - ar) & amask) << ashift);
+        }
+        int64_t s[NCT][2][2][4];
+#pragma unroll
+        for (int q = 0; q < NCT; ++q)
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) s[q][k][j][r] = 0;
+
+        // the C digit (no transform); its groups' registers take digit 0's rows
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+            __builtin_amdgcn_sched_barrier(0);
+            mac(s, Cp, pw[gi], gi);
+            issue(pw[gi], round_off, 0, gi);
+        }
+#pragma unroll
+        for (uint32_t l = 0; l < FDIG - 1; ++l) {
+            const int32_t kl = (int32_t)(((1u << (FLOGG * l)) - 1) / ((1u << FLOGG) - 1)) << (FLOGG - 1);
+            int32_t X[P][4];
+#pragma unroll
+            for (int q = 0; q < NCT; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    X[2 * q][r] = __builtin_amdgcn_sbfe(acc[q][0][r] + kl, FLOGG * l, FLOGG);
+                    X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, FLOGG * l, FLOGG);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            if (l & 1) ntt_fwd<XA1, P, EXP>(X, lds, C, K);
+            else ntt_fwd<XA0, P, EXP>(X, lds, C, K);
+            // next digit's rows (after digit 2: the next round's C rows; the last round re-fetches)
+            const uint32_t noff = l < 2 ? round_off : (i + 1 < n ? i + 1 : i) * ROWB;
+            const int nl = l < 2 ? (int)l + 1 : 3;
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) {
+                __builtin_amdgcn_sched_barrier(0);
+                mac(s, X, pw[gi], gi);
+                issue(pw[gi], noff, nl, gi);
+            }
+        }
+
+        // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1); rotated monomial table
+        __builtin_amdgcn_sched_barrier(0);
+        const char* mono = reinterpret_cast<const char*>(lds + L_MONO);
+        int32_t S[P][4];
+#pragma unroll
+        for (int q = 0; q < NCT; ++q) {
+            const uint32_t bp = (et * ai[q]) & 2047, bn = (0u - bp) & 2047;
+            const uint32_t F4p = ((bp >> 4) & 0x1C) | ((bp & 63) << 7), F4n = ((bn >> 4) & 0x1C) | ((bn & 63) << 7);
+            const uint32_t hp = (bp >> 4) & 0x60, hn = (bn >> 4) & 0x60;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t c = ((r & 1) << 1) | (r >> 1);  // bitrev2(r)
+                const uint32_t cs = c * 32 * ai[q];             // uniform
+                const int32_t mp = *reinterpret_cast<const int32_t*>(mono + ((((hp + cs) & 0x60)) | F4p));
+                const int32_t mn = *reinterpret_cast<const int32_t*>(mono + ((((hn - cs) & 0x60)) | F4n));
+                const int32_t A00 = sredc(s[q][0][0][r], K), A01 = sredc(s[q][0][1][r], K);
+                const int32_t A10 = sredc(s[q][1][0][r], K), A11 = sredc(s[q][1][1][r], K);
+                S[2 * q][r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
+                S[2 * q + 1][r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
+            }
+        }
+        // C <- C + S, reduced every 8 rounds
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Cp[p][r] += S[p][r];
+        if ((i & 7) == 7) {
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Cp[p][r] = smul(Cp[p][r], K.rM, K);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        ntt_inv<XA1, P, EXP>(S, lds, C, K);
+#pragma unroll
+        for (int q = 0; q < NCT; ++q)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    uint32_t u = (uint32_t)(acc[q][p][r] + S[2 * q + p][r]) + K.kacc;
+                    u = csub32(csub32(csub32(u, K.Q4), K.Q2), (uint32_t)K.Q);
+                    acc[q][p][r] = (int32_t)(u - K.h1);
+                }
+    }
+#pragma unroll
+    for (int q = 0; q < NCT; ++q) {
+        const uint32_t ct = blockIdx.x * NCT + q;
+        if (ct >= B) continue;
+        uint64_t* g = acc_io + (size_t)ct * 2 * FN;
+        // acc0 transposed (X -> X^-1, poly.cpp:762-770): out[(N-k) mod N] = -acc0[k]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t k = elem<1>(w, lane, r);
+            const uint32_t v = (uint32_t)(acc[q][0][r] < 0 ? acc[q][0][r] + K.Q : acc[q][0][r]);
+            const uint32_t v1 = (uint32_t)(acc[q][1][r] < 0 ? acc[q][1][r] + K.Q : acc[q][1][r]);
+            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
+            g[FN + k] = v1;
+        }
+    }
+}
+
+// generic psi / ipsi / mono tables (plain u32) -> the table block above (centred Montgomery)
+__global__ void k_pack_tables4(uint32_t Q, const uint32_t* __restrict__ psi, const uint32_t* __restrict__ ipsi,
+                               const uint32_t* __restrict__ mono, int32_t* __restrict__ out) {
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    auto mont = [Q](uint32_t v) {
+        const uint32_t m = (uint32_t)(((uint64_t)v << 32) % Q);
+        return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+    };
+    if (idx < PF_END) {
+        uint32_t m, base;
+        if (idx < P1F) m = 1, base = P0F;
+        else if (idx < P2F) m = 4, base = P1F;
+        else if (idx < P3F) m = 16, base = P2F;
+        else if (idx < P4F) m = 64, base = P3F;
+        else m = 256, base = P4F;
+        const uint32_t c = (idx - base) >> 2, e = (idx - base) & 3;
+        const uint32_t k = e == 0 ? m + c : 2 * m + 2 * c + (e - 1);
+        out[idx] = e == 3 ? 0 : mont(psi[k]);
+        out[P0I + idx] = e == 3 ? 0 : mont(ipsi[k]);
+    }
+    if (idx < 2 * FN) out[T4_MONO + ((idx >> 6) | ((idx & 63) << 5))] = mont(mono[idx]);
+}
+
+}  // namespace f4
+
+size_t fast4_table_words() { return f4::T4_WORDS; }
+
+hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, hipStream_t s) {
+    hipLaunchKernelGGL(f4::k_pack_tables4, dim3((f4::T4_WORDS + 255) / 256), dim3(256), 0, s, Q,
+                       (const uint32_t*)T.psi, (const uint32_t*)T.ipsi, (const uint32_t*)T.mono, (int32_t*)out);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
+                                     const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s) {
+    const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
+    auto launch = [&](auto kern, int nct) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)f4::lds_bytes(2 * nct));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct - 1) / nct)), dim3(f4::TPC), f4::lds_bytes(2 * nct), s, Kc,
+                           n, loga, tabs4, bsk, a, acc, (uint32_t)B);
+    };
+    switch (variant) {
+        case 59: launch(f4::k_blind_rotate_fast4<3, 1>, 1); break;
+        case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;      // two ciphertexts per wavefront
+        case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1>, 1); break;   // timing only: no barriers
+        case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2>, 1); break;   // timing only: no key loads
+        case 65: launch(f4::k_blind_rotate_fast4<4, 1, 8>, 1); break;   // timing only: no transforms
+        case 71: launch(f4::k_blind_rotate_fast4<2, 2, 1>, 2); break;   // timing only: no barriers
+        case 72: launch(f4::k_blind_rotate_fast4<2, 2, 2>, 2); break;   // timing only: no key loads
+        case 75: launch(f4::k_blind_rotate_fast4<2, 2, 8>, 2); break;   // timing only: no transforms
+        default: launch(f4::k_blind_rotate_fast4<4, 1>, 1); break;      // = 60: 4 waves/SIMD
+    }
+    return hipGetLastError();
+}
+
+}  // namespace tfhe

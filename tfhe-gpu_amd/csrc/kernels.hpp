@@ -42,6 +42,12 @@ bool fast_path_supported(const BRParams& P, int word_bits);
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s);
 size_t bsk_fast_bytes(const BRParams& P);
+// 4-wavefront variant (blind_rotate_fast4.hip): its table block, packed behind the fast tables,
+// and its launch (K: the fast kernel's FastConst).
+size_t fast4_table_words();
+hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, hipStream_t s);
+hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
+                                     const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s);
 
 // Exact-FP64 blind rotation for 2^32 <= Q < 2^40 (STD192 class): keys/tables as centred
 // doubles derived on device from the generic (u64) arena.

@@ -1,0 +1,66 @@
+"""Per-index worst-case magnitude bounds for the 4-wavefront fast kernel's transforms
+(blind_rotate_fast4.hip): radix-4 passes over index bit pairs (b9 b8), (b7 b6), ... (b1 b0)
+(forward, Cooley-Tukey) and the reverse (inverse, Gentleman-Sande), signed Montgomery
+products (|smul(y, w)| <= |y| (Q/2) / 2^32 + Q/2).  RED lists, per inverse pass, which stage's
+sum outputs are reduced (smul by R mod Q).  Asserts every 32-bit value < 2^31, the external
+product row sums < 2^63, and the accumulator update window.  Run: python3 tools/bounds_fast4.py [Q]"""
+import sys
+
+Q = int(sys.argv[1]) if len(sys.argv) > 1 else 134215681
+Qh = Q // 2
+LIM = 2 ** 31
+RED = {0: "B", 1: None, 2: "B", 3: None, 4: "B"}   # inverse pass -> stage whose sums are reduced
+
+
+def smul_b(y):
+    assert y < LIM, f"smul input {y / Q:.2f}Q"
+    return y * Qh / 2 ** 32 + LIM * Q / 2 ** 32
+
+
+def fwd(b_in):
+    b = list(b_in)
+    for p in range(5):
+        for bit in (9 - 2 * p, 8 - 2 * p):
+            m = 1 << bit
+            nb = list(b)
+            for i in range(1024):
+                if not i & m:
+                    j = i | m
+                    v = smul_b(b[j])
+                    nb[i] = nb[j] = b[i] + v
+                    assert nb[i] < LIM
+            b = nb
+    return b
+
+
+def inv(b_in):
+    b = list(b_in)
+    for p in range(5):
+        for s, bit in enumerate((2 * p, 2 * p + 1)):
+            m = 1 << bit
+            nb = list(b)
+            red = RED[p] == "AB"[s]
+            for i in range(1024):
+                if not i & m:
+                    j = i | m
+                    t = b[i] + b[j]
+                    assert t < LIM, f"inverse pass {p} stage {s}: {t / Q:.2f}Q"
+                    nb[i] = smul_b(t) if red else t
+                    nb[j] = smul_b(t)
+            b = nb
+    return b
+
+
+F = max(fwd([64] * 1024))                 # digit transforms
+C0 = smul_b(max(fwd([Qh + 1] * 1024)))    # C = N^-1 NTT(acc)
+rowsum = 6 * F * Qh + 2 * F * Qh          # 3 digits + C (kept <= F) over 2 polynomials
+assert rowsum < 2 ** 63
+A = rowsum / 2 ** 32 + Qh                 # sredc of the row sum
+S = (2 * A * Qh) / 2 ** 32 + Qh           # monomial combination
+Cmax = C0 + 8 * S
+Cred = smul_b(Cmax)
+assert max(C0, Cred) + 7 * S <= F
+out = max(inv([S] * 1024))
+assert out < 3 * Q, f"inverse output {out / Q:.2f}Q"
+print(f"Q={Q}: fwd {F / Q:.3f}Q, C {(max(C0, Cred) + 7 * S) / Q:.3f}Q, S {S / Q:.3f}Q, "
+      f"inverse out {out / Q:.3f}Q (reductions {RED})  OK")

@@ -46,6 +46,11 @@ def main():
             v, _ = per_launch(mix, kname, c)
             if v is not None:
                 res[c.lower() + "_per_launch"] = v
+        # duration of the profiled dispatches that carried GRBM_GUI_ACTIVE (same pass: clock = GUI / 8 / time)
+        ds = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in mix
+              if kname in r.get("Kernel_Name", "") and r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("End_Timestamp")]
+        if ds:
+            res["gui_pass_kernel_ns_per_launch"] = sum(ds) / len(ds)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
