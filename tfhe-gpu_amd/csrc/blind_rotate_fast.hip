@@ -1,8 +1,11 @@
 // blind_rotate_fast.hip -- CGGI blind rotation specialised for the STD128 class
-// (N = 1024, dG2 = 8, baseG = 2^7, Q < 2^27; STD128, STD128_OPT).
+// (N = 1024, dG2 = 8, baseG = 2^7, Q < 2^27; STD128, STD128_OPT): the key/table packing
+// shared by both specialised kernels, the two-wavefront kernel k_blind_rotate_fast2 and the
+// launcher, which runs the four-wavefront kernel of blind_rotate_fast4.hip by default.
 //
 // Same math as the generic kernel and the oracle (rgsw-acc-cggi.cpp:246-307 and
-// rgsw-acc.cpp:57-111), re-organised for gfx950:
+// rgsw-acc.cpp:57-111), re-organised for gfx950 (k_blind_rotate_fast2's layout below;
+// blind_rotate_fast4.hip describes its own):
 //
 //  * Two wavefronts (128 lanes) per ciphertext, two ciphertexts per workgroup.
 //    A lane holds 8 coefficients of each polynomial; a 1024-point negacyclic
@@ -68,7 +71,6 @@ constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS =
 // reading wavefront) x 2 polynomials x PS words.
 // (NB = 1: one buffer and an extra barrier before each cross-wavefront store)
 constexpr uint32_t PS = 576, WS = 2 * PS, XBUF = 2 * WS;
-constexpr size_t lds_bytes(int cts, int nb) { return (size_t)(T_WORDS + cts * nb * XBUF) * 4; }
 // the fast key buffer: [T_WORDS tables][4-wave kernel tables (blind_rotate_fast4.hip)][key rows]
 constexpr uint32_t T4W = 4776, TB_WORDS = T_WORDS + T4W;
 
@@ -404,181 +406,6 @@ __device__ __forceinline__ void ntt_inv2(int32_t (&x0)[8], int32_t (&x1)[8], con
     inv_pass8(x1, lo, hi, K);
 }
 
-// MINW: minimum waves per SIMD requested from the register allocator.
-// ACC64: exact 64-bit sums over all 8 rows, one reduction per output (32 more VGPRs);
-//        otherwise every digit's row pair is reduced into a 32-bit sum.
-// CTS: ciphertexts per workgroup (a workgroup barrier then spans 2*CTS wavefronts).
-// PF: BSK groups (of 4) whose loads are issued before the digit's forward NTT, so their
-//     latency hides behind it (16 VGPRs each); the rest are loaded when the MAC starts.
-// EXP: timing experiments (results invalid): 1 one BSK slice, 2 no BSK loads, 3 no barriers
-//      inside the transforms, 4 = 2 + 3.
-// NB: exchange buffers per ciphertext (2: alternate, 1: smaller LDS footprint, more barriers).
-template <int MINW, bool ACC64, int CTS, int EXP = 0, int PF = 0, int NB = 2>
-__global__ void __launch_bounds__(TPC * CTS, MINW)
-k_blind_rotate_fast(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
-                    const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
-                    uint32_t B) {
-    extern __shared__ __align__(16) int32_t lds[];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < T_WORDS; k += TPC * CTS) lds[k] = tabs[k];
-    const uint32_t cl = __builtin_amdgcn_readfirstlane(tid / TPC), t = tid % TPC;
-    const uint32_t ct = blockIdx.x * CTS + cl;
-    const bool active = ct < B;
-    const uint32_t ctbase = (T_WORDS + cl * NB * XBUF) * 4;  // bytes, uniform
-
-    LaneCtx C;
-    C.w = __builtin_amdgcn_readfirstlane(t >> 6);
-    C.f12 = ld_lane<1, 2>(t), C.f23 = ld_lane<2, 3>(t), C.f34 = ld_lane<3, 4>(t);
-    C.f43 = ld_lane<4, 3>(t), C.f32 = ld_lane<3, 2>(t), C.f21 = ld_lane<2, 1>(t);
-    const uint32_t w6 = t >> 6;
-    C.a2 = ((((t >> 3) & 3) | (w6 << 2)) * 16);            // block i >> 7 in L2
-    C.a3 = (((t & 31) | (w6 << 5)) * 16);                  // block i >> 4 in L3
-    const uint32_t nslot = ((t >> 5) & 1) | ((t & 31) << 1) | (w6 << 6);  // i >> 3 in L4
-    C.a4 = t * 16;                                          // TW4 is stored in lane order
-    C.zero = 0;
-
-    uint64_t* g = acc_io + (size_t)(active ? ct : 0) * 2 * FN;
-    const uint32_t Qh = (uint32_t)K.Q >> 1;
-    int32_t acc[2][8];  // L1, centred canonical, [-(Q>>1)-1, Q>>1)
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const uint64_t v0 = active ? g[p * FN + elem<1>(t, r)] : 0;
-            const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
-            acc[p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
-        }
-    __syncthreads();
-
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * (2 * FDG2 * 2 * FN * 4)), 0x00020000);
-    const uint32_t voff = nslot * 32;  // 8 consecutive slots per lane in L4
-    // slot exponent of L4 slot 8 nslot + r: e = 256 bitrev3(r) + et, et = 2 bitrev7(nslot) + 1
-    const uint32_t et = 2 * (__builtin_bitreverse32(nslot) >> 25) + 1;
-    const uint64_t* ap = a + (size_t)(active ? ct : 0) * n;
-    const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;  // 2N = 2^11
-    for (uint32_t i = 0; i < n; ++i) {
-        // a'_i = ((amod - a_i) mod amod) * (2N / amod)  (rgsw-acc-cggi.cpp:153)
-        const uint32_t ar = active ? (uint32_t)(ap[i] & amask) : 0;
-        const uint32_t ai = ((amask + 1 - ar) & amask) << ashift;
-
-        int64_t s[2][2][8];   // ACC64: exact sums
-        int32_t s32[2][2][8]; // otherwise: per-digit reduced sums
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    if constexpr (ACC64) s[k][j][r] = 0;
-                    else s32[k][j][r] = 0;
-                }
-
-        // BSK rows through a buffer resource: lane offset in a VGPR, row offset in an SGPR
-        const uint32_t round_off = EXP == 1 ? 0u : i * (2 * FDG2 * 2 * FN * 4);
-        // five cross-wavefront exchanges per round alternate between the two buffers
-        const uint32_t par = NB == 2 ? (i & 1) : 0;
-#pragma unroll
-        for (uint32_t l = 0; l < FDIG; ++l) {
-            const uint32_t sbuf = ctbase + ((par + l) & (NB - 1)) * XBUF * 4;
-            // signed digit l of the centred c (rgsw-acc.cpp:83-109, carries included):
-            //   d_l = (c + 64 (1 + 128 + ... + 128^(l-1))) >> 7l,  digit = sext7(d_l);
-            //   the top digit |d_3| <= 33 is its own sext7, so one v_bfe_i32 serves all four
-            const int32_t kl = (int32_t)(((1u << (FLOGG * l)) - 1) / ((1u << FLOGG) - 1)) << (FLOGG - 1);
-            int32_t x0[8], x1[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                x0[r] = __builtin_amdgcn_sbfe(acc[0][r] + kl, FLOGG * l, FLOGG);
-                x1[r] = __builtin_amdgcn_sbfe(acc[1][r] + kl, FLOGG * l, FLOGG);
-            }
-            // rows 2l (poly 0, digit l) and 2l+1 (poly 1, digit l); group g = (key k, poly j)
-            v4i pw[4][4];
-            auto issue = [&](int g) {
-                const int k = g >> 1, j = g & 1;
-                const uint32_t s0 = round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4;      // uniform
-                const uint32_t s1 = round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4;  // uniform
-                if constexpr (EXP == 2 || EXP == 4) {
-                    pw[g][0] = v4i{(int)s0, (int)s1, 3, 4};
-                    pw[g][1] = pw[g][0] + 1, pw[g][2] = pw[g][0] + 2, pw[g][3] = pw[g][0] + 3;
-                } else {
-                    pw[g][0] = ld_bsk(rsrc, voff, s0), pw[g][1] = ld_bsk(rsrc, voff + 16, s0);
-                    pw[g][2] = ld_bsk(rsrc, voff, s1), pw[g][3] = ld_bsk(rsrc, voff + 16, s1);
-                }
-            };
-#pragma unroll
-            for (int g = 0; g < PF; ++g) issue(g);
-            __builtin_amdgcn_sched_barrier(0);
-            ntt_fwd2<NB, (EXP < 3 ? 3 : 0)>(x0, x1, lds, sbuf, C, K);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int k = g >> 1, j = g & 1;
-                // groups not prefetched: one at a time, which bounds the staging registers
-                __builtin_amdgcn_sched_barrier(0);
-                if (g >= PF) issue(g);
-                const v4i a0 = pw[g][0], a1 = pw[g][1], b0 = pw[g][2], b1 = pw[g][3];
-                const int32_t w0[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                const int32_t w1[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    if constexpr (ACC64) {
-                        s[k][j][r] = (int64_t)x0[r] * w0[r] + s[k][j][r];
-                        s[k][j][r] = (int64_t)x1[r] * w1[r] + s[k][j][r];
-                    } else {
-                        const int64_t T = (int64_t)x0[r] * w0[r] + (int64_t)x1[r] * w1[r];
-                        s32[k][j][r] += sredc(T, K);
-                    }
-                }
-            }
-        }
-
-        // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1)
-        const uint32_t b4 = (et * ai) << 2;       // byte offsets into the 2N-entry table
-        const uint32_t st4 = (ai << 10) & 8191;   // 256 * ai * 4 mod 8192
-        const char* mono = reinterpret_cast<const char*>(lds + T_MONO);
-        int32_t S0[8], S1[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const uint32_t c = __builtin_bitreverse32((uint32_t)r) >> 29;
-            const uint32_t e4 = b4 + c * st4;
-            const int32_t mp = *reinterpret_cast<const int32_t*>(mono + (e4 & 8188));
-            const int32_t mn = *reinterpret_cast<const int32_t*>(mono + ((0u - e4) & 8188));
-            int32_t A00, A01, A10, A11;
-            if constexpr (ACC64) {
-                A00 = sredc(s[0][0][r], K), A01 = sredc(s[0][1][r], K);
-                A10 = sredc(s[1][0][r], K), A11 = sredc(s[1][1][r], K);
-            } else {
-                A00 = s32[0][0][r], A01 = s32[0][1][r], A10 = s32[1][0][r], A11 = s32[1][1][r];
-            }
-            S0[r] = sredc((int64_t)A00 * mp + (int64_t)A10 * mn, K);
-            S1[r] = sredc((int64_t)A01 * mp + (int64_t)A11 * mn, K);
-        }
-        ntt_inv2<NB, (EXP < 3 ? 3 : 0)>(S0, S1, lds, ctbase + ((par + FDIG - 1) & (NB - 1)) * XBUF * 4,
-                     ctbase + ((par + FDIG) & (NB - 1)) * XBUF * 4,
-                      C, K);
-        // acc <- centred canonical (acc + S): u = acc + S + (Q>>1) + 1 + 4Q in (0, 8Q)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            uint32_t u0 = (uint32_t)(acc[0][r] + S0[r]) + K.kacc;
-            uint32_t u1 = (uint32_t)(acc[1][r] + S1[r]) + K.kacc;
-            u0 = csub32(csub32(csub32(u0, K.Q4), K.Q2), (uint32_t)K.Q);
-            u1 = csub32(csub32(csub32(u1, K.Q4), K.Q2), (uint32_t)K.Q);
-            acc[0][r] = (int32_t)(u0 - K.h1);
-            acc[1][r] = (int32_t)(u1 - K.h1);
-        }
-    }
-    if (active) {
-        // acc0 transposed (X -> X^-1, poly.cpp:762-770): out[(N-k) mod N] = -acc0[k]
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const uint32_t k = elem<1>(t, r);
-            const uint32_t v = (uint32_t)(acc[0][r] < 0 ? acc[0][r] + K.Q : acc[0][r]);
-            const uint32_t v1 = (uint32_t)(acc[1][r] < 0 ? acc[1][r] + K.Q : acc[1][r]);
-            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
-            g[FN + k] = v1;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // k_blind_rotate_fast2: the same round with one digit's transforms eliminated.
 //
@@ -833,13 +660,10 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     }
 }
 
-// generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies, twiddles
-// packed per pass (see the table-block comment above)
-// PackMode: which kernel the copy is for (k_blind_rotate_fast: plain rows and table;
-// k_blind_rotate_fast2: digit-3-eliminated rows (hc[l] = 2^(7l-21), hc[3] = N 2^-21 mod Q)
-// and/or the rotated monomial table).
+// generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies: key rows with the
+// top digit folded in (hc[l] = 2^(7l-21), hc[3] = N 2^-21 mod Q; see k_blind_rotate_fast2),
+// twiddles packed per pass (table-block comment above), monomials in the rotated layout.
 struct PackMode {
-    uint32_t horner, mrot;
     uint32_t hc[4];
 };
 __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t words, const uint32_t* __restrict__ psi,
@@ -851,14 +675,11 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
         return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
     };
     if (idx < words) {
-        uint32_t v = bsk[idx];
-        if (M.horner) {
-            // idx = (((i * 2 + k) * 8 + row) * 2 + j) * N + slot; row = 2l + p
-            const uint32_t row = (uint32_t)((idx / (2 * FN)) % FDG2), l = row >> 1, p = row & 1;
-            const size_t i6 = idx + ((size_t)(6 + p) - row) * 2 * FN;  // row 6 + p, same k, j, slot
-            const uint64_t w6 = (uint64_t)(bsk[i6] % Q) * M.hc[l] % Q;
-            v = l < 3 ? (uint32_t)(((uint64_t)(v % Q) + Q - w6) % Q) : (uint32_t)w6;
-        }
+        // idx = (((i * 2 + k) * 8 + row) * 2 + j) * N + slot; row = 2l + p
+        const uint32_t row = (uint32_t)((idx / (2 * FN)) % FDG2), l = row >> 1, p = row & 1;
+        const size_t i6 = idx + ((size_t)(6 + p) - row) * 2 * FN;  // row 6 + p, same k, j, slot
+        const uint64_t w6 = (uint64_t)(bsk[i6] % Q) * M.hc[l] % Q;
+        const uint32_t v = l < 3 ? (uint32_t)(((uint64_t)(bsk[idx] % Q) + Q - w6) % Q) : (uint32_t)w6;
         out[TB_WORDS + idx] = mont(v);
     }
     if (idx < TW_WORDS) {
@@ -883,7 +704,7 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
     }
     if (idx < 2 * FN) {
         const uint32_t e = (uint32_t)idx;
-        out[T_MONO + (M.mrot ? (e >> 6) | ((e & 63) << 5) : e)] = mont(mono[idx]);
+        out[T_MONO + ((e >> 6) | ((e & 63) << 5))] = mont(mono[idx]);
     }
 }
 
@@ -897,9 +718,9 @@ bool fast_path_supported(const BRParams& P, int word_bits) {
 size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * FN + TB_WORDS) * 4; }
 
 namespace {
-// TFHE_FAST_VARIANT selects the kernel build (A/B experiments); < 30: k_blind_rotate_fast
-// (plain key rows and monomial table), 30-59: k_blind_rotate_fast2, >= 60 (default):
-// k_blind_rotate_fast4 (blind_rotate_fast4.hip; 59 is its 3-waves/SIMD build).
+// TFHE_FAST_VARIANT selects the kernel build (A/B experiments): 30-58 k_blind_rotate_fast2
+// (two wavefronts per ciphertext), >= 59 k_blind_rotate_fast4 (blind_rotate_fast4.hip; 60 =
+// default).  The variant table is in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 60;
 int fast_variant() {
     static const int v = [] {
@@ -924,13 +745,9 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
                                 hipStream_t s) {
     const size_t words = (size_t)P.n * 2 * FDG2 * 2 * FN;
     PackMode M{};
-    if (fast_variant() >= 30) {
-        M.horner = 1;
-        M.mrot = 1;
-        const uint64_t Q = P.Q, i21 = powmod(2, Q - 1 - 21, Q);  // 2^-21 (Q prime)
-        for (int l = 0; l < 3; ++l) M.hc[l] = (uint32_t)((unsigned __int128)powmod(2, 7 * l, Q) * i21 % Q);
-        M.hc[3] = (uint32_t)((unsigned __int128)FN * i21 % Q);
-    }
+    const uint64_t Q = P.Q, i21 = powmod(2, Q - 1 - 21, Q);  // 2^-21 (Q prime)
+    for (int l = 0; l < 3; ++l) M.hc[l] = (uint32_t)((unsigned __int128)powmod(2, 7 * l, Q) * i21 % Q);
+    M.hc[3] = (uint32_t)((unsigned __int128)FN * i21 % Q);
     hipLaunchKernelGGL(k_pack_fast, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint32_t)P.Q,
                        (const uint32_t*)bsk, words, (const uint32_t*)T.psi, (const uint32_t*)T.ipsi,
                        (const uint32_t*)T.mono, (int32_t*)bsk_fast, M);
@@ -963,60 +780,19 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     const int variant = fast_variant();
     if (variant >= 59)
         return launch_blind_rotate_fast4(variant, &K, P.n, loga, tabs + T_WORDS, bsk, a, acc, B, s);
-    auto launch = [&](auto kern, int cts, int nb = 2) {
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(cts, nb));
-        hipLaunchKernelGGL(kern, dim3((unsigned)((B + cts - 1) / cts)), dim3(TPC * cts), lds_bytes(cts, nb), s, K, P.n,
-                           loga, tabs, bsk, a, acc, (uint32_t)B);
-    };
     auto launch2 = [&](auto kern, int nb = 1) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes2(2, nb));
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(TPC * 2), lds_bytes2(2, nb), s, K, P.n, loga,
                            tabs, bsk, a, acc, (uint32_t)B);
     };
     switch (variant) {
-        // k_blind_rotate_fast2 <MINW, PF, PFA, MROT>
-        case 30: launch2(k_blind_rotate_fast2<3, 2, 4, true>); break;
-        case 31: launch2(k_blind_rotate_fast2<3, 2, 2, true>); break;
-        case 32: launch2(k_blind_rotate_fast2<3, 2, 0, true>); break;
-        case 33: launch2(k_blind_rotate_fast2<3, 0, 4, true>); break;
+        // k_blind_rotate_fast2 <MINW, PF, PFA, MROT, NB, DEPTH, EXP>
         case 34: launch2(k_blind_rotate_fast2<3, 1, 4, true>); break;
-        case 35: launch2(k_blind_rotate_fast2<3, 1, 2, true>); break;
-        case 36: launch2(k_blind_rotate_fast2<3, 0, 2, true>); break;
-        case 37: launch2(k_blind_rotate_fast2<3, 1, 4, true, 1, 1>); break;
-        case 38: launch2(k_blind_rotate_fast2<3, 0, 4, true, 1, 1>); break;
-        case 39: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1>); break;
-        case 43: launch2(k_blind_rotate_fast2<2, 2, 4, true, 2, 1>, 2); break;
-        case 51: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 1>); break;  // timing only
-        case 52: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 2>); break;  // timing only
-        case 53: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 3>); break;  // timing only
-        case 54: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 4>); break;  // timing only
         case 40: launch2(k_blind_rotate_fast2<2, 4, 4, true, 2>, 2); break;
-        case 41: launch2(k_blind_rotate_fast2<2, 2, 4, true, 2>, 2); break;
-        case 42: launch2(k_blind_rotate_fast2<2, 4, 4, true, 1>); break;
-        case 1: launch(k_blind_rotate_fast<3, false, 2>, 2); break;
-        case 2: launch(k_blind_rotate_fast<3, true, 1>, 1); break;
-        case 3: launch(k_blind_rotate_fast<2, true, 2>, 2); break;
-        case 4: launch(k_blind_rotate_fast<3, false, 1>, 1); break;
-        case 9: launch(k_blind_rotate_fast<3, true, 2, 1>, 2); break;  // timing experiment: one BSK slice
-        case 10: launch(k_blind_rotate_fast<3, true, 2, 2>, 2); break; // timing experiment: no BSK loads
-        case 13: launch(k_blind_rotate_fast<2, true, 2, 0, 4>, 2); break;
-        case 14: launch(k_blind_rotate_fast<3, false, 2, 0, 4>, 2); break;
-        case 15: launch(k_blind_rotate_fast<3, true, 2, 0, 2>, 2); break;
-        case 16: launch(k_blind_rotate_fast<2, true, 2, 0, 2>, 2); break;
-        case 17: launch(k_blind_rotate_fast<4, false, 2, 0, 0, 1>, 2, 1); break;
-        case 18: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1); break;
-        case 19: launch(k_blind_rotate_fast<4, true, 2, 0, 0, 1>, 2, 1); break;
-        case 20: launch(k_blind_rotate_fast<3, true, 2, 0, 0, 1>, 2, 1); break;
-        case 21: launch(k_blind_rotate_fast<3, true, 2, 0, 2, 2>, 2, 2); break;
-        case 23: launch(k_blind_rotate_fast<3, true, 2, 3, 2, 1>, 2, 1); break; // timing: no barriers
-        case 24: launch(k_blind_rotate_fast<3, true, 2, 4, 2, 1>, 2, 1); break; // timing: neither
-        case 22: launch(k_blind_rotate_fast<3, true, 1, 0, 2, 1>, 1, 1); break;
-        // default: 3 waves/SIMD (VGPRs <= 168 and 3 x 35 KB of LDS per CU), exact 64-bit
-        // row sums, half of each digit's BSK prefetched behind its forward NTT
-        default:
-            if (variant >= 30) launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1>);  // = 39
-            else launch(k_blind_rotate_fast<3, true, 2, 0, 2, 1>, 2, 1);
-            break;
+        case 51: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 1>); break;  // timing only: no pre-store barriers
+        case 52: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 2>); break;  // timing only: no barriers
+        case 53: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1, 3>); break;  // timing only: no key loads
+        default: launch2(k_blind_rotate_fast2<3, 1, 2, true, 1, 1>); break;     // = 39
     }
     return hipGetLastError();
 }
