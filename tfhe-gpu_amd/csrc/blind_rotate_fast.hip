@@ -72,12 +72,13 @@ constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS =
 // (NB = 1: one buffer and an extra barrier before each cross-wavefront store)
 constexpr uint32_t PS = 576, WS = 2 * PS, XBUF = 2 * WS;
 // the fast key buffer: [T_WORDS tables][4-wave kernel tables (blind_rotate_fast4.hip)][key rows]
-constexpr uint32_t T4W = 4776, TB_WORDS = T_WORDS + T4W;
+constexpr uint32_t T4W = 4904, TB_WORDS = T_WORDS + T4W;
 
 struct FastConst {
     int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x
     uint32_t Q2, Q4, h1, kacc;  // 2Q, 4Q, (Q>>1)+1, (Q>>1)+1+4Q
     int32_t ninv;               // N^-1 (centred Montgomery form)
+    uint32_t bm;                // floor(2^32 / Q) (blind_rotate_fast4.hip's Barrett update)
 };
 
 __device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
@@ -775,6 +776,7 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     K.h1 = (Q >> 1) + 1;
     K.kacc = K.h1 + 4 * Q;
     K.ninv = mont_centred(Q - (Q - 1) / FN, Q);  // N (Q-1)/N = -1 mod Q
+    K.bm = (uint32_t)((1ull << 32) / Q);
     const int32_t* tabs = (const int32_t*)bsk_fast;
     const int32_t* bsk = tabs + TB_WORDS;
     const int variant = fast_variant();

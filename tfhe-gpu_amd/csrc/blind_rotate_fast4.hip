@@ -36,11 +36,13 @@ constexpr int TPC = 256;
 //   pass p >= 1 block c (m = 4^p): [psi[m+c], psi[2m+2c], psi[2m+2c+1], 0]; pass 0 = block 0 of m = 1
 constexpr uint32_t P0F = 0, P1F = 4, P2F = 20, P3F = 84, P4F = 340, PF_END = 1364;
 constexpr uint32_t P0I = PF_END, P1I = P0I + P1F, P4I = P0I + P4F;
-constexpr uint32_t T4_MONO = 2 * PF_END, T4_WORDS = T4_MONO + 2 * FN;
+constexpr uint32_t T4_MONO = 2 * PF_END, T4_T1 = T4_MONO + 2 * FN, T4_WORDS = T4_T1 + 128;
 // LDS (words): pass 1-3 twiddles (fwd, inv), monomials, 4 local regions, 2 cross areas
 constexpr uint32_t L_TW = 0, L_TWI = P4F - P1F, L_MONO = 2 * L_TWI;  // passes 1-3 (fwd, inv)
 // then, for P polynomials per wavefront: 4 local regions of P x LP words, 2 cross areas of P x XP
-constexpr uint32_t LP = 304, XP = 1152, L_CT = L_MONO + 2 * FN;
+// T1[d + 64] = d psi[1] mod Q for digits d in [-64, 64): pass 0's first stage on a digit polynomial
+constexpr uint32_t L_T1 = L_MONO + 2 * FN;
+constexpr uint32_t LP = 304, XP = 1152, L_CT = L_T1 + 128;
 constexpr size_t lds_bytes(int P) { return (size_t)(L_CT + 4 * P * LP + 2 * P * XP) * 4; }
 
 struct Lay {
@@ -120,6 +122,7 @@ struct FastConst {  // same layout as blind_rotate_fast.hip's
     int32_t Q, nQ, qinv, rM;
     uint32_t Q2, Q4, h1, kacc;
     int32_t ninv;
+    uint32_t bm;  // floor(2^32 / Q)
 };
 __device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
     const int32_t m = (int32_t)((uint32_t)T * (uint32_t)K.qinv);
@@ -237,13 +240,24 @@ struct LaneCtx {
 template <int P, int p>
 constexpr int tail_wait() { return 4 * (P - 1 - p); }
 
-template <uint32_t XA, int P, int EXP = 0>
+// SMALL: the inputs are digits in [-64, 64); pass 0's first-stage products come from T1
+template <uint32_t XA, int P, int EXP = 0, bool SMALL = false>
 __device__ __forceinline__ void ntt_fwd(int32_t (&X)[P][4], const int32_t* lds, const LaneCtx& C, const FastConst& K) {
     if constexpr ((EXP & 8) != 0) return;
     constexpr int W = 4 * (P - 1);
     v4i w;
     // pass 0 (L1), exchange 1 -> 2
-    FOR_P(fwd4(X[p], C.w0f[0], C.w0f[1], C.w0f[2], K); store_rows<1, 2, p * LP>(X[p], C.m_loc, lds);)
+    if constexpr (SMALL) {
+        const int32_t* t1 = lds + L_T1 + 64;
+        int32_t v[P][2];
+        FOR_P(v[p][0] = t1[X[p][2]]; v[p][1] = t1[X[p][3]];)
+        FOR_P(const int32_t a0 = X[p][0], a1 = X[p][1];
+              X[p][0] = a0 + v[p][0]; X[p][2] = a0 - v[p][0]; X[p][1] = a1 + v[p][1]; X[p][3] = a1 - v[p][1];
+              bfly_ct(X[p][0], X[p][1], C.w0f[1], K); bfly_ct(X[p][2], X[p][3], C.w0f[2], K);
+              store_rows<1, 2, p * LP>(X[p], C.m_loc, lds);)
+    } else {
+        FOR_P(fwd4(X[p], C.w0f[0], C.w0f[1], C.w0f[2], K); store_rows<1, 2, p * LP>(X[p], C.m_loc, lds);)
+    }
     tw_load<L_TW>(w, C.t1, lds);
     FOR_P(gather_rows<1, 2, p * LP>(X[p], C.g12, lds);)
     // pass 1 (L2), exchange 2 -> 3
@@ -298,7 +312,8 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 
 // NCT ciphertexts per wavefront (the same slots of each): every key row loaded feeds NCT
 // ciphertexts, halving the vector-memory traffic per bootstrap at NCT = 2.
-template <int MINW, int NCT = 1, int EXP = 0>
+// OPT bit 0: T1 lookups in the digit transforms; bit 1: Barrett accumulator update
+template <int MINW, int NCT = 1, int EXP = 0, int OPT = 3>
 __global__ void __launch_bounds__(TPC, MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -307,7 +322,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     extern __shared__ __align__(16) int32_t lds[];
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < L_TWI; k += TPC) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
-    for (uint32_t k = tid; k < 2 * FN; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];
+    for (uint32_t k = tid; k < 2 * FN + 128; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     constexpr uint32_t LOCW = P * LP, XAW = P * XP;       // local region per wave, cross area (words)
     constexpr uint32_t XA0 = 4 * LOCW, XA1 = XA0 + XAW;  // cross areas, relative to L_CT
@@ -427,8 +442,8 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
                     X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, FLOGG * l, FLOGG);
                 }
             __builtin_amdgcn_sched_barrier(0);
-            if (l & 1) ntt_fwd<XA1, P, EXP>(X, lds, C, K);
-            else ntt_fwd<XA0, P, EXP>(X, lds, C, K);
+            if (l & 1) ntt_fwd<XA1, P, EXP, (OPT & 1) != 0>(X, lds, C, K);
+            else ntt_fwd<XA0, P, EXP, (OPT & 1) != 0>(X, lds, C, K);
             // next digit's rows (after digit 2: the next round's C rows; the last round re-fetches)
             const uint32_t noff = l < 2 ? round_off : (i + 1 < n ? i + 1 : i) * ROWB;
             const int nl = l < 2 ? (int)l + 1 : 3;
@@ -480,8 +495,16 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    uint32_t u = (uint32_t)(acc[q][p][r] + S[2 * q + p][r]) + K.kacc;
-                    u = csub32(csub32(csub32(u, K.Q4), K.Q2), (uint32_t)K.Q);
+                    uint32_t u = (uint32_t)(acc[q][p][r] + S[2 * q + p][r]) + K.kacc;  // in (0, 8Q)
+                    if constexpr ((OPT & 2) != 0) {
+                        // u - floor(u / Q) Q, off by at most one Q (u < 2^30): one mul_hi + one mad
+                        const uint32_t qt = __umulhi(u, K.bm);
+                        uint64_t t;
+                        asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(t) : "v"(qt), "s"(K.nQ), "v"((uint64_t)u) : "vcc");
+                        u = csub32((uint32_t)t, (uint32_t)K.Q);
+                    } else {
+                        u = csub32(csub32(csub32(u, K.Q4), K.Q2), (uint32_t)K.Q);
+                    }
                     acc[q][p][r] = (int32_t)(u - K.h1);
                 }
     }
@@ -523,6 +546,12 @@ __global__ void k_pack_tables4(uint32_t Q, const uint32_t* __restrict__ psi, con
         out[P0I + idx] = e == 3 ? 0 : mont(ipsi[k]);
     }
     if (idx < 2 * FN) out[T4_MONO + ((idx >> 6) | ((idx & 63) << 5))] = mont(mono[idx]);
+    if (idx < 128) {  // T1[d + 64] = d psi[1] mod Q, centred (plain: smul(d, mont(psi[1])) = d psi[1])
+        const int32_t d = (int32_t)idx - 64;
+        const uint32_t v = (uint32_t)((uint64_t)(uint32_t)(d < 0 ? -d : d) * psi[1] % Q);
+        const uint32_t m = d < 0 ? (v ? Q - v : 0) : v;
+        out[T4_T1 + idx] = m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+    }
 }
 
 }  // namespace f4
@@ -547,6 +576,9 @@ hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uin
     switch (variant) {
         case 59: launch(f4::k_blind_rotate_fast4<3, 1>, 1); break;
         case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;      // two ciphertexts per wavefront
+        case 76: launch(f4::k_blind_rotate_fast4<4, 1, 0, 0>, 1); break;  // without the OPT changes
+        case 77: launch(f4::k_blind_rotate_fast4<4, 1, 0, 1>, 1); break;
+        case 78: launch(f4::k_blind_rotate_fast4<4, 1, 0, 2>, 1); break;
         case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1>, 1); break;   // timing only: no barriers
         case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2>, 1); break;   // timing only: no key loads
         case 65: launch(f4::k_blind_rotate_fast4<4, 1, 8>, 1); break;   // timing only: no transforms
