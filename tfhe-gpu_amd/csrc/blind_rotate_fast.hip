@@ -72,7 +72,7 @@ constexpr uint32_t T_FWD = 0, T_INV = TW_WORDS, T_MONO = 2 * TW_WORDS, T_WORDS =
 // (NB = 1: one buffer and an extra barrier before each cross-wavefront store)
 constexpr uint32_t PS = 576, WS = 2 * PS, XBUF = 2 * WS;
 // the fast key buffer: [T_WORDS tables][4-wave kernel tables (blind_rotate_fast4.hip)][key rows]
-constexpr uint32_t T4W = 4904, TB_WORDS = T_WORDS + T4W;
+constexpr uint32_t T4W = 5416, TB_WORDS = T_WORDS + T4W;
 
 struct FastConst {
     int32_t Q, nQ, qinv, rM;  // rM = R mod Q (centred): smul(x, rM) reduces x

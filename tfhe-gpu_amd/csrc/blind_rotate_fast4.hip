@@ -36,14 +36,17 @@ constexpr int TPC = 256;
 //   pass p >= 1 block c (m = 4^p): [psi[m+c], psi[2m+2c], psi[2m+2c+1], 0]; pass 0 = block 0 of m = 1
 constexpr uint32_t P0F = 0, P1F = 4, P2F = 20, P3F = 84, P4F = 340, PF_END = 1364;
 constexpr uint32_t P0I = PF_END, P1I = P0I + P1F, P4I = P0I + P4F;
-constexpr uint32_t T4_MONO = 2 * PF_END, T4_T1 = T4_MONO + 2 * FN, T4_WORDS = T4_T1 + 128;
+constexpr uint32_t T4_MONO = 2 * PF_END, T4_T1 = T4_MONO + 2 * FN, T4_T23 = T4_T1 + 128, T4_T2131 = T4_T23 + 256,
+                   T4_WORDS = T4_T2131 + 256;
 // LDS (words): pass 1-3 twiddles (fwd, inv), monomials, 4 local regions, 2 cross areas
 constexpr uint32_t L_TW = 0, L_TWI = P4F - P1F, L_MONO = 2 * L_TWI;  // passes 1-3 (fwd, inv)
 // then, for P polynomials per wavefront: 4 local regions of P x LP words, 2 cross areas of P x XP
 // T1[d + 64] = d psi[1] mod Q for digits d in [-64, 64): pass 0's first stage on a digit polynomial
-constexpr uint32_t L_T1 = L_MONO + 2 * FN;
-constexpr uint32_t LP = 304, XP = 1152, L_CT = L_T1 + 128;
-constexpr size_t lds_bytes(int P) { return (size_t)(L_CT + 4 * P * LP + 2 * P * XP) * 4; }
+// T23[d] = (d psi[2], d psi[3]), T2131[d] = (d psi[2] psi[1], d psi[3] psi[1]): the rest of pass 0
+// P4F: pass-4 forward twiddles, lane order (one ds_read_b128 per lane, conflict-free)
+constexpr uint32_t L_T1 = L_MONO + 2 * FN, L_T23 = L_T1 + 128, L_T2131 = L_T23 + 256, L_P4F = L_T2131 + 256;
+constexpr uint32_t LP = 304, XP = 1152, L_CT = L_P4F + 4 * 256;
+constexpr size_t lds_bytes(int P, int XB = 2) { return (size_t)(L_CT + 4 * P * LP + XB * P * XP) * 4; }
 
 struct Lay {
     int reg[2];
@@ -214,7 +217,7 @@ struct LaneCtx {
     uint32_t g12, g23, g34, g45, g54, g43, g32, g21;  // gather bases (bytes; local ones include the region)
     uint32_t m_loc;                                   // this wavefront's local region (bytes, uniform)
     uint32_t m45, m54;                                // cross-store wave offsets (bytes, uniform)
-    uint32_t t1, t2, t3;                              // pass 1 / 2 / 3 twiddle block addresses (bytes)
+    uint32_t t1, t2, t3, t4;                          // pass 1 / 2 / 3 / 4 twiddle block addresses (bytes)
     int32_t w0f[3], w0i[3];                           // pass 0 (uniform)
     v4i w4f, w4i;                                     // pass 4 (per lane)
 };
@@ -240,14 +243,29 @@ struct LaneCtx {
 template <int P, int p>
 constexpr int tail_wait() { return 4 * (P - 1 - p); }
 
-// SMALL: the inputs are digits in [-64, 64); pass 0's first-stage products come from T1
-template <uint32_t XA, int P, int EXP = 0, bool SMALL = false>
+// SMALL (inputs are digits in [-64, 64)): 1 = pass 0's first-stage products from T1, 2 = all of
+// pass 0's products from T1, T23, T2131 (3 address computations + 8 additions per polynomial).
+// P4L: pass-4 twiddles from LDS (L_P4F) instead of registers.
+// PRE: one cross area only, so every wavefront must have finished reading its previous
+// contents before anyone stores (a plain barrier: those reads completed long ago)
+template <uint32_t XA, int P, int EXP = 0, int SMALL = 0, bool PRE = false, bool P4L = false>
 __device__ __forceinline__ void ntt_fwd(int32_t (&X)[P][4], const int32_t* lds, const LaneCtx& C, const FastConst& K) {
     if constexpr ((EXP & 8) != 0) return;
     constexpr int W = 4 * (P - 1);
     v4i w;
     // pass 0 (L1), exchange 1 -> 2
-    if constexpr (SMALL) {
+    if constexpr (SMALL == 2) {
+        const int32_t* t1 = lds + L_T1 + 64;
+        const int2* t23 = reinterpret_cast<const int2*>(lds + L_T23) + 64;
+        const int2* t2131 = reinterpret_cast<const int2*>(lds + L_T2131) + 64;
+        int32_t a[P];
+        int2 u23[P], u2131[P];
+        FOR_P(a[p] = t1[X[p][2]]; u23[p] = t23[X[p][1]]; u2131[p] = t2131[X[p][3]];)
+        FOR_P(const int32_t x0 = X[p][0], u = u23[p].x + u2131[p].x, v = u23[p].y - u2131[p].y;
+              const int32_t e0 = x0 + a[p], e2 = x0 - a[p];
+              X[p][0] = e0 + u; X[p][1] = e0 - u; X[p][2] = e2 + v; X[p][3] = e2 - v;
+              store_rows<1, 2, p * LP>(X[p], C.m_loc, lds);)
+    } else if constexpr (SMALL == 1) {
         const int32_t* t1 = lds + L_T1 + 64;
         int32_t v[P][2];
         FOR_P(v[p][0] = t1[X[p][2]]; v[p][1] = t1[X[p][3]];)
@@ -273,21 +291,29 @@ __device__ __forceinline__ void ntt_fwd(int32_t (&X)[P][4], const int32_t* lds, 
     // pass 3 (L4), cross exchange 4 -> 5
     FOR_P(if constexpr (p == 0) lds_wait<W>(X[0], w); else lds_wait<W>(X[p]);
           fwd4(X[p], w.x, w.y, w.z, K);
+          if constexpr (PRE && p == 0) __builtin_amdgcn_s_barrier();
           store_rows<4, 5, XA + p * XP>(X[p], C.m45, lds);)
     if constexpr (!(EXP & 1)) lds_drain_barrier();
+    if constexpr (P4L) tw_load<L_P4F>(w, C.t4, lds);
     FOR_P(gather_rows<4, 5, XA + p * XP>(X[p], C.g45, lds);)
     // pass 4 (L5)
-    FOR_P(lds_wait<tail_wait<P, p>()>(X[p]); fwd4(X[p], C.w4f.x, C.w4f.y, C.w4f.z, K);)
+    if constexpr (P4L) {
+        FOR_P(if constexpr (p == 0) lds_wait<tail_wait<P, 0>()>(X[0], w); else lds_wait<tail_wait<P, p>()>(X[p]);
+              fwd4(X[p], w.x, w.y, w.z, K);)
+    } else {
+        FOR_P(lds_wait<tail_wait<P, p>()>(X[p]); fwd4(X[p], C.w4f.x, C.w4f.y, C.w4f.z, K);)
+    }
 }
 
 // inverse (N^-1 folded into the keys), L5 -> L1
-template <uint32_t XA, int P, int EXP = 0>
+template <uint32_t XA, int P, int EXP = 0, bool PRE = false>
 __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, const LaneCtx& C, const FastConst& K) {
     if constexpr ((EXP & 8) != 0) return;
     constexpr int W = 4 * (P - 1);
     v4i w;
     // (b0 b1) (L5), cross exchange 5 -> 4
-    FOR_P(inv4<false>(X[p], C.w4i.x, C.w4i.y, C.w4i.z, K); store_rows<5, 4, XA + p * XP>(X[p], C.m54, lds);)
+    FOR_P(inv4<false>(X[p], C.w4i.x, C.w4i.y, C.w4i.z, K); if constexpr (PRE && p == 0) __builtin_amdgcn_s_barrier();
+          store_rows<5, 4, XA + p * XP>(X[p], C.m54, lds);)
     if constexpr (!(EXP & 1)) lds_drain_barrier();
     tw_load<L_TWI + 80>(w, C.t3, lds);
     FOR_P(gather_rows<5, 4, XA + p * XP>(X[p], C.g54, lds);)
@@ -312,8 +338,10 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 
 // NCT ciphertexts per wavefront (the same slots of each): every key row loaded feeds NCT
 // ciphertexts, halving the vector-memory traffic per bootstrap at NCT = 2.
-// OPT bit 0: T1 lookups in the digit transforms; bit 1: Barrett accumulator update
-template <int MINW, int NCT = 1, int EXP = 0, int OPT = 3>
+// OPT bit 0: T1 lookups in the digit transforms (bit 2: all of pass 0 from tables); bit 1: Barrett
+// accumulator update; bit 3: pass-4 forward twiddles from LDS
+// XB: cross-exchange areas (2: alternate, no barrier before the stores; 1: one area + a barrier)
+template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2>
 __global__ void __launch_bounds__(TPC, MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -322,10 +350,13 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     extern __shared__ __align__(16) int32_t lds[];
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = tid; k < L_TWI; k += TPC) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
-    for (uint32_t k = tid; k < 2 * FN + 128; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1
+    for (uint32_t k = tid; k < 2 * FN + 640; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1/T23/T2131
+    if constexpr ((OPT & 8) != 0)
+        for (uint32_t k = tid; k < 4 * 256; k += TPC) lds[L_P4F + k] = tabs[P4F + k];
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     constexpr uint32_t LOCW = P * LP, XAW = P * XP;       // local region per wave, cross area (words)
-    constexpr uint32_t XA0 = 4 * LOCW, XA1 = XA0 + XAW;  // cross areas, relative to L_CT
+    constexpr uint32_t XA0 = 4 * LOCW, XA1 = XB == 2 ? XA0 + XAW : XA0;  // cross areas, relative to L_CT
+    constexpr bool PRE = XB == 1;
 
     LaneCtx C;
     C.m_loc = (L_CT + w * LOCW) * 4;
@@ -335,9 +366,10 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     C.g45 = (L_CT + ld_lane<4, 5>(w, lane)) * 4, C.g54 = (L_CT + ld_lane<5, 4>(w, lane)) * 4;
     C.m45 = (L_CT + st_wave<4, 5>(w)) * 4, C.m54 = (L_CT + st_wave<5, 4>(w)) * 4;
     C.t1 = (elem<2>(w, lane, 0) >> 8) * 16, C.t2 = (elem<3>(w, lane, 0) >> 6) * 16;
-    C.t3 = (elem<4>(w, lane, 0) >> 4) * 16;
+    C.t3 = (elem<4>(w, lane, 0) >> 4) * 16, C.t4 = tid * 16;
     const v4i* tv = reinterpret_cast<const v4i*>(tabs);
-    C.w4f = tv[P4F / 4 + tid], C.w4i = tv[P4I / 4 + tid];
+    if constexpr ((OPT & 8) == 0) C.w4f = tv[P4F / 4 + tid];
+    C.w4i = tv[P4I / 4 + tid];
 #pragma unroll
     for (int k = 0; k < 3; ++k) C.w0f[k] = tabs[P0F + k], C.w0i[k] = tabs[P0I + k];
 
@@ -364,7 +396,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     for (int q = 0; q < NCT; ++q)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][1][r];
-    ntt_fwd<XA1, P, EXP>(Cp, lds, C, K);
+    ntt_fwd<XA1, P, EXP, 0, PRE, (OPT & 8) != 0>(Cp, lds, C, K);
 #pragma unroll
     for (int p = 0; p < P; ++p)
 #pragma unroll
@@ -442,8 +474,9 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
                     X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, FLOGG * l, FLOGG);
                 }
             __builtin_amdgcn_sched_barrier(0);
-            if (l & 1) ntt_fwd<XA1, P, EXP, (OPT & 1) != 0>(X, lds, C, K);
-            else ntt_fwd<XA0, P, EXP, (OPT & 1) != 0>(X, lds, C, K);
+            constexpr int SM = (OPT & 4) ? 2 : (OPT & 1) ? 1 : 0;
+            if (l & 1) ntt_fwd<XA1, P, EXP, SM, PRE, (OPT & 8) != 0>(X, lds, C, K);
+            else ntt_fwd<XA0, P, EXP, SM, PRE, (OPT & 8) != 0>(X, lds, C, K);
             // next digit's rows (after digit 2: the next round's C rows; the last round re-fetches)
             const uint32_t noff = l < 2 ? round_off : (i + 1 < n ? i + 1 : i) * ROWB;
             const int nl = l < 2 ? (int)l + 1 : 3;
@@ -488,7 +521,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
                 for (int r = 0; r < 4; ++r) Cp[p][r] = smul(Cp[p][r], K.rM, K);
         }
         __builtin_amdgcn_sched_barrier(0);
-        ntt_inv<XA1, P, EXP>(S, lds, C, K);
+        ntt_inv<XA1, P, EXP, PRE>(S, lds, C, K);
 #pragma unroll
         for (int q = 0; q < NCT; ++q)
 #pragma unroll
@@ -546,11 +579,17 @@ __global__ void k_pack_tables4(uint32_t Q, const uint32_t* __restrict__ psi, con
         out[P0I + idx] = e == 3 ? 0 : mont(ipsi[k]);
     }
     if (idx < 2 * FN) out[T4_MONO + ((idx >> 6) | ((idx & 63) << 5))] = mont(mono[idx]);
-    if (idx < 128) {  // T1[d + 64] = d psi[1] mod Q, centred (plain: smul(d, mont(psi[1])) = d psi[1])
+    if (idx < 128) {  // pass 0 of a digit polynomial: d w mod Q, centred (plain: smul(d, mont(w)) = d w)
         const int32_t d = (int32_t)idx - 64;
-        const uint32_t v = (uint32_t)((uint64_t)(uint32_t)(d < 0 ? -d : d) * psi[1] % Q);
-        const uint32_t m = d < 0 ? (v ? Q - v : 0) : v;
-        out[T4_T1 + idx] = m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+        auto dmul = [Q, d](uint64_t w) {
+            const uint32_t v = (uint32_t)((uint64_t)(uint32_t)(d < 0 ? -d : d) * (w % Q) % Q);
+            const uint32_t m = d < 0 ? (v ? Q - v : 0) : v;
+            return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
+        };
+        const uint64_t p21 = (uint64_t)psi[2] * psi[1] % Q, p31 = (uint64_t)psi[3] * psi[1] % Q;
+        out[T4_T1 + idx] = dmul(psi[1]);
+        out[T4_T23 + 2 * idx] = dmul(psi[2]), out[T4_T23 + 2 * idx + 1] = dmul(psi[3]);
+        out[T4_T2131 + 2 * idx] = dmul(p21), out[T4_T2131 + 2 * idx + 1] = dmul(p31);
     }
 }
 
@@ -567,25 +606,26 @@ hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, h
 hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
                                      const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s) {
     const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
-    auto launch = [&](auto kern, int nct) {
+    auto launch = [&](auto kern, int nct, int xb = 2) {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)f4::lds_bytes(2 * nct));
-        hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct - 1) / nct)), dim3(f4::TPC), f4::lds_bytes(2 * nct), s, Kc,
+                                  (int)f4::lds_bytes(2 * nct, xb));
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct - 1) / nct)), dim3(f4::TPC), f4::lds_bytes(2 * nct, xb), s, Kc,
                            n, loga, tabs4, bsk, a, acc, (uint32_t)B);
     };
     switch (variant) {
-        case 59: launch(f4::k_blind_rotate_fast4<3, 1>, 1); break;
+        case 59: launch(f4::k_blind_rotate_fast4<3, 1, 0, 3, 1>, 1, 1); break;
         case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;      // two ciphertexts per wavefront
-        case 76: launch(f4::k_blind_rotate_fast4<4, 1, 0, 0>, 1); break;  // without the OPT changes
-        case 77: launch(f4::k_blind_rotate_fast4<4, 1, 0, 1>, 1); break;
-        case 78: launch(f4::k_blind_rotate_fast4<4, 1, 0, 2>, 1); break;
-        case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1>, 1); break;   // timing only: no barriers
-        case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2>, 1); break;   // timing only: no key loads
-        case 65: launch(f4::k_blind_rotate_fast4<4, 1, 8>, 1); break;   // timing only: no transforms
+        case 81: launch(f4::k_blind_rotate_fast4<4, 1, 0, 3, 1>, 1, 1); break;   // pass-0 first stage only
+        case 83: launch(f4::k_blind_rotate_fast4<4, 1, 0, 11, 1>, 1, 1); break;  // + pass-4 twiddles in LDS
+        case 84: launch(f4::k_blind_rotate_fast4<4, 1, 0, 15, 1>, 1, 1); break;  // both
+        case 76: launch(f4::k_blind_rotate_fast4<4, 1, 0, 0, 1>, 1, 1); break;  // without the OPT changes
+        case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1, 3, 1>, 1, 1); break;  // timing only: no barriers
+        case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2, 3, 1>, 1, 1); break;  // timing only: no key loads
+        case 65: launch(f4::k_blind_rotate_fast4<4, 1, 8, 3, 1>, 1, 1); break;  // timing only: no transforms
         case 71: launch(f4::k_blind_rotate_fast4<2, 2, 1>, 2); break;   // timing only: no barriers
         case 72: launch(f4::k_blind_rotate_fast4<2, 2, 2>, 2); break;   // timing only: no key loads
         case 75: launch(f4::k_blind_rotate_fast4<2, 2, 8>, 2); break;   // timing only: no transforms
-        default: launch(f4::k_blind_rotate_fast4<4, 1>, 1); break;      // = 60: 4 waves/SIMD
+        default: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1>, 1, 1); break;  // = 60 (82)
     }
     return hipGetLastError();
 }

@@ -9,7 +9,7 @@ import sys
 Q = int(sys.argv[1]) if len(sys.argv) > 1 else 134215681
 Qh = Q // 2
 LIM = 2 ** 31
-RED = {0: "B", 1: None, 2: "B", 3: None, 4: "B"}   # inverse pass -> stage whose sums are reduced
+RED = {0: None, 1: "B", 2: None, 3: "B", 4: None}   # inverse pass (L5, L4, L3, L2, L1) -> reduced stage
 
 
 def smul_b(y):
@@ -17,9 +17,11 @@ def smul_b(y):
     return y * Qh / 2 ** 32 + LIM * Q / 2 ** 32
 
 
-def fwd(b_in):
+def fwd(b_in, small=False):
     b = list(b_in)
-    for p in range(5):
+    if small:  # pass 0 from the lookup tables: x0 + T1[x2] +- (T2[x1] + T21[x3]), tables reduced (<= Q/2)
+        b = [max(b_in) + 3 * (Qh + 1)] * 1024
+    for p in range(1 if small else 0, 5):
         for bit in (9 - 2 * p, 8 - 2 * p):
             m = 1 << bit
             nb = list(b)
@@ -51,7 +53,7 @@ def inv(b_in):
     return b
 
 
-F = max(fwd([64] * 1024))                 # digit transforms
+F = max(max(fwd([64] * 1024)), max(fwd([64] * 1024, small=True)))  # digit transforms (both pass-0 forms)
 C0 = smul_b(max(fwd([Qh + 1] * 1024)))    # C = N^-1 NTT(acc)
 rowsum = 6 * F * Qh + 2 * F * Qh          # 3 digits + C (kept <= F) over 2 polynomials
 assert rowsum < 2 ** 63
