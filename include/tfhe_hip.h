@@ -177,6 +177,12 @@ int tfhe_abi_version(void);
 /* host-only self test of the NTT tables and packing (no GPU needed); 0 = pass */
 tfhe_status tfhe_host_selftest(const tfhe_params* p);
 
+/* ---- extension (no reference counterpart): build of the specialised STD128-class blind
+ * rotation used by later calls, for A/B runs and tests; 0 restores the default.  Process-wide;
+ * initial value from TFHE_FAST_VARIANT.  Every build computes the same output. ---- */
+tfhe_status tfhe_set_kernel_variant(int variant);
+int tfhe_get_kernel_variant(void);
+
 #ifdef __cplusplus
 }
 #endif

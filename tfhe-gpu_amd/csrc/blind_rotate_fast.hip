@@ -41,6 +41,7 @@
 //  * Monomials: NTT(X^m - 1)[x] = psi^(e_x m) - 1 with e_x = 2 bitrev(x) + 1
 //    (checked at setup), so in L4 e = 256 bitrev3(r) + (2 bitrev7(t) + 1): one
 //    per-lane product per round plus a wave-uniform stride, and one 2N-entry table.
+#include <atomic>
 #include <cstdlib>
 
 #include "device_math.hpp"
@@ -723,11 +724,21 @@ namespace {
 // (two wavefronts per ciphertext), >= 59 k_blind_rotate_fast4 (blind_rotate_fast4.hip; 60 =
 // default).  The variant table is in DESIGN.md 3.1.
 constexpr int kDefaultVariant = 60;
+// builds the launchers know (blind_rotate_fast4.hip's list for >= 59); timing-only ones excluded
+bool known_variant(int v) {
+    static const int k[] = {34, 39, 40, 59, 60, 70, 76, 81, 83, 84, 85, 86, 87, 88};
+    for (int x : k)
+        if (x == v) return true;
+    return false;
+}
+std::atomic<int> g_variant{-1};
 int fast_variant() {
-    static const int v = [] {
+    int v = g_variant.load(std::memory_order_relaxed);
+    if (v < 0) {
         const char* e = std::getenv("TFHE_FAST_VARIANT");
-        return e && e[0] ? std::atoi(e) : kDefaultVariant;
-    }();
+        v = e && e[0] ? std::atoi(e) : kDefaultVariant;
+        g_variant.store(v, std::memory_order_relaxed);
+    }
     return v;
 }
 uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
@@ -741,6 +752,14 @@ int32_t mont_centred(uint64_t v, uint32_t Q) {
     return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
 }
 }  // namespace
+
+bool set_fast_variant(int v) {
+    if (v == 0) v = kDefaultVariant;
+    if (!known_variant(v)) return false;
+    g_variant.store(v, std::memory_order_relaxed);
+    return true;
+}
+int get_fast_variant() { return fast_variant(); }
 
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s) {

@@ -46,7 +46,7 @@ constexpr uint32_t L_TW = 0, L_TWI = P4F - P1F, L_MONO = 2 * L_TWI;  // passes 1
 // P4F: pass-4 forward twiddles, lane order (one ds_read_b128 per lane, conflict-free)
 constexpr uint32_t L_T1 = L_MONO + 2 * FN, L_T23 = L_T1 + 128, L_T2131 = L_T23 + 256, L_P4F = L_T2131 + 256;
 constexpr uint32_t LP = 304, XP = 1152, L_CT = L_P4F + 4 * 256;
-constexpr size_t lds_bytes(int P, int XB = 2) { return (size_t)(L_CT + 4 * P * LP + XB * P * XP) * 4; }
+constexpr size_t lds_bytes(int P, int XB = 2, int CTS = 1) { return (size_t)(L_CT + CTS * (4 * P * LP + XB * P * XP)) * 4; }
 
 struct Lay {
     int reg[2];
@@ -341,30 +341,37 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 // OPT bit 0: T1 lookups in the digit transforms (bit 2: all of pass 0 from tables); bit 1: Barrett
 // accumulator update; bit 3: pass-4 forward twiddles from LDS
 // XB: cross-exchange areas (2: alternate, no barrier before the stores; 1: one area + a barrier)
-template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2>
-__global__ void __launch_bounds__(TPC, MINW)
+// CTS (NCT = 1): ciphertexts per workgroup, in lockstep through the transforms' barriers, so
+// their wavefronts read each key row at about the same time (L1 reuse instead of L2 traffic).
+template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2, int CTS = 1>
+__global__ void __launch_bounds__(TPC * CTS, MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
                      uint32_t B) {
     constexpr int P = 2 * NCT;
     extern __shared__ __align__(16) int32_t lds[];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < L_TWI; k += TPC) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
-    for (uint32_t k = tid; k < 2 * FN + 640; k += TPC) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1/T23/T2131
+    static_assert(CTS == 1 || NCT == 1, "CTS > 1 needs NCT = 1");
+    const uint32_t cl = __builtin_amdgcn_readfirstlane(threadIdx.x / TPC);  // ciphertext in the workgroup
+    const uint32_t tid = threadIdx.x % TPC;
+    const uint32_t wg_ct = blockIdx.x * CTS * NCT + cl;                     // first ciphertext of this lane
+    for (uint32_t k = threadIdx.x; k < L_TWI; k += TPC * CTS) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
+    for (uint32_t k = threadIdx.x; k < 2 * FN + 640; k += TPC * CTS) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1/T23/T2131
     if constexpr ((OPT & 8) != 0)
-        for (uint32_t k = tid; k < 4 * 256; k += TPC) lds[L_P4F + k] = tabs[P4F + k];
+        for (uint32_t k = threadIdx.x; k < 4 * 256; k += TPC * CTS) lds[L_P4F + k] = tabs[P4F + k];
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     constexpr uint32_t LOCW = P * LP, XAW = P * XP;       // local region per wave, cross area (words)
     constexpr uint32_t XA0 = 4 * LOCW, XA1 = XB == 2 ? XA0 + XAW : XA0;  // cross areas, relative to L_CT
     constexpr bool PRE = XB == 1;
 
     LaneCtx C;
-    C.m_loc = (L_CT + w * LOCW) * 4;
+    constexpr uint32_t CTW = 4 * LOCW + XB * XAW;        // LDS words per ciphertext group
+    const uint32_t ctb = (L_CT + cl * CTW) * 4;         // bytes, uniform
+    C.m_loc = ctb + w * LOCW * 4;
     C.g12 = C.m_loc + ld_lane<1, 2>(w, lane) * 4, C.g23 = C.m_loc + ld_lane<2, 3>(w, lane) * 4;
     C.g34 = C.m_loc + ld_lane<3, 4>(w, lane) * 4, C.g43 = C.m_loc + ld_lane<4, 3>(w, lane) * 4;
     C.g32 = C.m_loc + ld_lane<3, 2>(w, lane) * 4, C.g21 = C.m_loc + ld_lane<2, 1>(w, lane) * 4;
-    C.g45 = (L_CT + ld_lane<4, 5>(w, lane)) * 4, C.g54 = (L_CT + ld_lane<5, 4>(w, lane)) * 4;
-    C.m45 = (L_CT + st_wave<4, 5>(w)) * 4, C.m54 = (L_CT + st_wave<5, 4>(w)) * 4;
+    C.g45 = ctb + ld_lane<4, 5>(w, lane) * 4, C.g54 = ctb + ld_lane<5, 4>(w, lane) * 4;
+    C.m45 = ctb + st_wave<4, 5>(w) * 4, C.m54 = ctb + st_wave<5, 4>(w) * 4;
     C.t1 = (elem<2>(w, lane, 0) >> 8) * 16, C.t2 = (elem<3>(w, lane, 0) >> 6) * 16;
     C.t3 = (elem<4>(w, lane, 0) >> 4) * 16, C.t4 = tid * 16;
     const v4i* tv = reinterpret_cast<const v4i*>(tabs);
@@ -377,7 +384,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     int32_t acc[NCT][2][4];  // L1, centred canonical
 #pragma unroll
     for (int q = 0; q < NCT; ++q) {
-        const uint32_t ct = blockIdx.x * NCT + q;
+        const uint32_t ct = wg_ct + q;
         const uint64_t* g = acc_io + (size_t)(ct < B ? ct : 0) * 2 * FN;
 #pragma unroll
         for (int p = 0; p < 2; ++p)
@@ -441,7 +448,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         uint32_t ai[NCT];  // a'_i = ((amod - a_i) mod amod) * (2N / amod)  (rgsw-acc-cggi.cpp:153)
 #pragma unroll
         for (int q = 0; q < NCT; ++q) {
-            const uint32_t ct = blockIdx.x * NCT + q;
+            const uint32_t ct = wg_ct + q;
             const uint32_t ar = ct < B ? (uint32_t)(a[(size_t)ct * n + i] & amask) : 0;
             ai[q] = __builtin_amdgcn_readfirstlane(((amask + 1 - ar) & amask) << ashift);
         }
@@ -543,7 +550,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     }
 #pragma unroll
     for (int q = 0; q < NCT; ++q) {
-        const uint32_t ct = blockIdx.x * NCT + q;
+        const uint32_t ct = wg_ct + q;
         if (ct >= B) continue;
         uint64_t* g = acc_io + (size_t)ct * 2 * FN;
         // acc0 transposed (X -> X^-1, poly.cpp:762-770): out[(N-k) mod N] = -acc0[k]
@@ -606,10 +613,10 @@ hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, h
 hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
                                      const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s) {
     const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
-    auto launch = [&](auto kern, int nct, int xb = 2) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)f4::lds_bytes(2 * nct, xb));
-        hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct - 1) / nct)), dim3(f4::TPC), f4::lds_bytes(2 * nct, xb), s, Kc,
+    auto launch = [&](auto kern, int nct, int xb = 2, int cts = 1) {
+        const size_t lb = f4::lds_bytes(2 * nct, xb, cts);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct * cts - 1) / (nct * cts))), dim3(f4::TPC * cts), lb, s, Kc,
                            n, loga, tabs4, bsk, a, acc, (uint32_t)B);
     };
     switch (variant) {
@@ -618,6 +625,10 @@ hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uin
         case 81: launch(f4::k_blind_rotate_fast4<4, 1, 0, 3, 1>, 1, 1); break;   // pass-0 first stage only
         case 83: launch(f4::k_blind_rotate_fast4<4, 1, 0, 11, 1>, 1, 1); break;  // + pass-4 twiddles in LDS
         case 84: launch(f4::k_blind_rotate_fast4<4, 1, 0, 15, 1>, 1, 1); break;  // both
+        case 85: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 2>, 1, 1, 2); break;  // 2 ciphertexts per workgroup
+        case 86: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 4>, 1, 1, 4); break;  // 4 ciphertexts per workgroup
+        case 87: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 2, 2>, 1, 2, 2); break;  // 2 per workgroup, 2 cross areas
+        case 88: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 2, 4>, 1, 2, 4); break;  // 4 per workgroup, 2 cross areas
         case 76: launch(f4::k_blind_rotate_fast4<4, 1, 0, 0, 1>, 1, 1); break;  // without the OPT changes
         case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1, 3, 1>, 1, 1); break;  // timing only: no barriers
         case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2, 3, 1>, 1, 1); break;  // timing only: no key loads

@@ -693,6 +693,12 @@ extern "C" {
 
 int tfhe_abi_version(void) { return TFHE_HIP_ABI_VERSION; }
 
+tfhe_status tfhe_set_kernel_variant(int variant) {
+    if (!set_fast_variant(variant)) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+    return TFHE_OK;
+}
+int tfhe_get_kernel_variant(void) { return get_fast_variant(); }
+
 const char* tfhe_last_error(void) { return g_last_error.c_str(); }
 
 const char* tfhe_status_string(tfhe_status s) {

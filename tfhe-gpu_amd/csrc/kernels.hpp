@@ -42,6 +42,9 @@ bool fast_path_supported(const BRParams& P, int word_bits);
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s);
 size_t bsk_fast_bytes(const BRParams& P);
+// build of the specialised kernel (see blind_rotate_fast.hip); 0 = default; false if unknown
+bool set_fast_variant(int v);
+int get_fast_variant();
 // 4-wavefront variant (blind_rotate_fast4.hip): its table block, packed behind the fast tables,
 // and its launch (K: the fast kernel's FastConst).
 size_t fast4_table_words();

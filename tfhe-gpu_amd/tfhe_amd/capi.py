@@ -55,6 +55,8 @@ P = C.POINTER(Params)
 
 _SIGS = {
     "tfhe_abi_version": ([], C.c_int),
+    "tfhe_set_kernel_variant": ([C.c_int], C.c_int),
+    "tfhe_get_kernel_variant": ([], C.c_int),
     "tfhe_last_error": ([], C.c_char_p),
     "tfhe_status_string": ([C.c_int], C.c_char_p),
     "tfhe_params_from_set": ([C.c_int, P], C.c_int),
