@@ -83,7 +83,7 @@ def b_alg_per_bootstrap(p):
     return bsk + ks + io, bsk
 
 
-def cpu_baseline(p, bsk, ksk, seconds):
+def cpu_baseline(p, bsk, ksk, seconds, gpu_sample=None):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
@@ -112,12 +112,20 @@ def cpu_baseline(p, bsk, ksk, seconds):
     orc.eval_bin_gate("NAND", c1[:B1], c2[:B1])
     dt1 = time.perf_counter() - t0
     orc.L.or_set_threads(threads)
+    # the same oracle checks the benchmarked GPU outputs (first ciphertexts of the last step)
+    parity = None
+    if gpu_sample is not None:
+        g1, g2, gout = gpu_sample
+        ref = orc.eval_bin_gate("NAND", g1, g2)
+        parity = {"ciphertexts": int(len(gout)), "bit_exact": bool(np.array_equal(ref, gout)),
+                  "vs": "oracle/tfhe_oracle.c on the same synthetic keys and inputs"}
     orc.close()
     return {"value": round(B / dt, 3), "unit": "bootstraps/s", "cores": threads, "kind": "port",
             "single_thread_value": round(B1 / dt1, 3),
             "sample": f"STD128 EvalBinGate(NAND) on {B} random ciphertext pairs, same synthetic keys; "
                       f"oracle/tfhe_oracle.c (exact u128 CPU restatement, OpenMP one ciphertext per thread); "
-                      f"{dt:.1f} s; single thread: {B1} pairs in {dt1:.1f} s"}
+                      f"{dt:.1f} s; single thread: {B1} pairs in {dt1:.1f} s",
+            "gpu_parity": parity}
 
 
 def p_oracle(pyoracle, p):
@@ -270,7 +278,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if bsk is None:
             bsk, ksk = synthetic_keys(p)
-        cpu = cpu_baseline(p, bsk, ksk, args.cpu_seconds)
+        K = min(B, 64)
+        sample = tuple(x[:K].cpu().numpy().astype(np.uint64) for x in (ct1, ct2, out))
+        cpu = cpu_baseline(p, bsk, ksk, args.cpu_seconds, sample)
+        if cpu["gpu_parity"] and not cpu["gpu_parity"]["bit_exact"]:
+            print("[bench] ERROR: GPU outputs differ from the oracle", file=sys.stderr)
 
     if rank == 0:
         line = {

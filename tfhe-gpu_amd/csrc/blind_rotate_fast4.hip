@@ -8,20 +8,22 @@
 //    the per-lane state halves (row sums 32 VGPRs, accumulator 8, C 8) and the kernel fits
 //    128 VGPRs.  A 1024-point transform is five radix-4 register passes over the index-bit
 //    pairs (b9 b8) (b7 b6) (b5 b4) (b3 b2) (b1 b0) with four LDS exchanges; only the last
-//    one crosses wavefronts (one barrier per transform, tools/lds_layouts4.py):
+//    one crosses wavefronts (tools/lds_layouts4.py models and checks all eight exchanges):
 //        L1 regs (b8 b9)  lanes (b2 b3 b4 b6 b7 b5)  waves (b0 b1)   coefficient order
 //        L2 regs (b6 b7)  lanes (b2 b3 b8 b9 b4 b5)  waves (b0 b1)
 //        L3 regs (b4 b5)  lanes (b2 b3 b6 b8 b9 b7)  waves (b0 b1)
 //        L4 regs (b2 b3)  lanes (b4 b5 b6 b8 b9 b7)  waves (b0 b1)
 //        L5 regs (b0 b1)  lanes (b2 .. b7)           waves (b8 b9)   MAC: lane t owns slots 4t..4t+3
 //    Every exchange stores lane-contiguous rows (ds_write_addtid_b32) and gathers with
-//    conflict-free ds_read_b32; the cross-wavefront exchanges alternate between two areas, so
-//    no barrier is needed before their stores.
+//    conflict-free ds_read_b32.  The cross-wavefront exchange uses one LDS area (XB = 1, the
+//    default: a barrier after its stores and a plain one before them) or alternates between
+//    two (XB = 2: no barrier before the stores, 18 KiB more LDS; measured no faster).
 //  * Key rows stream through a ring: while the MAC consumes group g of one digit, group g of
 //    the next digit (or of the next round's C rows) is loaded into the freed registers, so
 //    every row has a whole transform to arrive.
 //  * Twiddles of pass 4 are per-lane constants kept in registers, pass 0's are uniform
-//    (SGPRs), passes 1-3 come from LDS (ds_read_b128).
+//    (SGPRs), passes 1-3 come from LDS (ds_read_b128).  Pass 0 of a digit polynomial (7-bit
+//    inputs) reads all its products from three 128-entry LDS tables.
 //  * Inverse passes on L4 and L2 reduce their second-stage sums (tools/bounds_fast4.py).
 #include "device_math.hpp"
 #include "kernels.hpp"
