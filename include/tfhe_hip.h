@@ -98,7 +98,14 @@ typedef struct tfhe_info {
     uint64_t ksk_device_bytes; /* per device */
     uint64_t bootstraps;       /* blind rotations executed since setup */
     uint64_t key_image_bytes;  /* size of the exportable device key image */
+    int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
 } tfhe_info;
+
+/* tfhe_info.br_kernel */
+#define TFHE_BR_GENERIC 0      /* generic v2 (or v1) Shoup kernel, blind_rotate_generic.hip */
+#define TFHE_BR_FAST 1         /* specialised STD128 kernel, blind_rotate_fast4.hip */
+#define TFHE_BR_F64 2          /* exact-FP64 kernel, blind_rotate_f64.hip */
+#define TFHE_BR_F64_FOLD 3     /* exact-FP64 kernel, top digit's transforms eliminated */
 
 typedef struct tfhe_ctx tfhe_ctx;
 

@@ -23,11 +23,28 @@
 namespace tfhe {
 namespace {
 
-constexpr int F64_THREADS = 256;
 
 struct F64Const {
     double Q, Qinv;
     int64_t Qi;
+    double Ninv;  // N^-1 mod Q, centred (FOLD)
+    double wfac;  // 2^(gL) N^-1 mod Q, centred (WRAP)
+};
+
+// Top-digit elimination (FOLD), as in the specialised STD128 kernel (blind_rotate_fast4.hip):
+// with thr = 0 and a top digit that is always the exact remainder, c = sum_l 2^(gl) d_l, so
+//   sum_l D_l W_l = sum_{l<L-1} D_l (W_l - 2^-(g(L-1-l)) W_top) + C' (N 2^-(g(L-1)) W_top)
+// with C' = N^-1 NTT(acc) kept in registers (C' += S every round, S the NTT-domain increment;
+// the BSK carries N^-1).  One forward transform of both polynomials fewer per round.
+// WRAP: when the top digit is not always exact (STD128Q: Q = 2^50 - 2^14 + 1, g = 25, the
+// centred c in [2^49 - 2^24, Q/2) leaves a residual w = 1 after the last signed digit), the
+// reference's digits sum to c - 2^(gL) w, so the round uses C' - 2^(gL) N^-1 NTT(w) in place
+// of C'.  w is almost always 0 (about 2^-14 of rounds have a w != 0 coefficient); a
+// workgroup-uniform vote skips the correction otherwise.
+struct F64Fold {
+    uint64_t hc[8];  // l < L-1: 2^-(g(L-1-l)); l = L-1: N 2^-(g(L-1))  (mod Q)
+    uint32_t L;
+    uint32_t on;
 };
 
 __device__ __forceinline__ double fmodmul(double a, double b, const F64Const& K) {
@@ -41,72 +58,77 @@ __device__ __forceinline__ double fred(double x, const F64Const& K) {
     return __fma_rn(-__builtin_rint(__dmul_rn(x, K.Qinv)), K.Q, x);
 }
 
-// CT stages m and 2m fused (radix-4 units); RED: reduce the unit's outputs
-template <bool RED>
-__device__ __forceinline__ void f64_ntt_fwd(double* buf, uint32_t N, uint32_t logN, const double* psi,
-                                            const F64Const& K) {
-    uint32_t m = 1, loglen = logN - 1;
-    while (m < N) {
-        if (m * 2 < N) {
-            const uint32_t lh = loglen - 1, h = 1u << lh, units = N >> 2;
-            for (uint32_t u = threadIdx.x; u < 2 * units; u += blockDim.x) {
-                const uint32_t poly = u >= units, uu = u - poly * units;
-                const uint32_t i = uu >> lh, jj = uu & (h - 1);
-                double* a = buf + (size_t)poly * N + ((size_t)i << (loglen + 1)) + jj;
-                const double w = psi[m + i], w1 = psi[2 * m + 2 * i], w2 = psi[2 * m + 2 * i + 1];
-                double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
-                double v = fmodmul(a2, w, K);
-                a2 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
-                v = fmodmul(a3, w, K);
-                a3 = __dsub_rn(a1, v), a1 = __dadd_rn(a1, v);
-                v = fmodmul(a1, w1, K);
-                a1 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
-                v = fmodmul(a3, w2, K);
-                a3 = __dsub_rn(a2, v), a2 = __dadd_rn(a2, v);
-                if constexpr (RED) a0 = fred(a0, K), a1 = fred(a1, K), a2 = fred(a2, K), a3 = fred(a3, K);
-                a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
-            }
-            m <<= 2;
-            loglen -= 2;
-        } else {
-            const uint32_t half = N >> 1;
-            for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
-                const uint32_t poly = b >= half, bb = b - poly * half;
-                double* a = buf + (size_t)poly * N + 2 * bb;
-                const double v = fmodmul(a[1], psi[m + bb], K), u0 = a[0];
-                a[0] = RED ? fred(__dadd_rn(u0, v), K) : __dadd_rn(u0, v);
-                a[1] = RED ? fred(__dsub_rn(u0, v), K) : __dsub_rn(u0, v);
-            }
-            m <<= 1;
+constexpr uint32_t ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+
+// CT stages m and 2m fused (radix-4 units), both polynomials of buf[2][N]; TH threads, all
+// trip counts and strides compile-time; RED: reduce the unit's outputs
+template <uint32_t N, uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_ntt_fwd(double* buf, const double* psi, const F64Const& K) {
+    constexpr uint32_t logN = ilog2c(N), units = N >> 2;
+    static_assert((2 * units) % TH == 0 && N % TH == 0, "thread mapping");
+    const uint32_t t = threadIdx.x;
+#pragma unroll 1
+    for (uint32_t st = 0; st < logN / 2; ++st) {
+        const uint32_t m = 1u << (2 * st), loglen = logN - 1 - 2 * st, lh = loglen - 1, h = 1u << lh;
+#pragma unroll
+        for (uint32_t r = 0; r < 2 * units / TH; ++r) {
+            const uint32_t u = t + r * TH, poly = u >= units, uu = u - poly * units;
+            const uint32_t i = uu >> lh, jj = uu & (h - 1);
+            double* a = buf + poly * N + (i << (loglen + 1)) + jj;
+            const double w = psi[m + i], w1 = psi[2 * m + 2 * i], w2 = psi[2 * m + 2 * i + 1];
+            double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
+            double v = fmodmul(a2, w, K);
+            a2 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
+            v = fmodmul(a3, w, K);
+            a3 = __dsub_rn(a1, v), a1 = __dadd_rn(a1, v);
+            v = fmodmul(a1, w1, K);
+            a1 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
+            v = fmodmul(a3, w2, K);
+            a3 = __dsub_rn(a2, v), a2 = __dadd_rn(a2, v);
+            if constexpr (RED) a0 = fred(a0, K), a1 = fred(a1, K), a2 = fred(a2, K), a3 = fred(a3, K);
+            a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
+        }
+        __syncthreads();
+    }
+    if constexpr (logN & 1) {
+        constexpr uint32_t m = N >> 1, half = N >> 1;
+#pragma unroll
+        for (uint32_t r = 0; r < N / TH; ++r) {
+            const uint32_t b = t + r * TH, poly = b >= half, bb = b - poly * half;
+            double* a = buf + poly * N + 2 * bb;
+            const double v = fmodmul(a[1], psi[m + bb], K), u0 = a[0];
+            a[0] = RED ? fred(__dadd_rn(u0, v), K) : __dadd_rn(u0, v);
+            a[1] = RED ? fred(__dsub_rn(u0, v), K) : __dsub_rn(u0, v);
         }
         __syncthreads();
     }
 }
 
 // GS inverse without N^-1 (folded into the BSK); RED: reduce the doubling outputs
-template <bool RED>
-__device__ __forceinline__ void f64_ntt_inv(double* buf, uint32_t N, uint32_t logN, const double* ipsi,
-                                            const F64Const& K) {
-    uint32_t m = N >> 1, loglen = 0;
-    if (logN & 1) {
-        const uint32_t half = N >> 1;
-        for (uint32_t b = threadIdx.x; b < 2 * half; b += blockDim.x) {
-            const uint32_t poly = b >= half, bb = b - poly * half;
-            double* a = buf + (size_t)poly * N + 2 * bb;
+template <uint32_t N, uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_ntt_inv(double* buf, const double* ipsi, const F64Const& K) {
+    constexpr uint32_t logN = ilog2c(N), units = N >> 2, half = N >> 1;
+    constexpr uint32_t lg0 = logN & 1;
+    const uint32_t t = threadIdx.x;
+    if constexpr (logN & 1) {
+#pragma unroll
+        for (uint32_t r = 0; r < N / TH; ++r) {
+            const uint32_t b = t + r * TH, poly = b >= half, bb = b - poly * half;
+            double* a = buf + poly * N + 2 * bb;
             const double u0 = a[0], u1 = a[1];
             a[0] = RED ? fred(__dadd_rn(u0, u1), K) : __dadd_rn(u0, u1);
-            a[1] = fmodmul(__dsub_rn(u0, u1), ipsi[m + bb], K);
+            a[1] = fmodmul(__dsub_rn(u0, u1), ipsi[half + bb], K);
         }
         __syncthreads();
-        m >>= 1;
-        loglen = 1;
     }
-    while (m > 1) {
-        const uint32_t lh = loglen, h = 1u << lh, units = N >> 2;
-        for (uint32_t u = threadIdx.x; u < 2 * units; u += blockDim.x) {
-            const uint32_t poly = u >= units, uu = u - poly * units;
+#pragma unroll 1
+    for (uint32_t st = 0; st < logN / 2; ++st) {
+        const uint32_t lh = lg0 + 2 * st, h = 1u << lh, m = (N >> lg0) >> (1 + 2 * st);
+#pragma unroll
+        for (uint32_t r = 0; r < 2 * units / TH; ++r) {
+            const uint32_t u = t + r * TH, poly = u >= units, uu = u - poly * units;
             const uint32_t i = uu >> lh, jj = uu & (h - 1);
-            double* a = buf + (size_t)poly * N + ((size_t)i << (lh + 2)) + jj;
+            double* a = buf + poly * N + (i << (lh + 2)) + jj;
             const double w1 = ipsi[m + 2 * i], w2 = ipsi[m + 2 * i + 1], w = ipsi[(m >> 1) + i];
             const double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
             const double s0 = __dadd_rn(a0, a1), d0 = fmodmul(__dsub_rn(a0, a1), w1, K);
@@ -117,8 +139,6 @@ __device__ __forceinline__ void f64_ntt_inv(double* buf, uint32_t N, uint32_t lo
             a[3 * h] = fmodmul(__dsub_rn(d0, d1), w, K);
         }
         __syncthreads();
-        m >>= 2;
-        loglen += 2;
     }
 }
 
@@ -130,12 +150,16 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 }
 
 // table block (doubles): psi[N] ipsi[N] mono[2N], then the BSK [n][2][dG2][2][N]
-template <int CN, bool RED>
-__global__ void __launch_bounds__(F64_THREADS, 2)
+// TH threads own CN slots each (t + TH k): N = 1024 runs 256 x 4, N = 2048 runs 512 x 4, so a
+// thread's state (acc, sums, C') fits 128 VGPRs and a CU holds 4 waves per SIMD (two 64 KiB
+// workgroups).
+template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false>
+__global__ void __launch_bounds__(TH, 4)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
     extern __shared__ __align__(16) double lds_d[];
-    constexpr uint32_t N = F64_THREADS * CN;
+    constexpr uint32_t N = TH * CN;
+    constexpr int F64_THREADS = TH;
     double* psi = lds_d;
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
@@ -160,6 +184,26 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
         }
     __syncthreads();
+    double Cn[2][CN];  // FOLD: N^-1 NTT(acc), |Cn| <~ Q/2
+    if constexpr (FOLD) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k)
+                buf[p * N + t + F64_THREADS * k] =
+                    (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
+        __syncthreads();
+        f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) Cn[p][k] = fmodmul(buf[p * N + t + F64_THREADS * k], K.Ninv, K);
+        __syncthreads();
+    }
+    const uint32_t Ld = FOLD ? P.digits - 1 : P.digits;  // digits that are transformed
+    int64_t KdL = 0;  // WRAP: residual after all digits = (c + KdL) >> (L g)
+    for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
+    const uint32_t shiftL = P.digits * logG;
 
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
@@ -172,7 +216,17 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0.0;
         const double* ek = bsk + (size_t)i * round_words;
-        for (uint32_t l = 0; l < P.digits; ++l) {
+        int wrap = 0;
+        if constexpr (WRAP) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
+                    wrap |= ((c + KdL) >> shiftL) != 0;
+                }
+        }
+        for (uint32_t l = 0; l < Ld; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
             for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
@@ -185,8 +239,9 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     const int32_t r = (int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
                     buf[p * N + t + F64_THREADS * k] = (double)r;
                 }
-            __syncthreads();
-            f64_ntt_fwd<RED>(buf, N, P.logN, psi, K);
+            if (WRAP && l == 0) wrap = __syncthreads_or(wrap);
+            else __syncthreads();
+            f64_ntt_fwd<N, TH, RED>(buf, psi, K);
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
                 const uint32_t x = t + F64_THREADS * k;
@@ -202,16 +257,76 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             }
             __syncthreads();
         }
+        if constexpr (FOLD) {  // the top digit's rows carry N 2^-(g(L-1)) W_top: multiply C'
+            const uint32_t l = Ld;
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const uint32_t x = t + F64_THREADS * k;
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
+                        const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
+                        A[kk][j][k] = __dadd_rn(A[kk][j][k],
+                                                __dadd_rn(fmodmul(Cn[0][k], ek[o0], K), fmodmul(Cn[1][k], ek[o1], K)));
+                    }
+            }
+        }
+        if constexpr (WRAP) {
+            // Rare path (workgroup-uniform vote): subtract 2^(gL) N^-1 NTT(w) times the C rows.
+            // w is sparse, so NTT(w)[x] = sum_j w_j psi^(e_x j) is evaluated directly from the
+            // monomial table (psi^k = mono[k] + 1) by a broadcast scan over w in LDS.
+            if (wrap) {
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int k = 0; k < CN; ++k) {
+                        const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
+                        buf[p * N + t + F64_THREADS * k] = (double)((c + KdL) >> shiftL);
+                    }
+                __syncthreads();
+                const uint32_t l = Ld;
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const uint32_t x = t + F64_THREADS * k, e = eidx[x];
+                    double n0 = 0.0, n1 = 0.0;
+#pragma unroll 1
+                    for (uint32_t jx = 0; jx < N; ++jx) {
+                        const double w0 = buf[jx], w1 = buf[N + jx];
+                        if (w0 != 0.0 || w1 != 0.0) {
+                            const double z = __dadd_rn(mono[(e * jx) & (twoN - 1)], 1.0);
+                            n0 = fred(__fma_rn(w0, z, n0), K);
+                            n1 = fred(__fma_rn(w1, z, n1), K);
+                        }
+                    }
+                    n0 = fmodmul(n0, K.wfac, K);
+                    n1 = fmodmul(n1, K.wfac, K);
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
+                            const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
+                            A[kk][j][k] = __dsub_rn(A[kk][j][k], __dadd_rn(fmodmul(n0, ek[o0], K), fmodmul(n1, ek[o1], K)));
+                        }
+                }
+                __syncthreads();  // every scan is done before the increment overwrites buf
+            }
+        }
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
             const uint32_t x = t + F64_THREADS * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
             const double mp = mono[ip], mn = mono[in];
-            buf[x] = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
-            buf[N + x] = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
+            const double s0 = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
+            const double s1 = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
+            buf[x] = s0;
+            buf[N + x] = s1;
+            if constexpr (FOLD) Cn[0][k] = fred(__dadd_rn(Cn[0][k], s0), K), Cn[1][k] = fred(__dadd_rn(Cn[1][k], s1), K);
         }
         __syncthreads();
-        f64_ntt_inv<RED>(buf, N, P.logN, ipsi, K);
+        f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -237,14 +352,69 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
 }
 
 // canonical u64 tables / BSK (generic arena) -> centred doubles
-__global__ void k_pack_f64(uint64_t Q, uint32_t N, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ ipsi,
-                           const uint64_t* __restrict__ mono, const uint64_t* __restrict__ bsk, size_t words,
-                           double* __restrict__ out) {
+// a * b mod Q for Q < 2^50 in 12-bit steps (one-time packing only)
+__device__ uint64_t mulmod_slow(uint64_t a, uint64_t b, uint64_t Q) {
+    uint64_t r = 0;
+    for (int s = 48; s >= 0; s -= 12) r = ((r << 12) % Q + a * ((b >> s) & 0xfff)) % Q;
+    return r;
+}
+
+// canonical u64 tables / BSK (generic arena) -> centred doubles; F.on: fold the top digit's
+// rows into the others (row = 2l + p of [n][2][dG2][2][N])
+__global__ void k_pack_f64(uint64_t Q, uint32_t N, uint32_t dG2, F64Fold F, const uint64_t* __restrict__ psi,
+                           const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ mono,
+                           const uint64_t* __restrict__ bsk, size_t words, double* __restrict__ out) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     auto cen = [Q](uint64_t v) { return v > Q / 2 ? (double)(int64_t)(v - Q) : (double)v; };
     if (idx < N) out[idx] = cen(psi[idx]), out[N + idx] = cen(ipsi[idx]);
     if (idx < 2 * (size_t)N) out[2 * N + idx] = cen(mono[idx]);
-    if (idx < words) out[4 * (size_t)N + idx] = cen(bsk[idx]);
+    if (idx < words) {
+        uint64_t v = bsk[idx] % Q;
+        if (F.on) {
+            const uint32_t row = (uint32_t)((idx / (2 * (size_t)N)) % dG2), l = row >> 1, p = row & 1;
+            const uint32_t top = 2 * (F.L - 1) + p;
+            const uint64_t wt = bsk[idx + ((size_t)top - row) * 2 * N] % Q;
+            v = l + 1 < F.L ? (v + Q - mulmod_slow(wt, F.hc[l], Q)) % Q : mulmod_slow(v, F.hc[l], Q);
+        }
+        out[4 * (size_t)N + idx] = cen(v);
+    }
+}
+
+uint64_t pow_mod(uint64_t b, uint64_t e, uint64_t Q) {
+    unsigned __int128 r = 1, x = b % Q;
+    for (; e; e >>= 1, x = x * x % Q)
+        if (e & 1) r = r * x % Q;
+    return (uint64_t)r;
+}
+
+// The top digit is the exact remainder (c = sum_l 2^(gl) d_l) for every centred c: the digit
+// recursion d -> (d + 2^(g-1)) >> g is monotone, so checking both extremes suffices.
+bool fold_possible(const BRParams& P) { return P.thr == 0 && P.digits >= 2 && P.digits <= 8; }
+
+bool fold_exact(const BRParams& P) {
+    if (!fold_possible(P)) return false;
+    const int64_t Qs = (int64_t)P.Q, half = (int64_t)(P.Q >> 1);
+    const uint32_t sh = 64 - P.logG;
+    for (int64_t c : {half - 1, half - Qs}) {
+        int64_t d = c;
+        for (uint32_t l = 0; l < P.digits; ++l) {
+            const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+            d = (d - r) >> P.logG;
+        }
+        if (d != 0) return false;
+    }
+    return true;
+}
+
+F64Fold make_fold(const BRParams& P, bool on) {
+    F64Fold F{};
+    F.on = on;
+    F.L = P.digits;
+    if (!F.on) return F;
+    const uint64_t inv2 = (P.Q + 1) / 2, L = P.digits;
+    for (uint32_t l = 0; l + 1 < L; ++l) F.hc[l] = pow_mod(inv2, (uint64_t)P.logG * (L - 1 - l), P.Q);
+    F.hc[L - 1] = (uint64_t)((unsigned __int128)P.N * pow_mod(inv2, (uint64_t)P.logG * (L - 1), P.Q) % P.Q);
+    return F;
 }
 
 }  // namespace
@@ -256,30 +426,55 @@ bool f64_path_supported(const BRParams& P, int word_bits) {
 
 size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
 
-hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s) {
+// TFHE_F64_FOLD: unset/1 = fold when the top digit is always exact (STD192 classes); 0 = never;
+// 2 = also with the WRAP correction (STD128Q: correct, but measured slower, 10.2K vs 11.8K
+// bootstraps/s on C5a, so not the default)
+bool f64_fold_enabled(const BRParams& P) {
+    const char* e = std::getenv("TFHE_F64_FOLD");
+    const int mode = e && e[0] ? e[0] - '0' : 1;
+    return mode == 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
+}
+
+hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
+                               hipStream_t s) {
+    if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const size_t words = (size_t)P.n * 4 * P.dG2 * P.N;
-    hipLaunchKernelGGL(k_pack_f64, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, P.N,
-                       (const uint64_t*)T.psi, (const uint64_t*)T.ipsi, (const uint64_t*)T.mono, (const uint64_t*)bsk,
+    hipLaunchKernelGGL(k_pack_f64, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, P.N, P.dG2,
+                       make_fold(P, fold), (const uint64_t*)T.psi, (const uint64_t*)T.ipsi, (const uint64_t*)T.mono, (const uint64_t*)bsk,
                        words, (double*)out);
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, const uint64_t* a,
-                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s) {
+hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold,
+                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
     F64Const K;
     K.Q = (double)P.Q;
     K.Qinv = 1.0 / K.Q;
     K.Qi = (int64_t)P.Q;
+    const uint64_t ninv = P.Q - (P.Q - 1) / P.N;  // N (Q-1)/N = -1 mod Q
+    K.Ninv = -(double)((P.Q - 1) / P.N);
+    const uint64_t wf = (uint64_t)((unsigned __int128)pow_mod(2, (uint64_t)P.logG * P.digits, P.Q) * ninv % P.Q);
+    K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
+    if (fold && !fold_possible(P)) return hipErrorInvalidValue;
+    const bool wrap = fold && !fold_exact(P);
     const size_t lds = (size_t)4 * P.N * sizeof(double);  // psi, ipsi, two polynomials
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(F64_THREADS), lds, s, P, K, (const double*)keys, T.eidx, a,
+        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
                            amod, acc);
     };
     const bool red = P.Q >= (1ull << 40);
-    if (P.N == 1024) red ? go(k_blind_rotate_f64<4, true>) : go(k_blind_rotate_f64<4, false>);
-    else red ? go(k_blind_rotate_f64<8, true>) : go(k_blind_rotate_f64<8, false>);
+    if (wrap) {
+        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, true, true>) : go(k_blind_rotate_f64<256, 4, false, true, true>);
+        else red ? go(k_blind_rotate_f64<512, 4, true, true, true>) : go(k_blind_rotate_f64<512, 4, false, true, true>);
+    } else if (fold) {
+        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, true>) : go(k_blind_rotate_f64<256, 4, false, true>);
+        else red ? go(k_blind_rotate_f64<512, 4, true, true>) : go(k_blind_rotate_f64<512, 4, false, true>);
+    } else {
+        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, false>) : go(k_blind_rotate_f64<256, 4, false, false>);
+        else red ? go(k_blind_rotate_f64<512, 4, true, false>) : go(k_blind_rotate_f64<512, 4, false, false>);
+    }
     return hipGetLastError();
 }
 

@@ -118,6 +118,8 @@ struct Device {
     Scratch sc2;
     void* pin[2] = {};               // pinned staging blocks for the host-array API
     hipEvent_t pin_ev[2] = {};       // last DMA that used each block
+    hipStream_t pipe[2] = {};        // chunked bootstrap pipeline (dev_bootstrap)
+    hipEvent_t pipe_ev[3] = {};      // [0] inputs ready, [1..2] each pipe stream done
 };
 
 constexpr size_t kStageBytes = (size_t)8 << 20;
@@ -130,6 +132,7 @@ struct tfhe_ctx {
     int ksk_bits = 64;
     bool use_fast = false;
     bool use_f64 = false;
+    bool f64_fold = false;  // exact-FP64 kernel with the top digit's transforms eliminated
     BRParams br{};
     KSParams ks{};
     ArenaLayout layout{};
@@ -167,6 +170,7 @@ tfhe_status init_derived(tfhe_ctx* c) {
     const char* force = std::getenv("TFHE_FORCE_GENERIC");
     c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     c->use_f64 = f64_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
+    c->f64_fold = c->use_f64 && f64_fold_enabled(c->br);
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
         return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
     if (p.baseKS > 256) return fail(TFHE_ERR_UNSUPPORTED, "baseKS > 256 not supported");
@@ -275,7 +279,7 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
     }
     if (c->use_f64) {
         HCHECK(hipMalloc(&d.keys_f64, bsk_f64_bytes(c->br)));
-        HCHECK(launch_pack_bsk_f64(c->br, d.tables, d.arena + c->layout.bsk, d.keys_f64, d.stream));
+        HCHECK(launch_pack_bsk_f64(c->br, d.tables, d.arena + c->layout.bsk, c->f64_fold, d.keys_f64, d.stream));
         HCHECK(hipStreamSynchronize(d.stream));
     }
     return TFHE_OK;
@@ -289,6 +293,10 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     if (d.stream2) hipStreamSynchronize(d.stream2);
+    for (hipStream_t ps : d.pipe)
+        if (ps) hipStreamSynchronize(ps), hipStreamDestroy(ps);
+    for (hipEvent_t e : d.pipe_ev)
+        if (e) hipEventDestroy(e);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
         hipFree(sc->a);
@@ -304,6 +312,12 @@ void free_device(Device& d) {
     if (d.stream2) hipStreamDestroy(d.stream2);
     d = Device{};
     d.id = -1;
+}
+
+tfhe_status create_streams(Device& d) {
+    HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    return TFHE_OK;
 }
 
 tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
@@ -344,7 +358,7 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     if (c->use_fast && (amod & (amod - 1)) == 0) {
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
     } else if (c->use_f64) {
-        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, a, amod, acc, B, d.stream));
+        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
                                            amod, acc, B, d.stream));
@@ -360,9 +374,53 @@ tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, 
     return TFHE_OK;
 }
 
+// Chunks of the bootstrap pipeline: TFHE_PIPELINE=K splits a batch of B >= 2048 into K
+// contiguous chunks on two alternating streams, so chunk i's extraction + key switch runs
+// beside chunk i+1's blind rotation (default 1: one launch per stage).
+int pipeline_chunks(size_t B) {
+    static const int k = [] {
+        const char* e = std::getenv("TFHE_PIPELINE");
+        return e ? std::max(1, std::min(16, std::atoi(e))) : 1;
+    }();
+    return B >= 2048 ? k : 1;
+}
+
+tfhe_status dev_bootstrap_one(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
+                              size_t B);
+
 // BootstrapFunc / BootstrapGate on device: ct[B][n+1] mod tv.ctmod -> out mod fmod
 tfhe_status dev_bootstrap(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
                           size_t B) {
+    const int K = pipeline_chunks(B);
+    if (K == 1) return dev_bootstrap_one(c, d, tv, b_add, ct, out, B);
+    for (int j = 0; j < 2; ++j)
+        if (!d.pipe[j]) HCHECK(hipStreamCreateWithFlags(&d.pipe[j], hipStreamNonBlocking));
+    for (hipEvent_t& e : d.pipe_ev)
+        if (!e) HCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HCHECK(hipEventRecord(d.pipe_ev[0], d.stream));
+    for (int j = 0; j < 2; ++j) HCHECK(hipStreamWaitEvent(d.pipe[j], d.pipe_ev[0], 0));
+    const size_t N = c->p.N, n = c->p.n, per = (B + K - 1) / K;
+    for (int i = 0; i < K; ++i) {
+        const size_t off = (size_t)i * per, len = std::min(per, B - std::min(B, off));
+        if (len == 0) break;
+        Device dl = d;  // same keys and scratch, a slice of it, the chunk's stream
+        dl.stream = d.pipe[i & 1];
+        dl.sc.acc += off * 2 * N;
+        dl.sc.a += off * n;
+        dl.sc.ext += off * (N + 1);
+        TvParams tc = tv;
+        if (tc.lut) tc.lut += off * tc.lut_stride;  // per-ciphertext LUTs
+        SCHECK(dev_bootstrap_one(c, dl, tc, b_add, ct + off * (n + 1), out + off * (n + 1), len));
+    }
+    for (int j = 0; j < 2; ++j) {
+        HCHECK(hipEventRecord(d.pipe_ev[1 + j], d.pipe[j]));
+        HCHECK(hipStreamWaitEvent(d.stream, d.pipe_ev[1 + j], 0));
+    }
+    return TFHE_OK;
+}
+
+tfhe_status dev_bootstrap_one(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
+                              size_t B) {
     tv.N = c->p.N;
     tv.n = c->p.n;
     tv.Q = c->p.Q;
@@ -748,9 +806,7 @@ tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* b
     for (size_t g = 0; g < c->devs.size(); ++g) {
         Device& d = c->devs[g];
         HCHECK(hipSetDevice(d.id));
-        HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
-        HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+        SCHECK(create_streams(d));
         HCHECK(hipMalloc(&d.arena, bytes));
         if (g == 0) {
             HCHECK(hipMemcpy(d.arena, img.data(), bytes, hipMemcpyHostToDevice));
@@ -785,8 +841,7 @@ tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, cons
     Device& d = c->devs[0];
     d.id = device;
     HCHECK(hipSetDevice(device));
-    HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    SCHECK(create_streams(d));
     HCHECK(hipMalloc(&d.arena, bytes));
     HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
     SCHECK(finish_device(c.get(), d));
@@ -862,8 +917,7 @@ tfhe_status tfhe_setup_from_key_file(tfhe_ctx** out, const tfhe_params* p, const
     Device& d = c->devs[0];
     d.id = device;
     HCHECK(hipSetDevice(device));
-    HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    SCHECK(create_streams(d));
     HCHECK(hipMalloc(&d.arena, img.size()));
     HCHECK(hipMemcpy(d.arena, img.data(), img.size(), hipMemcpyHostToDevice));
     SCHECK(finish_device(c.get(), d));
@@ -898,6 +952,7 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
     out->ksk_device_bytes = c->layout.total - c->layout.ksk;
     out->bootstraps = c->bootstraps.load();
     out->key_image_bytes = c->layout.total;
+    out->br_kernel = c->use_fast ? TFHE_BR_FAST : c->use_f64 ? (c->f64_fold ? TFHE_BR_F64_FOLD : TFHE_BR_F64) : TFHE_BR_GENERIC;
     return TFHE_OK;
 }
 

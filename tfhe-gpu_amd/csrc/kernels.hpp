@@ -56,8 +56,12 @@ hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uin
 // doubles derived on device from the generic (u64) arena.
 bool f64_path_supported(const BRParams& P, int word_bits);
 size_t bsk_f64_bytes(const BRParams& P);
-hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
-hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, const uint64_t* a,
+// fold: eliminate the top digit's transforms (keys packed accordingly); only when
+// f64_fold_enabled(P) (thr = 0, top digit always exact; TFHE_F64_FOLD=0 turns it off).
+bool f64_fold_enabled(const BRParams& P);
+hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
+                               hipStream_t s);
+hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold, const uint64_t* a,
                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
 
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).

@@ -43,7 +43,8 @@ class Params(C.Structure):
 
 class Info(C.Structure):
     _fields_ = [("num_devices", C.c_int), ("word_bits", C.c_int), ("bsk_device_bytes", C.c_uint64),
-                ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64)]
+                ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64),
+                ("br_kernel", C.c_int)]
 
 
 u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
