@@ -142,6 +142,193 @@ __device__ __forceinline__ void f64_ntt_inv(double* buf, const double* ipsi, con
     }
 }
 
+// ---- N = 2048: radix-8 register passes over a swizzled LDS buffer -------------------------
+// One thread owns 8 elements of ONE polynomial per pass (threads 0..TH/2-1 polynomial 0), so a
+// transform is four passes -- stages (0-2) (3-5) (6-8) radix-8 and (9-10) two radix-4 units --
+// with four barriers instead of six, and a third fewer LDS round trips.  The buffer is stored
+// at swz(x): bits 0-4 of x XOR f(bits 5-7), which makes every pass's 64-bit LDS accesses, and
+// the slot-per-lane accesses of the rest of the kernel, conflict-free
+// (tools/lds_layouts_f64.py checks every access pattern and the index algebra).
+__device__ __forceinline__ uint32_t swz(uint32_t x) {
+    const uint32_t c = (x >> 5) & 7;
+    return x ^ (c << 2) ^ (c & 3);
+}
+template <uint32_t N>
+__device__ __forceinline__ uint32_t bidx(uint32_t x) {
+    if constexpr (N == 2048) return swz(x);
+    else return x;
+}
+
+__device__ __forceinline__ void ct_bf(double& a, double& b, double w, const F64Const& K) {
+    const double v = fmodmul(b, w, K);
+    b = __dsub_rn(a, v), a = __dadd_rn(a, v);
+}
+__device__ __forceinline__ void gs_bf(double& a, double& b, double w, const F64Const& K) {
+    const double d = __dsub_rn(a, b);
+    a = __dadd_rn(a, b), b = fmodmul(d, w, K);
+}
+
+// Element addresses of a pass: ad[k] = swz(x_k) from one swizzled base and one XOR per
+// element (x_k's varying bits never mix with the swizzle's inputs in an add):
+//   pass A  x = tau + 256k:          swz(tau) + 256k
+//   pass B  x = 256b + o + 32k:      ((256b + o) ^ f(k)) + 32k,  f(c) = (c << 2) ^ (c & 3)
+//   pass C  x = 32b + o + 4k, o < 4: swz(32b + o) ^ 4k
+//   unit    x = 4u + k, k < 4:       swz(4u) ^ k
+__device__ __forceinline__ uint32_t swzf(uint32_t c) { return (c << 2) ^ (c & 3); }
+
+// forward CT stages s0, s0+1, s0+2 (m0 = 2^s0) on the 8 elements at ad[]; g = block
+template <bool RED>
+__device__ __forceinline__ void f64_r8_fwd(double* p, const uint32_t (&ad)[8], uint32_t m0, uint32_t g,
+                                           const double* psi, const F64Const& K) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+    const double w0 = psi[m0 + g];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ct_bf(v[k], v[k + 4], w0, K);
+    const double2 w1 = *(const double2*)(psi + 2 * m0 + 2 * g);
+    ct_bf(v[0], v[2], w1.x, K), ct_bf(v[1], v[3], w1.x, K);
+    ct_bf(v[4], v[6], w1.y, K), ct_bf(v[5], v[7], w1.y, K);
+    const double2 w2 = *(const double2*)(psi + 4 * m0 + 4 * g);
+    const double2 w3 = *(const double2*)(psi + 4 * m0 + 4 * g + 2);
+    ct_bf(v[0], v[1], w2.x, K), ct_bf(v[2], v[3], w2.y, K);
+    ct_bf(v[4], v[5], w3.x, K), ct_bf(v[6], v[7], w3.y, K);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
+}
+
+// inverse GS stages h0, 2h0, 4h0 on the 8 elements at ad[]; g = block (8 h0 elements), m = N/(2h0)
+template <bool RED>
+__device__ __forceinline__ void f64_r8_inv(double* p, const uint32_t (&ad)[8], uint32_t m, uint32_t g,
+                                           const double* ipsi, const F64Const& K) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+    const double2 w0 = *(const double2*)(ipsi + m + 4 * g);
+    const double2 w1 = *(const double2*)(ipsi + m + 4 * g + 2);
+    gs_bf(v[0], v[1], w0.x, K), gs_bf(v[2], v[3], w0.y, K);
+    gs_bf(v[4], v[5], w1.x, K), gs_bf(v[6], v[7], w1.y, K);
+    const double2 w2 = *(const double2*)(ipsi + (m >> 1) + 2 * g);
+    gs_bf(v[0], v[2], w2.x, K), gs_bf(v[1], v[3], w2.x, K);
+    gs_bf(v[4], v[6], w2.y, K), gs_bf(v[5], v[7], w2.y, K);
+    const double w3 = ipsi[(m >> 2) + g];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) gs_bf(v[k], v[k + 4], w3, K);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[ad[k]] = (RED && k < 4) ? fred(v[k], K) : v[k];
+}
+
+__device__ __forceinline__ void ad_A(uint32_t tau, uint32_t (&ad)[8]) {
+    const uint32_t a0 = swz(tau);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) ad[k] = a0 + 256 * k;
+}
+__device__ __forceinline__ void ad_B(uint32_t tau, uint32_t (&ad)[8]) {
+    const uint32_t b0 = ((tau >> 5) << 8) + (tau & 31);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) ad[k] = (b0 ^ swzf(k)) + 32 * k;
+}
+__device__ __forceinline__ void ad_C(uint32_t tau, uint32_t (&ad)[8]) {
+    const uint32_t c0 = swz(((tau >> 2) << 5) + (tau & 3));
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) ad[k] = c0 ^ (4 * k);
+}
+
+// tau, laundered so that no pass's addresses are hoisted out of the round loop (they would
+// stay live across the whole kernel and spill)
+__device__ __forceinline__ uint32_t f64_tau() {
+    uint32_t tau = threadIdx.x & 255;
+    asm volatile("" : "+v"(tau));
+    return tau;
+}
+
+template <uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_ntt_fwd2048(double* buf, const double* psi, const F64Const& K) {
+    static_assert(TH == 512, "one thread per 8 elements of one polynomial");
+    constexpr uint32_t N = 2048;
+    const uint32_t tau = f64_tau();
+    double* p = buf + (threadIdx.x >> 8) * N;
+    {
+        uint32_t ad[8];
+        ad_A(tau, ad);
+        f64_r8_fwd<RED>(p, ad, 1, 0, psi, K);
+    }
+    __syncthreads();
+    {
+        uint32_t ad[8];
+        ad_B(tau, ad);
+        f64_r8_fwd<RED>(p, ad, 8, tau >> 5, psi, K);
+    }
+    __syncthreads();
+    {
+        uint32_t ad[8];
+        ad_C(tau, ad);
+        f64_r8_fwd<RED>(p, ad, 64, tau >> 2, psi, K);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
+        const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
+        double v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        const double w = psi[N / 4 + u];
+        ct_bf(v0, v2, w, K), ct_bf(v1, v3, w, K);
+        const double2 w1 = *(const double2*)(psi + N / 2 + 2 * u);
+        ct_bf(v0, v1, w1.x, K), ct_bf(v2, v3, w1.y, K);
+        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
+        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
+    }
+    __syncthreads();
+}
+
+template <uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_ntt_inv2048(double* buf, const double* ipsi, const F64Const& K) {
+    static_assert(TH == 512, "one thread per 8 elements of one polynomial");
+    constexpr uint32_t N = 2048;
+    const uint32_t tau = f64_tau();
+    double* p = buf + (threadIdx.x >> 8) * N;
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {  // h = 1 then h = 2 on units 4u .. 4u+3
+        const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
+        double v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        const double2 w1 = *(const double2*)(ipsi + N / 2 + 2 * u);
+        gs_bf(v0, v1, w1.x, K), gs_bf(v2, v3, w1.y, K);
+        const double w = ipsi[N / 4 + u];
+        gs_bf(v0, v2, w, K), gs_bf(v1, v3, w, K);
+        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K);
+        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
+    }
+    __syncthreads();
+    {
+        uint32_t ad[8];
+        ad_C(tau, ad);
+        f64_r8_inv<RED>(p, ad, 256, tau >> 2, ipsi, K);
+    }
+    __syncthreads();
+    {
+        uint32_t ad[8];
+        ad_B(tau, ad);
+        f64_r8_inv<RED>(p, ad, 32, tau >> 5, ipsi, K);
+    }
+    __syncthreads();
+    {
+        uint32_t ad[8];
+        ad_A(tau, ad);
+        f64_r8_inv<RED>(p, ad, 4, 0, ipsi, K);
+    }
+    __syncthreads();
+}
+
+template <uint32_t N, uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_fwd(double* buf, const double* psi, const F64Const& K) {
+    if constexpr (N == 2048) f64_ntt_fwd2048<TH, RED>(buf, psi, K);
+    else f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+}
+template <uint32_t N, uint32_t TH, bool RED>
+__device__ __forceinline__ void f64_inv(double* buf, const double* ipsi, const F64Const& K) {
+    if constexpr (N == 2048) f64_ntt_inv2048<TH, RED>(buf, ipsi, K);
+    else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
+}
+
 // exact double (|x| < 2^52, integer) -> int64
 __device__ __forceinline__ int64_t d2ll(double x) {
     const double hi = floor(__dmul_rn(x, 0x1p-32));
@@ -164,6 +351,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const uint32_t ts = bidx<N>(t);  // swz(t + TH k) = swz(t) + TH k (TH a multiple of 256)
     for (uint32_t k = t; k < twoN; k += F64_THREADS) lds_d[k] = tabs[k];
     const double* mono = tabs + twoN;
     const double* bsk = tabs + 2 * twoN;
@@ -190,14 +378,14 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int k = 0; k < CN; ++k)
-                buf[p * N + t + F64_THREADS * k] =
+                buf[p * N + ts + F64_THREADS * k] =
                     (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
         __syncthreads();
-        f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+        f64_fwd<N, TH, RED>(buf, psi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int k = 0; k < CN; ++k) Cn[p][k] = fmodmul(buf[p * N + t + F64_THREADS * k], K.Ninv, K);
+            for (int k = 0; k < CN; ++k) Cn[p][k] = fmodmul(buf[p * N + ts + F64_THREADS * k], K.Ninv, K);
         __syncthreads();
     }
     const uint32_t Ld = FOLD ? P.digits - 1 : P.digits;  // digits that are transformed
@@ -237,15 +425,15 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
                     const int64_t d = (c + Kd) >> shift;
                     const int32_t r = (int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
-                    buf[p * N + t + F64_THREADS * k] = (double)r;
+                    buf[p * N + ts + F64_THREADS * k] = (double)r;
                 }
             if (WRAP && l == 0) wrap = __syncthreads_or(wrap);
             else __syncthreads();
-            f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+            f64_fwd<N, TH, RED>(buf, psi, K);
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
                 const uint32_t x = t + F64_THREADS * k;
-                const double d0 = buf[x], d1 = buf[N + x];
+                const double d0 = buf[ts + F64_THREADS * k], d1 = buf[N + ts + F64_THREADS * k];
 #pragma unroll
                 for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -321,17 +509,17 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             const double mp = mono[ip], mn = mono[in];
             const double s0 = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
             const double s1 = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
-            buf[x] = s0;
-            buf[N + x] = s1;
+            buf[ts + F64_THREADS * k] = s0;
+            buf[N + ts + F64_THREADS * k] = s1;
             if constexpr (FOLD) Cn[0][k] = fred(__dadd_rn(Cn[0][k], s0), K), Cn[1][k] = fred(__dadd_rn(Cn[1][k], s1), K);
         }
         __syncthreads();
-        f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
+        f64_inv<N, TH, RED>(buf, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
-                const double r = buf[p * N + t + F64_THREADS * k];  // |r| < 2^52
+                const double r = buf[p * N + ts + F64_THREADS * k];  // |r| < 2^52
                 const double q = __builtin_rint(__dmul_rn(r, K.Qinv));
                 int64_t v = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
                 v = v < 0 ? v + Qs : v;
