@@ -177,12 +177,8 @@ __device__ __forceinline__ void gs_bf(double& a, double& b, double w, const F64C
 __device__ __forceinline__ uint32_t swzf(uint32_t c) { return (c << 2) ^ (c & 3); }
 
 // forward CT stages s0, s0+1, s0+2 (m0 = 2^s0) on the 8 elements at ad[]; g = block
-template <bool RED>
-__device__ __forceinline__ void f64_r8_fwd(double* p, const uint32_t (&ad)[8], uint32_t m0, uint32_t g,
-                                           const double* psi, const F64Const& K) {
-    double v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+__device__ __forceinline__ void f64_r8_fwd_core(double (&v)[8], uint32_t m0, uint32_t g, const double* psi,
+                                                const F64Const& K) {
     const double w0 = psi[m0 + g];
 #pragma unroll
     for (int k = 0; k < 4; ++k) ct_bf(v[k], v[k + 4], w0, K);
@@ -193,17 +189,21 @@ __device__ __forceinline__ void f64_r8_fwd(double* p, const uint32_t (&ad)[8], u
     const double2 w3 = *(const double2*)(psi + 4 * m0 + 4 * g + 2);
     ct_bf(v[0], v[1], w2.x, K), ct_bf(v[2], v[3], w2.y, K);
     ct_bf(v[4], v[5], w3.x, K), ct_bf(v[6], v[7], w3.y, K);
+}
+template <bool RED>
+__device__ __forceinline__ void f64_r8_fwd(double* p, const uint32_t (&ad)[8], uint32_t m0, uint32_t g,
+                                           const double* psi, const F64Const& K) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+    f64_r8_fwd_core(v, m0, g, psi, K);
 #pragma unroll
     for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
 }
 
 // inverse GS stages h0, 2h0, 4h0 on the 8 elements at ad[]; g = block (8 h0 elements), m = N/(2h0)
-template <bool RED>
-__device__ __forceinline__ void f64_r8_inv(double* p, const uint32_t (&ad)[8], uint32_t m, uint32_t g,
-                                           const double* ipsi, const F64Const& K) {
-    double v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+__device__ __forceinline__ void f64_r8_inv_core(double (&v)[8], uint32_t m, uint32_t g, const double* ipsi,
+                                                const F64Const& K) {
     const double2 w0 = *(const double2*)(ipsi + m + 4 * g);
     const double2 w1 = *(const double2*)(ipsi + m + 4 * g + 2);
     gs_bf(v[0], v[1], w0.x, K), gs_bf(v[2], v[3], w0.y, K);
@@ -214,6 +214,14 @@ __device__ __forceinline__ void f64_r8_inv(double* p, const uint32_t (&ad)[8], u
     const double w3 = ipsi[(m >> 2) + g];
 #pragma unroll
     for (int k = 0; k < 4; ++k) gs_bf(v[k], v[k + 4], w3, K);
+}
+template <bool RED>
+__device__ __forceinline__ void f64_r8_inv(double* p, const uint32_t (&ad)[8], uint32_t m, uint32_t g,
+                                           const double* ipsi, const F64Const& K) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+    f64_r8_inv_core(v, m, g, ipsi, K);
 #pragma unroll
     for (int k = 0; k < 8; ++k) p[ad[k]] = (RED && k < 4) ? fred(v[k], K) : v[k];
 }
@@ -243,15 +251,17 @@ __device__ __forceinline__ uint32_t f64_tau() {
 }
 
 template <uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_fwd2048(double* buf, const double* psi, const F64Const& K) {
+__device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], const double* psi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
     const uint32_t tau = f64_tau();
     double* p = buf + (threadIdx.x >> 8) * N;
-    {
+    {  // pass A on v = elements tau + 256k of polynomial t >> 8, held in registers
         uint32_t ad[8];
         ad_A(tau, ad);
-        f64_r8_fwd<RED>(p, ad, 1, 0, psi, K);
+        f64_r8_fwd_core(v, 1, 0, psi, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
     }
     __syncthreads();
     {
@@ -281,7 +291,7 @@ __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, const double* psi, 
 }
 
 template <uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_inv2048(double* buf, const double* ipsi, const F64Const& K) {
+__device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], const double* ipsi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
     const uint32_t tau = f64_tau();
@@ -310,23 +320,13 @@ __device__ __forceinline__ void f64_ntt_inv2048(double* buf, const double* ipsi,
         f64_r8_inv<RED>(p, ad, 32, tau >> 5, ipsi, K);
     }
     __syncthreads();
-    {
+    {  // pass A: v = elements tau + 256k of polynomial t >> 8, left in registers
         uint32_t ad[8];
         ad_A(tau, ad);
-        f64_r8_inv<RED>(p, ad, 4, 0, ipsi, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+        f64_r8_inv_core(v, 4, 0, ipsi, K);
     }
-    __syncthreads();
-}
-
-template <uint32_t N, uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_fwd(double* buf, const double* psi, const F64Const& K) {
-    if constexpr (N == 2048) f64_ntt_fwd2048<TH, RED>(buf, psi, K);
-    else f64_ntt_fwd<N, TH, RED>(buf, psi, K);
-}
-template <uint32_t N, uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_inv(double* buf, const double* ipsi, const F64Const& K) {
-    if constexpr (N == 2048) f64_ntt_inv2048<TH, RED>(buf, ipsi, K);
-    else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
 }
 
 // exact double (|x| < 2^52, integer) -> int64
@@ -339,7 +339,10 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 // table block (doubles): psi[N] ipsi[N] mono[2N], then the BSK [n][2][dG2][2][N]
 // TH threads own CN slots each (t + TH k): N = 1024 runs 256 x 4, N = 2048 runs 512 x 4, so a
 // thread's state (acc, sums, C') fits 128 VGPRs and a CU holds 4 waves per SIMD (two 64 KiB
-// workgroups).
+// workgroups).  N = 2048 (AM): the accumulator is held in the layout of the transforms' pass A
+// instead (thread t: polynomial t >> 8, coefficients (t & 255) + 256q, q < 8), so the digits
+// enter the forward transform and the inverse transform's output enters the accumulator
+// update in registers; the products (C', sums, monomials) keep the slot layout.
 template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false>
 __global__ void __launch_bounds__(TH, 4)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
@@ -352,6 +355,12 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     double* buf = lds_d + 2 * N;  // [2][N]
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t ts = bidx<N>(t);  // swz(t + TH k) = swz(t) + TH k (TH a multiple of 256)
+    constexpr bool AM = N == 2048;
+    // logical position (polynomial * N + coefficient) of accumulator entry [p][k]
+    auto lpos = [t](int p, int k) -> uint32_t {
+        if constexpr (AM) return (t >> 8) * N + (t & 255) + 256 * (p * CN + k);
+        else return p * N + t + TH * k;
+    };
     for (uint32_t k = t; k < twoN; k += F64_THREADS) lds_d[k] = tabs[k];
     const double* mono = tabs + twoN;
     const double* bsk = tabs + 2 * twoN;
@@ -368,20 +377,30 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
-            const uint64_t v = g[p * N + t + F64_THREADS * k];
+            const uint64_t v = g[lpos(p, k)];
             acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
         }
     __syncthreads();
     double Cn[2][CN];  // FOLD: N^-1 NTT(acc), |Cn| <~ Q/2
     if constexpr (FOLD) {
+        if constexpr (AM) {
+            double v[8];
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+            for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int k = 0; k < CN; ++k)
-                buf[p * N + ts + F64_THREADS * k] =
-                    (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
-        __syncthreads();
-        f64_fwd<N, TH, RED>(buf, psi, K);
+                for (int k = 0; k < CN; ++k)
+                    v[p * CN + k] = (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
+            f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
+        } else {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k)
+                    buf[p * N + ts + F64_THREADS * k] =
+                        (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
+            __syncthreads();
+            f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+        }
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -413,11 +432,13 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
                     wrap |= ((c + KdL) >> shiftL) != 0;
                 }
+            if constexpr (AM) wrap = __syncthreads_or(wrap);
         }
         for (uint32_t l = 0; l < Ld; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
             for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
+            double v[8];
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -425,11 +446,16 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
                     const int64_t d = (c + Kd) >> shift;
                     const int32_t r = (int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
-                    buf[p * N + ts + F64_THREADS * k] = (double)r;
+                    if constexpr (AM) v[p * CN + k] = (double)r;
+                    else buf[p * N + ts + F64_THREADS * k] = (double)r;
                 }
-            if (WRAP && l == 0) wrap = __syncthreads_or(wrap);
-            else __syncthreads();
-            f64_fwd<N, TH, RED>(buf, psi, K);
+            if constexpr (AM) {
+                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);  // no barrier: pass A writes this thread's own entries
+            } else {
+                if (WRAP && l == 0) wrap = __syncthreads_or(wrap);
+                else __syncthreads();
+                f64_ntt_fwd<N, TH, RED>(buf, psi, K);
+            }
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
                 const uint32_t x = t + F64_THREADS * k;
@@ -471,7 +497,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
 #pragma unroll
                     for (int k = 0; k < CN; ++k) {
                         const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
-                        buf[p * N + t + F64_THREADS * k] = (double)((c + KdL) >> shiftL);
+                        buf[lpos(p, k)] = (double)((c + KdL) >> shiftL);
                     }
                 __syncthreads();
                 const uint32_t l = Ld;
@@ -514,23 +540,28 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             if constexpr (FOLD) Cn[0][k] = fred(__dadd_rn(Cn[0][k], s0), K), Cn[1][k] = fred(__dadd_rn(Cn[1][k], s1), K);
         }
         __syncthreads();
-        f64_inv<N, TH, RED>(buf, ipsi, K);
+        double v[8];
+        if constexpr (AM) f64_ntt_inv2048<TH, RED>(buf, v, ipsi, K);
+        else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
-                const double r = buf[p * N + ts + F64_THREADS * k];  // |r| < 2^52
+                const double r = AM ? v[p * CN + k] : buf[p * N + ts + F64_THREADS * k];  // |r| < 2^52
                 const double q = __builtin_rint(__dmul_rn(r, K.Qinv));
-                int64_t v = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
-                v = v < 0 ? v + Qs : v;
-                acc[p][k] = v >= Qs ? v - Qs : v;
+                int64_t u = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
+                u = u < 0 ? u + Qs : u;
+                acc[p][k] = u >= Qs ? u - Qs : u;
             }
-        __syncthreads();
+        // AM: the last inverse pass only read this thread's own entries, and the next writes
+        // (the next round's pass A) are to the same entries -- no barrier
+        if constexpr (!AM) __syncthreads();
     }
+    if constexpr (AM) __syncthreads();  // every last inverse pass has read its entries
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int k = 0; k < CN; ++k) buf[p * N + t + F64_THREADS * k] = __builtin_bit_cast(double, acc[p][k]);
+        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = __builtin_bit_cast(double, acc[p][k]);
     __syncthreads();
     for (uint32_t k = t; k < N; k += F64_THREADS) {  // acc0 transposed (poly.cpp:762-770)
         const uint64_t v = __builtin_bit_cast(uint64_t, buf[k == 0 ? 0 : N - k]);
