@@ -1,0 +1,33 @@
+"""CPU checks of the kernels' LDS layouts and transform schedules (no GPU).
+
+The N = 2048 transforms of the exact-FP64 kernel and of the generic u64 kernel gen3 share one
+schedule (radix-8 passes over stages 0-2, 3-5, 6-8, two radix-4 units on 9-10) and one XOR
+swizzle; tools/lds_layouts_f64.py replays the kernels' thread -> element and twiddle formulas
+against the plain stage loops and checks every 64-bit LDS access pattern for bank conflicts.
+The four-wavefront STD128 kernel's exchanges are checked by tools/lds_layouts4.py.
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_tool(name):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", name)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_f64_gen3_transform_schedule_and_banks():
+    out = run_tool("lds_layouts_f64.py")
+    assert "index algebra: forward and inverse passes equal the stage loops" in out
+    assert out.strip().endswith("OK")
+
+
+def test_fast4_exchange_layouts():
+    out = run_tool("lds_layouts4.py")
+    ways = [int(w) for w in re.findall(r"max (\d+)-way", out)]
+    assert len(ways) == 8 and max(ways) == 1, out

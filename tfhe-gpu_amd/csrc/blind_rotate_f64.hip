@@ -16,6 +16,7 @@
 // (canonical [0, Q)) for the closed-form digit decomposition of the generic v2 kernel.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_math.hpp"
 #include "kernels.hpp"
@@ -29,6 +30,7 @@ struct F64Const {
     int64_t Qi;
     double Ninv;  // N^-1 mod Q, centred (FOLD)
     double wfac;  // 2^(gL) N^-1 mod Q, centred (WRAP)
+    int wrap_vote;  // WRAP: 1; 0 = timing experiment (TFHE_F64_FOLD=4: the vote is never raised)
 };
 
 // Top-digit elimination (FOLD), as in the specialised STD128 kernel (blind_rotate_fast4.hip):
@@ -353,6 +355,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     double* psi = lds_d;
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
+    __shared__ int wflag[2];  // WRAP vote of round i in wflag[i & 1], published by the round's first barrier
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t ts = bidx<N>(t);  // swz(t + TH k) = swz(t) + TH k (TH a multiple of 256)
     constexpr bool AM = N == 2048;
@@ -380,6 +383,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             const uint64_t v = g[lpos(p, k)];
             acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
         }
+    if (WRAP && t < 2) wflag[t] = 0;
     __syncthreads();
     double Cn[2][CN];  // FOLD: N^-1 NTT(acc), |Cn| <~ Q/2
     if constexpr (FOLD) {
@@ -423,37 +427,45 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0.0;
         const double* ek = bsk + (size_t)i * round_words;
-        int wrap = 0;
-        if constexpr (WRAP) {
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int k = 0; k < CN; ++k) {
-                    const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
-                    wrap |= ((c + KdL) >> shiftL) != 0;
-                }
-            if constexpr (AM) wrap = __syncthreads_or(wrap);
-        }
-        for (uint32_t l = 0; l < Ld; ++l) {
+        // One digit: extraction (registers), forward transform, products with rows 2l, 2l+1.
+        // CHECK (WRAP, digit 0): also raise the round's vote, wflag[i & 1], published by the
+        // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
+        // the correction "digit" -2^(gL) N^-1 w against the top rows, so that the round uses
+        // C' - 2^(gL) N^-1 NTT(w) in place of C' (w = 0 almost everywhere, |w| <= 1).
+        auto digit = [&](uint32_t l, auto corr_c, auto check_c) {
+            constexpr bool CORR = decltype(corr_c)::value, CHECK = decltype(check_c)::value;
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
             for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
             double v[8];
+            bool w = false;
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) {
                     const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
-                    const int64_t d = (c + Kd) >> shift;
-                    const int32_t r = (int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
-                    if constexpr (AM) v[p * CN + k] = (double)r;
-                    else buf[p * N + ts + F64_THREADS * k] = (double)r;
+                    double dv;
+                    if constexpr (CORR) {
+                        dv = __dmul_rn((double)((c + KdL) >> shiftL), -K.wfac);
+                    } else {
+                        const int64_t d = (c + Kd) >> shift;
+                        dv = (double)(int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
+                    }
+                    if constexpr (CHECK) w |= ((c + KdL) >> shiftL) != 0;
+                    if constexpr (AM) v[p * CN + k] = dv;
+                    else buf[p * N + ts + F64_THREADS * k] = dv;
                 }
+            if constexpr (CHECK) {
+                // round i - 1 read wflag[(i + 1) & 1] before its last barriers; round i + 1
+                // writes it after this round's barriers
+                if (t == 0) wflag[(i + 1) & 1] = 0;
+                if (w && K.wrap_vote) wflag[i & 1] = 1;
+            }
             if constexpr (AM) {
-                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);  // no barrier: pass A writes this thread's own entries
+                // no barrier before: pass A writes this thread's own entries
+                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
             } else {
-                if (WRAP && l == 0) wrap = __syncthreads_or(wrap);
-                else __syncthreads();
+                __syncthreads();
                 f64_ntt_fwd<N, TH, RED>(buf, psi, K);
             }
 #pragma unroll
@@ -470,6 +482,15 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                     }
             }
             __syncthreads();
+        };
+        using F_ = std::false_type;
+        using T_ = std::true_type;
+        if constexpr (WRAP) {
+            digit(0, F_{}, T_{});
+            for (uint32_t l = 1; l < Ld; ++l) digit(l, F_{}, F_{});
+            if (wflag[i & 1]) digit(Ld, T_{}, F_{});
+        } else {
+            for (uint32_t l = 0; l < Ld; ++l) digit(l, F_{}, F_{});
         }
         if constexpr (FOLD) {  // the top digit's rows carry N 2^-(g(L-1)) W_top: multiply C'
             const uint32_t l = Ld;
@@ -485,47 +506,6 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                         A[kk][j][k] = __dadd_rn(A[kk][j][k],
                                                 __dadd_rn(fmodmul(Cn[0][k], ek[o0], K), fmodmul(Cn[1][k], ek[o1], K)));
                     }
-            }
-        }
-        if constexpr (WRAP) {
-            // Rare path (workgroup-uniform vote): subtract 2^(gL) N^-1 NTT(w) times the C rows.
-            // w is sparse, so NTT(w)[x] = sum_j w_j psi^(e_x j) is evaluated directly from the
-            // monomial table (psi^k = mono[k] + 1) by a broadcast scan over w in LDS.
-            if (wrap) {
-#pragma unroll
-                for (int p = 0; p < 2; ++p)
-#pragma unroll
-                    for (int k = 0; k < CN; ++k) {
-                        const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
-                        buf[lpos(p, k)] = (double)((c + KdL) >> shiftL);
-                    }
-                __syncthreads();
-                const uint32_t l = Ld;
-#pragma unroll
-                for (int k = 0; k < CN; ++k) {
-                    const uint32_t x = t + F64_THREADS * k, e = eidx[x];
-                    double n0 = 0.0, n1 = 0.0;
-#pragma unroll 1
-                    for (uint32_t jx = 0; jx < N; ++jx) {
-                        const double w0 = buf[jx], w1 = buf[N + jx];
-                        if (w0 != 0.0 || w1 != 0.0) {
-                            const double z = __dadd_rn(mono[(e * jx) & (twoN - 1)], 1.0);
-                            n0 = fred(__fma_rn(w0, z, n0), K);
-                            n1 = fred(__fma_rn(w1, z, n1), K);
-                        }
-                    }
-                    n0 = fmodmul(n0, K.wfac, K);
-                    n1 = fmodmul(n1, K.wfac, K);
-#pragma unroll
-                    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) {
-                            const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
-                            const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
-                            A[kk][j][k] = __dsub_rn(A[kk][j][k], __dadd_rn(fmodmul(n0, ek[o0], K), fmodmul(n1, ek[o1], K)));
-                        }
-                }
-                __syncthreads();  // every scan is done before the increment overwrites buf
             }
         }
 #pragma unroll
@@ -651,7 +631,7 @@ size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n 
 bool f64_fold_enabled(const BRParams& P) {
     const char* e = std::getenv("TFHE_F64_FOLD");
     const int mode = e && e[0] ? e[0] - '0' : 1;
-    return mode == 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
+    return mode >= 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
 }
 
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
@@ -676,7 +656,16 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     const uint64_t wf = (uint64_t)((unsigned __int128)pow_mod(2, (uint64_t)P.logG * P.digits, P.Q) * ninv % P.Q);
     K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
-    const bool wrap = fold && !fold_exact(P);
+    static const bool nowrap = [] {  // TFHE_F64_FOLD=3: timing experiment only (drops the correction)
+        const char* e = std::getenv("TFHE_F64_FOLD");
+        return e && e[0] == '3';
+    }();
+    const bool wrap = fold && !fold_exact(P) && !nowrap;
+    static const bool novote = [] {
+        const char* e = std::getenv("TFHE_F64_FOLD");
+        return e && e[0] == '4';
+    }();
+    K.wrap_vote = !novote;
     const size_t lds = (size_t)4 * P.N * sizeof(double);  // psi, ipsi, two polynomials
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
