@@ -432,8 +432,11 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
         // the correction "digit" -2^(gL) N^-1 w against the top rows, so that the round uses
         // C' - 2^(gL) N^-1 NTT(w) in place of C' (w = 0 almost everywhere, |w| <= 1).
-        auto digit = [&](uint32_t l, auto corr_c, auto check_c) {
+        // CMERGE (FOLD without WRAP, last digit): the C' rows' products join this digit's product
+        // loop, so a round has one key-load phase fewer
+        auto digit = [&](uint32_t l, auto corr_c, auto check_c, auto cmerge_c) {
             constexpr bool CORR = decltype(corr_c)::value, CHECK = decltype(check_c)::value;
+            constexpr bool CMERGE = decltype(cmerge_c)::value;
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
             for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
@@ -479,6 +482,12 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                         const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
                         const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
                         A[kk][j][k] = __dadd_rn(A[kk][j][k], __dadd_rn(fmodmul(d0, ek[o0], K), fmodmul(d1, ek[o1], K)));
+                        if constexpr (CMERGE) {
+                            const size_t c0 = ((size_t)(kk * P.dG2 + 2 * Ld) * 2 + j) * N + x;
+                            const size_t c1 = ((size_t)(kk * P.dG2 + 2 * Ld + 1) * 2 + j) * N + x;
+                            A[kk][j][k] = __dadd_rn(A[kk][j][k],
+                                                    __dadd_rn(fmodmul(Cn[0][k], ek[c0], K), fmodmul(Cn[1][k], ek[c1], K)));
+                        }
                     }
             }
             __syncthreads();
@@ -486,13 +495,16 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         using F_ = std::false_type;
         using T_ = std::true_type;
         if constexpr (WRAP) {
-            digit(0, F_{}, T_{});
-            for (uint32_t l = 1; l < Ld; ++l) digit(l, F_{}, F_{});
-            if (wflag[i & 1]) digit(Ld, T_{}, F_{});
+            digit(0, F_{}, T_{}, F_{});
+            for (uint32_t l = 1; l < Ld; ++l) digit(l, F_{}, F_{}, F_{});
+            if (wflag[i & 1]) digit(Ld, T_{}, F_{}, F_{});
+        } else if constexpr (FOLD) {
+            for (uint32_t l = 0; l + 1 < Ld; ++l) digit(l, F_{}, F_{}, F_{});
+            digit(Ld - 1, F_{}, F_{}, T_{});
         } else {
-            for (uint32_t l = 0; l < Ld; ++l) digit(l, F_{}, F_{});
+            for (uint32_t l = 0; l < Ld; ++l) digit(l, F_{}, F_{}, F_{});
         }
-        if constexpr (FOLD) {  // the top digit's rows carry N 2^-(g(L-1)) W_top: multiply C'
+        if constexpr (FOLD && WRAP) {  // the top digit's rows carry N 2^-(g(L-1)) W_top: multiply C'
             const uint32_t l = Ld;
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
