@@ -471,24 +471,43 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                 __syncthreads();
                 f64_ntt_fwd<N, TH, RED>(buf, psi, K);
             }
-#pragma unroll
-            for (int k = 0; k < CN; ++k) {
-                const uint32_t x = t + F64_THREADS * k;
-                const double d0 = buf[ts + F64_THREADS * k], d1 = buf[N + ts + F64_THREADS * k];
+            // Products, software-pipelined: group g = (slot k, rows) has 8 key values; the next
+            // group's loads are issued before this group's arithmetic (double-buffered
+            // registers, sched_barrier fences), so key misses overlap instead of being paid one
+            // load at a time.  Rows: the digit's (2l, 2l+1); CMERGE adds the C' rows (2Ld, 2Ld+1).
+            constexpr int GPS = CMERGE ? 2 : 1, NG = CN * GPS;
+            auto kload = [&](int g, double (&kv)[8]) {
+                const uint32_t x = t + F64_THREADS * (g / GPS);
+                const uint32_t r = (GPS == 2 && (g & 1)) ? Ld : l;
 #pragma unroll
                 for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
-                        const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
-                        A[kk][j][k] = __dadd_rn(A[kk][j][k], __dadd_rn(fmodmul(d0, ek[o0], K), fmodmul(d1, ek[o1], K)));
-                        if constexpr (CMERGE) {
-                            const size_t c0 = ((size_t)(kk * P.dG2 + 2 * Ld) * 2 + j) * N + x;
-                            const size_t c1 = ((size_t)(kk * P.dG2 + 2 * Ld + 1) * 2 + j) * N + x;
-                            A[kk][j][k] = __dadd_rn(A[kk][j][k],
-                                                    __dadd_rn(fmodmul(Cn[0][k], ek[c0], K), fmodmul(Cn[1][k], ek[c1], K)));
-                        }
+                        kv[(kk * 2 + j) * 2] = ek[((size_t)(kk * P.dG2 + 2 * r) * 2 + j) * N + x];
+                        kv[(kk * 2 + j) * 2 + 1] = ek[((size_t)(kk * P.dG2 + 2 * r + 1) * 2 + j) * N + x];
                     }
+            };
+            double kv[2][8];
+            kload(0, kv[0]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g + 1 < NG) kload(g + 1, kv[(g + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int k = g / GPS;
+                double d0, d1;
+                if (GPS == 2 && (g & 1)) {
+                    d0 = Cn[0][k], d1 = Cn[1][k];
+                } else {
+                    d0 = buf[ts + F64_THREADS * k], d1 = buf[N + ts + F64_THREADS * k];
+                }
+                const double(&cur)[8] = kv[g & 1];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        A[kk][j][k] = __dadd_rn(A[kk][j][k], __dadd_rn(fmodmul(d0, cur[(kk * 2 + j) * 2], K),
+                                                                       fmodmul(d1, cur[(kk * 2 + j) * 2 + 1], K)));
+                __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
         };
