@@ -577,20 +577,36 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
                     v[p * CN + k] = (uint64_t)r;
                 }
             g3_ntt_fwd(buf, v, TF, Q2, Q);  // pass A writes this thread's own entries: no barrier before
-            // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both output polynomials
+            // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both output polynomials;
+            // software-pipelined as in blind_rotate_f64.hip: group g = (slot k, key kk) holds 4 key
+            // words + 4 Shoup companions, the next group's loads are issued before this group's
+            // arithmetic (double-buffered, sched_barrier fences)
+            constexpr int NG = CN * 2;
+            auto kload = [&](int g, uint64_t (&kv)[8]) {
+                const uint32_t x = t + TH * (g >> 1), kk = g & 1;
 #pragma unroll
-            for (int k = 0; k < CN; ++k) {
-                const uint32_t x = t + TH * k;
-                const uint64_t d0 = buf[ts + TH * k], d1 = buf[N + ts + TH * k];
+                for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
-                        const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
-                        A[kk][j][k] += shoup_lazy<uint64_t>(d0, ek[o0], eks[o0], Q) +
-                                       shoup_lazy<uint64_t>(d1, ek[o1], eks[o1], Q);
+                    for (int r = 0; r < 2; ++r) {
+                        const size_t o = ((size_t)(kk * P.dG2 + 2 * l + r) * 2 + j) * N + x;
+                        kv[(j * 2 + r) * 2] = ek[o];
+                        kv[(j * 2 + r) * 2 + 1] = eks[o];
                     }
+            };
+            uint64_t kv[2][8];
+            kload(0, kv[0]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g + 1 < NG) kload(g + 1, kv[(g + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int k = g >> 1, kk = g & 1;
+                const uint64_t d0 = buf[ts + TH * k], d1 = buf[N + ts + TH * k];
+                const uint64_t(&c)[8] = kv[g & 1];
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    A[kk][j][k] += shoup_lazy<uint64_t>(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], Q) +
+                                   shoup_lazy<uint64_t>(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], Q);
+                __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();  // the next pass A rewrites entries other threads' products read
         }
