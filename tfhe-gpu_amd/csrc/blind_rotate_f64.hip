@@ -432,8 +432,8 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
         // the correction "digit" -2^(gL) N^-1 w against the top rows, so that the round uses
         // C' - 2^(gL) N^-1 NTT(w) in place of C' (w = 0 almost everywhere, |w| <= 1).
-        // CMERGE (FOLD without WRAP, last digit): the C' rows' products join this digit's product
-        // loop, so a round has one key-load phase fewer
+        // CMERGE (FOLD, last digit): the C' rows' products join this digit's product loop, so a
+        // round has one key-load phase fewer
         auto digit = [&](uint32_t l, auto corr_c, auto check_c, auto cmerge_c) {
             constexpr bool CORR = decltype(corr_c)::value, CHECK = decltype(check_c)::value;
             constexpr bool CMERGE = decltype(cmerge_c)::value;
@@ -514,30 +514,19 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         using F_ = std::false_type;
         using T_ = std::true_type;
         if constexpr (WRAP) {
-            digit(0, F_{}, T_{}, F_{});
-            for (uint32_t l = 1; l < Ld; ++l) digit(l, F_{}, F_{}, F_{});
+            if (Ld == 1) {
+                digit(0, F_{}, T_{}, T_{});
+            } else {
+                digit(0, F_{}, T_{}, F_{});
+                for (uint32_t l = 1; l + 1 < Ld; ++l) digit(l, F_{}, F_{}, F_{});
+                digit(Ld - 1, F_{}, F_{}, T_{});
+            }
             if (wflag[i & 1]) digit(Ld, T_{}, F_{}, F_{});
         } else if constexpr (FOLD) {
             for (uint32_t l = 0; l + 1 < Ld; ++l) digit(l, F_{}, F_{}, F_{});
             digit(Ld - 1, F_{}, F_{}, T_{});
         } else {
             for (uint32_t l = 0; l < Ld; ++l) digit(l, F_{}, F_{}, F_{});
-        }
-        if constexpr (FOLD && WRAP) {  // the top digit's rows carry N 2^-(g(L-1)) W_top: multiply C'
-            const uint32_t l = Ld;
-#pragma unroll
-            for (int k = 0; k < CN; ++k) {
-                const uint32_t x = t + F64_THREADS * k;
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const size_t o0 = ((size_t)(kk * P.dG2 + 2 * l) * 2 + j) * N + x;
-                        const size_t o1 = ((size_t)(kk * P.dG2 + 2 * l + 1) * 2 + j) * N + x;
-                        A[kk][j][k] = __dadd_rn(A[kk][j][k],
-                                                __dadd_rn(fmodmul(Cn[0][k], ek[o0], K), fmodmul(Cn[1][k], ek[o1], K)));
-                    }
-            }
         }
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
@@ -656,12 +645,12 @@ bool f64_path_supported(const BRParams& P, int word_bits) {
 
 size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
 
-// TFHE_F64_FOLD: unset/1 = fold when the top digit is always exact (STD192 classes); 0 = never;
-// 2 = also with the WRAP correction (STD128Q: correct, but measured slower, 10.2K vs 11.8K
-// bootstraps/s on C5a, so not the default)
+// TFHE_F64_FOLD: unset/2 = fold whenever thr = 0, with the WRAP correction where the top digit
+// is not always exact (STD128Q: 16.2K vs 15.2K bootstraps/s unfolded on C5a); 1 = only where it
+// is always exact (STD192 classes); 0 = never; 3/4 = timing experiments (see launch below)
 bool f64_fold_enabled(const BRParams& P) {
     const char* e = std::getenv("TFHE_F64_FOLD");
-    const int mode = e && e[0] ? e[0] - '0' : 1;
+    const int mode = e && e[0] ? e[0] - '0' : 2;
     return mode >= 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
 }
 

@@ -57,7 +57,8 @@ hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uin
 bool f64_path_supported(const BRParams& P, int word_bits);
 size_t bsk_f64_bytes(const BRParams& P);
 // fold: eliminate the top digit's transforms (keys packed accordingly); only when
-// f64_fold_enabled(P) (thr = 0, top digit always exact; TFHE_F64_FOLD=0 turns it off).
+// f64_fold_enabled(P) (thr = 0; WRAP correction where the top digit is not always exact;
+// TFHE_F64_FOLD=1 folds only exact sets, 0 turns it off).
 bool f64_fold_enabled(const BRParams& P);
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
                                hipStream_t s);
