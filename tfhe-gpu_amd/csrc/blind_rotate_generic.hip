@@ -534,7 +534,12 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
     const uint64_t Qhalf = P.Q >> 1;
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
     const uint32_t sh = 64 - logG;
-    const G3Tw TF{psi, psi_sh}, TI{ipsi, ipsi_sh};
+    // forward twiddles (word + Shoup companion) live in LDS after the two polynomials: 64 KiB
+    // per workgroup, two workgroups per CU
+    uint64_t* psi_l = buf + 2 * N;
+    uint64_t* psis_l = psi_l + N;
+    for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psis_l[k] = psi_sh[k];
+    const G3Tw TF{psi_l, psis_l}, TI{ipsi, ipsi_sh};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
@@ -547,6 +552,7 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int k = 0; k < CN; ++k) acc[p][k] = g[lpos(p, k)];
+    __syncthreads();  // forward twiddles in LDS
 
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
@@ -657,7 +663,7 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
         return e && e[0] == '0';
     }();
     if (!v1 && !no_gen3 && word_bits == 64 && P.N == G3_N) {
-        const size_t lds = (size_t)2 * G3_N * sizeof(uint64_t);
+        const size_t lds = (size_t)4 * G3_N * sizeof(uint64_t);  // two polynomials + forward twiddles
         hipFuncSetAttribute((const void*)k_blind_rotate_gen3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_blind_rotate_gen3, dim3((unsigned)B), dim3(G3_TH), lds, s, P, (const uint64_t*)T.psi,
                            (const uint64_t*)T.psi_sh, (const uint64_t*)T.ipsi, (const uint64_t*)T.ipsi_sh,
