@@ -340,6 +340,32 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     orc.close()
 
 
+
+@pytest.mark.parametrize("pset", ["STD128Q", "STD128Q_OPT"])
+def test_wrap_correction_late_round(capi, oracle, pset):
+    """The STD128Q fold's WRAP correction in the LAST round (vote flag of round parity
+    (n-1) & 1, after n-1 rounds of flag resets): a_i = 0 for i < n-1 makes those rounds add
+    (X^0 - 1)(...) = 0, so the accumulator keeps its boundary values (centred c just below Q/2,
+    where the reference's signed digits leave a residual) until the last round, whose
+    a_{n-1} is random.  Equal to the oracle."""
+    op = oracle.params_from_set(pset)
+    cp = capi.params_from_set(pset)
+    rs = np.random.default_rng(11)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    assert ctx.info().br_kernel == 3
+    B = 3
+    a = np.zeros((B, op.n), dtype=np.uint64)
+    a[:, -1] = rs.integers(1, op.q, B, dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    half = op.Q >> 1
+    acc[:, :, 10:20] = (half - 1 - rs.integers(0, 1 << 23, (B, 2, 10))).astype(np.uint64)
+    acc[2] = rs.integers(0, op.Q, (2, op.N), dtype=np.uint64)  # a ciphertext without residuals
+    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+    ctx.GPUClean()
+    orc.close()
+
 def _prime_1_mod(m, bits):
     """Largest prime p < 2^bits with p = 1 (mod m) (deterministic Miller-Rabin for 64-bit)."""
     def is_prime(n):
