@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8192, help="ciphertexts per GPU")
+    ap.add_argument("--params", default="STD128",
+                    help="parameter set (default STD128 = the BASELINE metric; e.g. STD192 for the C4 class, "
+                         "device-resident, with --no-cpu-baseline)")
     ap.add_argument("--kernel-reps", type=int, default=2, help="blind-rotation launches timed for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--generic", action="store_true", help="force the generic LDS blind-rotation kernel")
@@ -134,6 +137,8 @@ def p_oracle(pyoracle, p):
 
 def main():
     args = parse()
+    if args.params != "STD128" and not args.no_cpu_baseline:
+        sys.exit("[bench] the cpu_baseline leg is defined for STD128; add --no-cpu-baseline")
     if args.generic:
         os.environ["TFHE_FORCE_GENERIC"] = "1"
     import torch
@@ -155,7 +160,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    p = tfhe_amd.params_from_set("STD128")
+    p = tfhe_amd.params_from_set(args.params)
     B = args.batch
     # a dedicated (non-null) stream: the engine's kernels, torch's tensors and the
     # HIP events below are all ordered on it
@@ -286,11 +291,13 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "bootstraps/sec (whole node), STD128 GINX batch=8192",
+            "metric": f"bootstraps/sec (whole node), {args.params} GINX batch={B}",
             "value": round(value, 2), "unit": "bootstraps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "STD128 GINX EvalBinGate(NAND), inputs resident in HBM",
+            "scaling": "weak", "vs_baseline": None, "data": "synthetic",
+            "dtype": {0: "u32" if int(ctx.info().word_bits) == 32 else "u64", 1: "u32", 2: "f64",
+                      3: "f64"}[int(ctx.info().br_kernel)],
+            "config": {"workload": f"{args.params} GINX EvalBinGate(NAND), inputs resident in HBM",
                        "global_batch": B * world, "batch_per_gpu": B, "n": p.n, "N": p.N, "Q": p.Q,
                        "dG2": p.dG2, "parallelism": f"shard{world}"},
             "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
