@@ -18,6 +18,11 @@ namespace tfhe {
 //          row (VEC columns of the packed, 16-byte-padded KSK A part) and adds
 //          them into exact per-column sums; the B column lives in its own array
 //          and is accumulated wave-uniformly.  One reduction, then RoundqQ to fmod.
+// The u32/u64 rows of the larger sets span 5 to 11 chunks of 64*VEC columns.  Below ~4096
+// ciphertexts one wave per ciphertext sweeping them in turn leaves the gather
+// latency-bound (C5a, 1024 per launch: 19 ms of key switch next to 44 ms of blind rotation),
+// so up to ceil(4096 / B) waves share a ciphertext's chunks; at 4096+ more waves per
+// ciphertext only widen the per-coefficient row set past L2 (measured: C3 -15 %, C4 -3.5 %).
 // The gather is L2/MALL-bandwidth bound: STD128 reads N*dKS rows x 1 KiB per
 // ciphertext (SURVEY.md 8(d) "KS gather", 2 MiB u16).
 // ---------------------------------------------------------------------------
@@ -29,13 +34,18 @@ template <> struct MkmAcc<uint16_t> { using T = uint32_t; };  // N*dKS*2^16 < 2^
 template <typename KW>
 __global__ void __launch_bounds__(64 * MKM_WAVES)
 k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, const uint64_t* __restrict__ ext,
-      uint64_t fmod, uint64_t* __restrict__ out, size_t B) {
+      uint64_t fmod, uint64_t* __restrict__ out, size_t B, uint32_t split) {
     constexpr uint32_t VEC = 16 / sizeof(KW);
     using Acc = typename MkmAcc<KW>::T;
     extern __shared__ __align__(16) unsigned char smem[];
     const uint32_t N = P.N, n = P.n, dks = P.dKS, bks = P.baseKS, npad = P.n_pad;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t ct = (size_t)blockIdx.x * MKM_WAVES + w;
+    // `split` wavefronts per ciphertext; wave s sweeps the column chunks s, s + split, ...
+    // (chunk = 64 * VEC columns)
+    const uint32_t chunks = (npad + 64 * VEC - 1) / (64 * VEC);
+    const size_t item = (size_t)blockIdx.x * MKM_WAVES + w;
+    const size_t ct = item / split;
+    const uint32_t first = (uint32_t)(item - ct * split);
     if (ct >= B) return;  // whole wavefront; no workgroup barrier below
     uint8_t* dig = smem + (size_t)w * N * dks;
     const uint64_t* e = ext + ct * (N + 1);
@@ -57,7 +67,8 @@ k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, cons
     const uint64_t qks = P.qKS;
     uint64_t* o = out + ct * (size_t)(n + 1);
     uint64_t bsum = 0;
-    for (uint32_t c0 = 0; c0 < npad; c0 += 64 * VEC) {
+    for (uint32_t chunk = first; chunk < chunks; chunk += split) {
+        const uint32_t c0 = chunk * 64 * VEC;
         const uint32_t col = c0 + lane * VEC;
         const bool on = col < npad;
         Acc acc[VEC];
@@ -75,7 +86,7 @@ k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, cons
 #pragma unroll
                     for (uint32_t v = 0; v < VEC; ++v) acc[v] += (Acc)vals[v];
                 }
-                if (c0 == 0) bsum += (uint64_t)kskb[row];
+                if (chunk == 0) bsum += (uint64_t)kskb[row];
             }
         }
 #pragma unroll
@@ -87,7 +98,7 @@ k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, cons
             }
         }
     }
-    if (lane == 0) {
+    if (first == 0 && lane == 0) {
         const uint64_t r = bsum % qks;
         o[n] = round_qQ(bq >= r ? bq - r : bq + (qks - r), fmod, qks);  // b - sum
     }
@@ -99,27 +110,31 @@ hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const v
     if (P.baseKS > 256) return hipErrorNotSupported;
     const size_t lds = (size_t)MKM_WAVES * P.N * P.dKS;
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    dim3 grid((unsigned)((B + MKM_WAVES - 1) / MKM_WAVES)), block(64 * MKM_WAVES);
+    // enough wavefronts for the gather's latency (~4096), but no more: every extra wave per
+    // ciphertext widens the rows in flight per coefficient past what the L2 holds
+    const size_t vec = 16 / (ksk_bits / 8), chunks = (P.n_pad + 64 * vec - 1) / (64 * vec);
+    const uint32_t split = (uint32_t)std::max<size_t>(1, std::min(chunks, (4096 + B - 1) / B));
+    dim3 grid((unsigned)((B * split + MKM_WAVES - 1) / MKM_WAVES)), block(64 * MKM_WAVES);
     switch (ksk_bits) {
         case 16: {
             auto k = k_mkm<uint16_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint16_t*)kska, (const uint16_t*)kskb, ext, fmod, out,
-                               B);
+                               B, split);
             break;
         }
         case 32: {
             auto k = k_mkm<uint32_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint32_t*)kska, (const uint32_t*)kskb, ext, fmod, out,
-                               B);
+                               B, split);
             break;
         }
         default: {
             auto k = k_mkm<uint64_t>;
             hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint64_t*)kska, (const uint64_t*)kskb, ext, fmod, out,
-                               B);
+                               B, split);
             break;
         }
     }
