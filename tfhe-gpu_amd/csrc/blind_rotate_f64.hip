@@ -30,7 +30,6 @@ struct F64Const {
     int64_t Qi;
     double Ninv;  // N^-1 mod Q, centred (FOLD)
     double wfac;  // 2^(gL) N^-1 mod Q, centred (WRAP)
-    int wrap_vote;  // WRAP: 1; 0 = timing experiment (TFHE_F64_FOLD=4: the vote is never raised)
 };
 
 // Top-digit elimination (FOLD), as in the specialised STD128 kernel (blind_rotate_fast4.hip):
@@ -462,7 +461,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
                 // round i - 1 read wflag[(i + 1) & 1] before its last barriers; round i + 1
                 // writes it after this round's barriers
                 if (t == 0) wflag[(i + 1) & 1] = 0;
-                if (w && K.wrap_vote) wflag[i & 1] = 1;
+                if (w) wflag[i & 1] = 1;
             }
             if constexpr (AM) {
                 // no barrier before: pass A writes this thread's own entries
@@ -647,11 +646,11 @@ size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n 
 
 // TFHE_F64_FOLD: unset/2 = fold whenever thr = 0, with the WRAP correction where the top digit
 // is not always exact (STD128Q: 16.2K vs 15.2K bootstraps/s unfolded on C5a); 1 = only where it
-// is always exact (STD192 classes); 0 = never; 3/4 = timing experiments (see launch below)
+// is always exact (STD192 classes); 0 = never
 bool f64_fold_enabled(const BRParams& P) {
     const char* e = std::getenv("TFHE_F64_FOLD");
     const int mode = e && e[0] ? e[0] - '0' : 2;
-    return mode >= 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
+    return mode == 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
 }
 
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
@@ -676,16 +675,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     const uint64_t wf = (uint64_t)((unsigned __int128)pow_mod(2, (uint64_t)P.logG * P.digits, P.Q) * ninv % P.Q);
     K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
-    static const bool nowrap = [] {  // TFHE_F64_FOLD=3: timing experiment only (drops the correction)
-        const char* e = std::getenv("TFHE_F64_FOLD");
-        return e && e[0] == '3';
-    }();
-    const bool wrap = fold && !fold_exact(P) && !nowrap;
-    static const bool novote = [] {
-        const char* e = std::getenv("TFHE_F64_FOLD");
-        return e && e[0] == '4';
-    }();
-    K.wrap_vote = !novote;
+    const bool wrap = fold && !fold_exact(P);
     const size_t lds = (size_t)4 * P.N * sizeof(double);  // psi, ipsi, two polynomials
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -118,8 +118,6 @@ struct Device {
     Scratch sc2;
     void* pin[2] = {};               // pinned staging blocks for the host-array API
     hipEvent_t pin_ev[2] = {};       // last DMA that used each block
-    hipStream_t pipe[2] = {};        // chunked bootstrap pipeline (dev_bootstrap)
-    hipEvent_t pipe_ev[3] = {};      // [0] inputs ready, [1..2] each pipe stream done
 };
 
 constexpr size_t kStageBytes = (size_t)8 << 20;
@@ -293,10 +291,6 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     if (d.stream2) hipStreamSynchronize(d.stream2);
-    for (hipStream_t ps : d.pipe)
-        if (ps) hipStreamSynchronize(ps), hipStreamDestroy(ps);
-    for (hipEvent_t e : d.pipe_ev)
-        if (e) hipEventDestroy(e);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
         hipFree(sc->a);
@@ -374,53 +368,9 @@ tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, 
     return TFHE_OK;
 }
 
-// Chunks of the bootstrap pipeline: TFHE_PIPELINE=K splits a batch of B >= 2048 into K
-// contiguous chunks on two alternating streams, so chunk i's extraction + key switch runs
-// beside chunk i+1's blind rotation (default 1: one launch per stage).
-int pipeline_chunks(size_t B) {
-    static const int k = [] {
-        const char* e = std::getenv("TFHE_PIPELINE");
-        return e ? std::max(1, std::min(16, std::atoi(e))) : 1;
-    }();
-    return B >= 2048 ? k : 1;
-}
-
-tfhe_status dev_bootstrap_one(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
-                              size_t B);
-
 // BootstrapFunc / BootstrapGate on device: ct[B][n+1] mod tv.ctmod -> out mod fmod
 tfhe_status dev_bootstrap(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
                           size_t B) {
-    const int K = pipeline_chunks(B);
-    if (K == 1) return dev_bootstrap_one(c, d, tv, b_add, ct, out, B);
-    for (int j = 0; j < 2; ++j)
-        if (!d.pipe[j]) HCHECK(hipStreamCreateWithFlags(&d.pipe[j], hipStreamNonBlocking));
-    for (hipEvent_t& e : d.pipe_ev)
-        if (!e) HCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HCHECK(hipEventRecord(d.pipe_ev[0], d.stream));
-    for (int j = 0; j < 2; ++j) HCHECK(hipStreamWaitEvent(d.pipe[j], d.pipe_ev[0], 0));
-    const size_t N = c->p.N, n = c->p.n, per = (B + K - 1) / K;
-    for (int i = 0; i < K; ++i) {
-        const size_t off = (size_t)i * per, len = std::min(per, B - std::min(B, off));
-        if (len == 0) break;
-        Device dl = d;  // same keys and scratch, a slice of it, the chunk's stream
-        dl.stream = d.pipe[i & 1];
-        dl.sc.acc += off * 2 * N;
-        dl.sc.a += off * n;
-        dl.sc.ext += off * (N + 1);
-        TvParams tc = tv;
-        if (tc.lut) tc.lut += off * tc.lut_stride;  // per-ciphertext LUTs
-        SCHECK(dev_bootstrap_one(c, dl, tc, b_add, ct + off * (n + 1), out + off * (n + 1), len));
-    }
-    for (int j = 0; j < 2; ++j) {
-        HCHECK(hipEventRecord(d.pipe_ev[1 + j], d.pipe[j]));
-        HCHECK(hipStreamWaitEvent(d.stream, d.pipe_ev[1 + j], 0));
-    }
-    return TFHE_OK;
-}
-
-tfhe_status dev_bootstrap_one(tfhe_ctx* c, Device& d, TvParams tv, uint64_t b_add, const uint64_t* ct, uint64_t* out,
-                              size_t B) {
     tv.N = c->p.N;
     tv.n = c->p.n;
     tv.Q = c->p.Q;
