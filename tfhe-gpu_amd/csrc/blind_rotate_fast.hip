@@ -722,7 +722,8 @@ size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * 
 namespace {
 // TFHE_FAST_VARIANT selects the kernel build (A/B experiments): 30-58 k_blind_rotate_fast2
 // (two wavefronts per ciphertext), >= 59 k_blind_rotate_fast4 (blind_rotate_fast4.hip; 60 =
-// default).  The variant table is in DESIGN.md 3.1.
+// default).  The variant table is in DESIGN.md 3.1.  Timing-only builds (no barriers / no key
+// loads / no transforms: results invalid) are taken only with TFHE_TIMING_EXPERIMENTS=1.
 constexpr int kDefaultVariant = 60;
 // builds the launchers know (blind_rotate_fast4.hip's list for >= 59); timing-only ones excluded
 bool known_variant(int v) {
@@ -737,6 +738,9 @@ int fast_variant() {
     if (v < 0) {
         const char* e = std::getenv("TFHE_FAST_VARIANT");
         v = e && e[0] ? std::atoi(e) : kDefaultVariant;
+        // timing-only builds (results invalid) need an explicit opt-in
+        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+        if (!known_variant(v) && !(x && x[0] == '1')) v = kDefaultVariant;
         g_variant.store(v, std::memory_order_relaxed);
     }
     return v;
