@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 1
+#define TFHE_HIP_ABI_VERSION 2  /* 2: tfhe_info.br_kernel */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,

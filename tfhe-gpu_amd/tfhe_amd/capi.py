@@ -12,6 +12,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
+ABI_VERSION = 2  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (2: tfhe_info.br_kernel)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -125,6 +126,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        if L.tfhe_abi_version() != ABI_VERSION:  # the structs above mirror this ABI version
+            raise TfheError(-1, "load", f"{_LIB} has ABI {L.tfhe_abi_version()}, binding expects {ABI_VERSION}: "
+                                        "rebuild (make -C tfhe-gpu_amd)")
         _lib = L
     return _lib
 
