@@ -385,21 +385,25 @@ __device__ __forceinline__ uint32_t g3_swz(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t g3_swzf(uint32_t c) { return (c << 2) ^ (c & 3); }
 
+template <typename W>
 struct G3Tw {
-    const uint64_t* __restrict__ w;
-    const uint64_t* __restrict__ s;
+    const W* __restrict__ w;
+    const W* __restrict__ s;
 };
 
-__device__ __forceinline__ void g3_ct(uint64_t& x, uint64_t& y, const G3Tw& T, uint32_t i, uint64_t Q2, uint64_t Q) {
-    ct_lazy<uint64_t>(x, y, T.w[i], T.s[i], Q2, Q);
+template <typename W>
+__device__ __forceinline__ void g3_ct(W& x, W& y, const G3Tw<W>& T, uint32_t i, W Q2, W Q) {
+    ct_lazy<W>(x, y, T.w[i], T.s[i], Q2, Q);
 }
-__device__ __forceinline__ void g3_gs(uint64_t& x, uint64_t& y, const G3Tw& T, uint32_t i, uint64_t Q2, uint64_t Q) {
-    gs_lazy<uint64_t>(x, y, T.w[i], T.s[i], Q2, Q);
+template <typename W>
+__device__ __forceinline__ void g3_gs(W& x, W& y, const G3Tw<W>& T, uint32_t i, W Q2, W Q) {
+    gs_lazy<W>(x, y, T.w[i], T.s[i], Q2, Q);
 }
 
 // forward CT stages s0 .. s0+2 (m0 = 2^s0) on 8 elements; g = block
-__device__ __forceinline__ void g3_fwd_core(uint64_t (&v)[8], uint32_t m0, uint32_t g, const G3Tw& T, uint64_t Q2,
-                                            uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_fwd_core(W (&v)[8], uint32_t m0, uint32_t g, const G3Tw<W>& T, W Q2,
+                                            W Q) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) g3_ct(v[k], v[k + 4], T, m0 + g, Q2, Q);
     g3_ct(v[0], v[2], T, 2 * m0 + 2 * g, Q2, Q), g3_ct(v[1], v[3], T, 2 * m0 + 2 * g, Q2, Q);
@@ -408,8 +412,9 @@ __device__ __forceinline__ void g3_fwd_core(uint64_t (&v)[8], uint32_t m0, uint3
     for (int j = 0; j < 4; ++j) g3_ct(v[2 * j], v[2 * j + 1], T, 4 * m0 + 4 * g + j, Q2, Q);
 }
 // inverse GS stages h0, 2h0, 4h0 on 8 elements; g = block, m = N / (2 h0)
-__device__ __forceinline__ void g3_inv_core(uint64_t (&v)[8], uint32_t m, uint32_t g, const G3Tw& T, uint64_t Q2,
-                                            uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_inv_core(W (&v)[8], uint32_t m, uint32_t g, const G3Tw<W>& T, W Q2,
+                                            W Q) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) g3_gs(v[2 * j], v[2 * j + 1], T, m + 4 * g + j, Q2, Q);
     g3_gs(v[0], v[2], T, (m >> 1) + 2 * g, Q2, Q), g3_gs(v[1], v[3], T, (m >> 1) + 2 * g, Q2, Q);
@@ -441,22 +446,24 @@ __device__ __forceinline__ uint32_t g3_tau() {
     return tau;
 }
 
-__device__ __forceinline__ void g3_pass_fwd(uint64_t* p, int pass, uint32_t tau, uint32_t m0, uint32_t g, const G3Tw& T,
-                                            uint64_t Q2, uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_pass_fwd(W* p, int pass, uint32_t tau, uint32_t m0, uint32_t g, const G3Tw<W>& T,
+                                            W Q2, W Q) {
     uint32_t ad[8];
     g3_ad(pass, tau, ad);
-    uint64_t v[8];
+    W v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
     g3_fwd_core(v, m0, g, T, Q2, Q);
 #pragma unroll
     for (int k = 0; k < 8; ++k) p[ad[k]] = v[k];
 }
-__device__ __forceinline__ void g3_pass_inv(uint64_t* p, int pass, uint32_t tau, uint32_t m, uint32_t g, const G3Tw& T,
-                                            uint64_t Q2, uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_pass_inv(W* p, int pass, uint32_t tau, uint32_t m, uint32_t g, const G3Tw<W>& T,
+                                            W Q2, W Q) {
     uint32_t ad[8];
     g3_ad(pass, tau, ad);
-    uint64_t v[8];
+    W v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
     g3_inv_core(v, m, g, T, Q2, Q);
@@ -465,10 +472,11 @@ __device__ __forceinline__ void g3_pass_inv(uint64_t* p, int pass, uint32_t tau,
 }
 
 // forward transform of polynomial t >> 8; v = its pass-A elements (registers), outputs in LDS
-__device__ __forceinline__ void g3_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], const G3Tw& T, uint64_t Q2, uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_ntt_fwd(W* buf, W (&v)[8], const G3Tw<W>& T, W Q2, W Q) {
     constexpr uint32_t N = G3_N;
     const uint32_t tau = g3_tau();
-    uint64_t* p = buf + (threadIdx.x >> 8) * N;
+    W* p = buf + (threadIdx.x >> 8) * N;
     {
         uint32_t ad[8];
         g3_ad(0, tau, ad);
@@ -484,7 +492,7 @@ __device__ __forceinline__ void g3_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], cons
 #pragma unroll
     for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
         const uint32_t u = tau + 256 * r, u0 = g3_swz(4 * u);
-        uint64_t v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        W v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
         g3_ct(v0, v2, T, N / 4 + u, Q2, Q), g3_ct(v1, v3, T, N / 4 + u, Q2, Q);
         g3_ct(v0, v1, T, N / 2 + 2 * u, Q2, Q), g3_ct(v2, v3, T, N / 2 + 2 * u + 1, Q2, Q);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
@@ -494,14 +502,15 @@ __device__ __forceinline__ void g3_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], cons
 
 // inverse transform of polynomial t >> 8 from LDS; v = its pass-A outputs, left in registers
 // (no trailing barrier: the last pass only read this thread's own entries)
-__device__ __forceinline__ void g3_ntt_inv(uint64_t* buf, uint64_t (&v)[8], const G3Tw& T, uint64_t Q2, uint64_t Q) {
+template <typename W>
+__device__ __forceinline__ void g3_ntt_inv(W* buf, W (&v)[8], const G3Tw<W>& T, W Q2, W Q) {
     constexpr uint32_t N = G3_N;
     const uint32_t tau = g3_tau();
-    uint64_t* p = buf + (threadIdx.x >> 8) * N;
+    W* p = buf + (threadIdx.x >> 8) * N;
 #pragma unroll
     for (uint32_t r = 0; r < 2; ++r) {  // h = 1 then h = 2 on units 4u .. 4u+3
         const uint32_t u = tau + 256 * r, u0 = g3_swz(4 * u);
-        uint64_t v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        W v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
         g3_gs(v0, v1, T, N / 2 + 2 * u, Q2, Q), g3_gs(v2, v3, T, N / 2 + 2 * u + 1, Q2, Q);
         g3_gs(v0, v2, T, N / 4 + u, Q2, Q), g3_gs(v1, v3, T, N / 4 + u, Q2, Q);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
@@ -518,28 +527,29 @@ __device__ __forceinline__ void g3_ntt_inv(uint64_t* buf, uint64_t (&v)[8], cons
     g3_inv_core(v, 4, 0, T, Q2, Q);
 }
 
+template <typename W>
 __global__ void __launch_bounds__(G3_TH, 4)
-k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi_sh,
-                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi_sh,
-                    const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono_sh,
-                    const uint32_t* __restrict__ eidx, const uint64_t* __restrict__ bsk,
-                    const uint64_t* __restrict__ bsk_sh, const uint64_t* __restrict__ a, uint64_t amod,
+k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__ psi_sh,
+                    const W* __restrict__ ipsi, const W* __restrict__ ipsi_sh,
+                    const W* __restrict__ mono, const W* __restrict__ mono_sh,
+                    const uint32_t* __restrict__ eidx, const W* __restrict__ bsk,
+                    const W* __restrict__ bsk_sh, const uint64_t* __restrict__ a, uint64_t amod,
                     uint64_t* __restrict__ acc_io) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr uint32_t N = G3_N, TH = G3_TH, CN = G3_CN;
-    uint64_t* buf = reinterpret_cast<uint64_t*>(smem);  // [2][N], swizzled
+    W* buf = reinterpret_cast<W*>(smem);  // [2][N], swizzled
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t ts = g3_swz(t);  // slot t + 512k lives at swz(t) + 512k
-    const uint64_t Q = P.Q, Q2 = 2 * Q, r1 = P.r1;
+    const W Q = (W)P.Q, Q2 = 2 * Q, r1 = (W)P.r1;
     const uint64_t Qhalf = P.Q >> 1;
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
     const uint32_t sh = 64 - logG;
     // forward twiddles (word + Shoup companion) live in LDS after the two polynomials: 64 KiB
     // per workgroup, two workgroups per CU
-    uint64_t* psi_l = buf + 2 * N;
-    uint64_t* psis_l = psi_l + N;
+    W* psi_l = buf + 2 * N;
+    W* psis_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psis_l[k] = psi_sh[k];
-    const G3Tw TF{psi_l, psis_l}, TI{ipsi, ipsi_sh};
+    const G3Tw<W> TF{psi_l, psis_l}, TI{ipsi, ipsi_sh};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
@@ -547,40 +557,40 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
     // accumulator entry [p][k]: polynomial t >> 8, coefficient (t & 255) + 256 (p CN + k)
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
 
-    uint64_t acc[2][CN];
+    W acc[2][CN];
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int k = 0; k < CN; ++k) acc[p][k] = g[lpos(p, k)];
+        for (int k = 0; k < CN; ++k) acc[p][k] = (W)g[lpos(p, k)];
     __syncthreads();  // forward twiddles in LDS
 
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-        uint64_t A[2][2][CN];  // A_kj per owned slot, lazily reduced (< 2 dG2 Q)
+        W A[2][2][CN];  // A_kj per owned slot, lazily reduced (< 2 dG2 Q)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0;
-        const uint64_t* ek = bsk + (size_t)i * round_words;
-        const uint64_t* eks = bsk_sh + (size_t)i * round_words;
+        const W* ek = bsk + (size_t)i * round_words;
+        const W* eks = bsk_sh + (size_t)i * round_words;
         for (uint32_t l = 0; l < P.digits; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
             for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
-            uint64_t v[8];
+            W v[8];
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) {
-                    const uint64_t x = acc[p][k];
+                    const uint64_t x = (uint64_t)acc[p][k];
                     const int64_t c = x < Qhalf ? (int64_t)x : (int64_t)x - Qs;
                     const int64_t d = (c + Kd) >> shift;
                     int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
                     if (r < 0) r += Qs;
-                    v[p * CN + k] = (uint64_t)r;
+                    v[p * CN + k] = (W)r;
                 }
             g3_ntt_fwd(buf, v, TF, Q2, Q);  // pass A writes this thread's own entries: no barrier before
             // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both output polynomials;
@@ -588,7 +598,7 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
             // words + 4 Shoup companions, the next group's loads are issued before this group's
             // arithmetic (double-buffered, sched_barrier fences)
             constexpr int NG = CN * 2;
-            auto kload = [&](int g, uint64_t (&kv)[8]) {
+            auto kload = [&](int g, W (&kv)[8]) {
                 const uint32_t x = t + TH * (g >> 1), kk = g & 1;
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
@@ -599,19 +609,19 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
                         kv[(j * 2 + r) * 2 + 1] = eks[o];
                     }
             };
-            uint64_t kv[2][8];
+            W kv[2][8];
             kload(0, kv[0]);
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
                 if (g + 1 < NG) kload(g + 1, kv[(g + 1) & 1]);
                 __builtin_amdgcn_sched_barrier(0);
                 const int k = g >> 1, kk = g & 1;
-                const uint64_t d0 = buf[ts + TH * k], d1 = buf[N + ts + TH * k];
-                const uint64_t(&c)[8] = kv[g & 1];
+                const W d0 = buf[ts + TH * k], d1 = buf[N + ts + TH * k];
+                const W(&c)[8] = kv[g & 1];
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    A[kk][j][k] += shoup_lazy<uint64_t>(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], Q) +
-                                   shoup_lazy<uint64_t>(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], Q);
+                    A[kk][j][k] += shoup_lazy<W>(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], Q) +
+                                   shoup_lazy<W>(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], Q);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();  // the next pass A rewrites entries other threads' products read
@@ -620,19 +630,19 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
         for (int k = 0; k < CN; ++k) {
             const uint32_t x = t + TH * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            const uint64_t mp = mono[ip], mps = mono_sh[ip], mn = mono[in], mns = mono_sh[in];
-            const uint64_t A00 = reduce_full<uint64_t>(A[0][0][k], r1, Q), A01 = reduce_full<uint64_t>(A[0][1][k], r1, Q);
-            const uint64_t A10 = reduce_full<uint64_t>(A[1][0][k], r1, Q), A11 = reduce_full<uint64_t>(A[1][1][k], r1, Q);
-            buf[ts + TH * k] = addm<uint64_t>(shoup<uint64_t>(A00, mp, mps, Q), shoup<uint64_t>(A10, mn, mns, Q), Q);
-            buf[N + ts + TH * k] = addm<uint64_t>(shoup<uint64_t>(A01, mp, mps, Q), shoup<uint64_t>(A11, mn, mns, Q), Q);
+            const W mp = mono[ip], mps = mono_sh[ip], mn = mono[in], mns = mono_sh[in];
+            const W A00 = reduce_full<W>(A[0][0][k], r1, Q), A01 = reduce_full<W>(A[0][1][k], r1, Q);
+            const W A10 = reduce_full<W>(A[1][0][k], r1, Q), A11 = reduce_full<W>(A[1][1][k], r1, Q);
+            buf[ts + TH * k] = addm<W>(shoup<W>(A00, mp, mps, Q), shoup<W>(A10, mn, mns, Q), Q);
+            buf[N + ts + TH * k] = addm<W>(shoup<W>(A01, mp, mps, Q), shoup<W>(A11, mn, mns, Q), Q);
         }
         __syncthreads();
-        uint64_t v[8];
+        W v[8];
         g3_ntt_inv(buf, v, TI, Q2, Q);  // outputs in [0, 2Q)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int k = 0; k < CN; ++k) acc[p][k] = csub<uint64_t>(csub<uint64_t>(acc[p][k] + v[p * CN + k], Q2), Q);
+            for (int k = 0; k < CN; ++k) acc[p][k] = csub<W>(csub<W>(acc[p][k] + v[p * CN + k], Q2), Q);
     }
     __syncthreads();  // every last inverse pass has read its entries
 #pragma unroll
@@ -642,7 +652,7 @@ k_blind_rotate_gen3(BRParams P, const uint64_t* __restrict__ psi, const uint64_t
     __syncthreads();
     for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
         const uint64_t v = buf[k == 0 ? 0 : N - k];
-        g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+        g[k] = k == 0 ? v : (v == 0 ? 0 : (uint64_t)Q - v);
         g[N + k] = buf[N + k];
     }
 }
@@ -662,13 +672,18 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
         const char* e = std::getenv("TFHE_GENERIC_GEN3");
         return e && e[0] == '0';
     }();
-    if (!v1 && !no_gen3 && word_bits == 64 && P.N == G3_N) {
-        const size_t lds = (size_t)4 * G3_N * sizeof(uint64_t);  // two polynomials + forward twiddles
-        hipFuncSetAttribute((const void*)k_blind_rotate_gen3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_blind_rotate_gen3, dim3((unsigned)B), dim3(G3_TH), lds, s, P, (const uint64_t*)T.psi,
-                           (const uint64_t*)T.psi_sh, (const uint64_t*)T.ipsi, (const uint64_t*)T.ipsi_sh,
-                           (const uint64_t*)T.mono, (const uint64_t*)T.mono_sh, T.eidx, (const uint64_t*)bsk,
-                           (const uint64_t*)bsk_sh, a, amod, acc);
+    if (!v1 && !no_gen3 && P.N == G3_N) {
+        const size_t lds = (size_t)4 * G3_N * wb;  // two polynomials + forward twiddles
+        auto go3 = [&](auto tag) {
+            using W = decltype(tag);
+            auto kern = k_blind_rotate_gen3<W>;
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, (const W*)T.psi, (const W*)T.psi_sh,
+                               (const W*)T.ipsi, (const W*)T.ipsi_sh, (const W*)T.mono, (const W*)T.mono_sh, T.eidx,
+                               (const W*)bsk, (const W*)bsk_sh, a, amod, acc);
+        };
+        if (word_bits == 32) go3(uint32_t{});
+        else go3(uint64_t{});
         return hipGetLastError();
     }
     if (!v1 && (P.N == 1024 || P.N == 2048)) {
