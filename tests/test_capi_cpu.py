@@ -80,3 +80,54 @@ def test_key_file_rejected_before_device_use(tmp_path):
         tfhe_amd.BinFHEContextHIP.from_key_file(p, str(bad))
     with pytest.raises(capi.TfheError, match="cannot open"):
         tfhe_amd.BinFHEContextHIP.from_key_file(p, str(tmp_path / "missing.kimg"))
+
+
+def test_binding_rejects_malformed_shapes(capi):
+    """The binding hands bare pointers to the C-ABI, so it checks every shape first
+    (the reference throws 'input ciphertexts size unmatched', binfhe-base-scheme.cpp:607).
+    The checks run before any library call, so an un-set-up context suffices."""
+    import numpy as np
+
+    p = capi.params_from_set("TOY")
+    ctx = capi.BinFHEContextHIP(p)
+    n, N, q = p.n, p.N, p.q
+    ct = np.zeros((3, n + 1), dtype=np.uint64)
+    with pytest.raises(ValueError, match="size unmatched"):
+        ctx.EvalBinGate("NAND", ct, ct[:2])
+    with pytest.raises(ValueError, match="expected shape"):
+        ctx.EvalBinGate("NAND", ct[:, :n], ct)
+    with pytest.raises(ValueError, match="expected shape"):
+        ctx.EvalBinGate("NAND", ct, np.zeros((3, n + 2), dtype=np.uint64))
+    with pytest.raises(ValueError, match="B\\*2\\*N"):
+        ctx.EvalAcc(np.zeros((2, n), dtype=np.uint64), q, np.zeros((1, 2, N), dtype=np.uint64))
+    with pytest.raises(ValueError, match="B\\*n"):
+        ctx.EvalAcc(np.zeros(n + 1, dtype=np.uint64), q, np.zeros((1, 2, N), dtype=np.uint64))
+    with pytest.raises(ValueError, match="LUT"):
+        ctx.EvalFunc(ct, np.zeros(q - 1, dtype=np.uint64))
+    with pytest.raises(ValueError, match="LUT"):
+        ctx.EvalFunc(ct, np.zeros((2, q), dtype=np.uint64))
+    with pytest.raises(ValueError, match="expected shape"):
+        ctx.MKMSwitch(np.zeros((2, N), dtype=np.uint64), q)
+    for fn in (lambda c: ctx.EvalFloor(c, 4 * q), lambda c: ctx.EvalSign(c, 4 * q),
+               lambda c: ctx.EvalDecomp(c, 4 * q)):
+        with pytest.raises(ValueError, match="expected shape"):
+            fn(np.zeros((2, n), dtype=np.uint64))
+    with pytest.raises(ValueError, match="expected shape"):
+        ctx.CiphertextMulMatrix(np.zeros((2, n), dtype=np.uint64), np.zeros((2, 2), dtype=np.int64), 1 << 20)
+
+
+def test_key_file_size_field_checked_before_allocation(tmp_path):
+    """A header whose size field disagrees with the parameters is refused before the
+    library allocates it (a hostile 2^62 must not reach std::vector::resize)."""
+    import struct
+
+    import tfhe_amd
+    from tfhe_amd import capi
+
+    p = capi.params_from_set("TOY")
+    raw = bytes(p)  # tfhe_params as laid out by the C struct
+    hdr = b"TFHEKIMG" + struct.pack("<II", capi.ABI_VERSION, 0) + raw + struct.pack("<QQ", 1 << 62, 0)
+    f = tmp_path / "huge.kimg"
+    f.write_bytes(hdr)
+    with pytest.raises(capi.TfheError, match="size field"):
+        tfhe_amd.BinFHEContextHIP.from_key_file(p, str(f))

@@ -1,0 +1,95 @@
+"""GPU parity of the batch-tiled key switch (ks_tiled.hip) against the oracle's
+ModSwitch -> KeySwitch -> ModSwitch (lwe-pke.cpp:204-215, 299-321).
+
+Batches of >= TFHE_KS_TILED_MIN ciphertexts (default 256) take the tiled form, smaller
+ones the per-ciphertext gather; both must equal the oracle bit for bit.  Every KSK word
+width the engine packs is covered: u16 (STD128, qKS = 2^14), u32 with 32-bit sums
+(STD192, qKS = 2^19, N dKS (qKS-1) < 2^32), u32 with 64-bit sums (STD128Q, qKS = 2^25)
+and u64 (the logQ = 12 arbFunc context, qKS = 2^35, dKS = 7).  Batches are ragged
+(not multiples of the 512/1024-ciphertext tiles) and include all-zero and all-(Q-1)
+extracts.  Random keys: bit-exactness does not need valid ones."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SETS = {
+    "STD128": lambda m: m.params_from_set("STD128"),
+    "STD192": lambda m: m.params_from_set("STD192"),
+    "STD128Q": lambda m: m.params_from_set("STD128Q"),
+    "ARB12": lambda m: m.params_from_logq("STD128", True, 12, 0, 0, 1),
+}
+
+
+@pytest.fixture(scope="module", params=list(SETS))
+def ks_ctx(request, oracle):
+    import tfhe_amd
+
+    op = SETS[request.param](oracle)
+    cp = SETS[request.param](tfhe_amd)
+    rs = np.random.default_rng(31)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ksk.reshape(-1, cp.n + 1)[::97] = op.qKS - 1  # rows of maximal entries: the sums' upper bound
+    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    yield request.param, op, ctx, orc
+    ctx.GPUClean()
+    orc.close()
+
+
+def _ext(op, B, seed):
+    rs = np.random.default_rng(seed)
+    ext = rs.integers(0, op.Q, (B, op.N + 1), dtype=np.uint64)
+    ext[0, :] = 0
+    ext[1, :] = op.Q - 1
+    ext[B - 1, :] = op.Q // 2
+    return ext
+
+
+def _with_min(value, fn):
+    old = os.environ.get("TFHE_KS_TILED_MIN")
+    os.environ["TFHE_KS_TILED_MIN"] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop("TFHE_KS_TILED_MIN")
+        else:
+            os.environ["TFHE_KS_TILED_MIN"] = old
+
+
+@pytest.mark.parametrize("B", [300, 1029])
+def test_tiled_keyswitch_equals_oracle(ks_ctx, B):
+    name, op, ctx, orc = ks_ctx
+    ext = _ext(op, B, B)
+    fmod = op.q
+    tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, fmod))
+    gather = _with_min("0", lambda: ctx.MKMSwitch(ext, fmod))
+    assert np.array_equal(tiled, gather)
+    # the oracle on a sample (all of them for the cheap STD128 key switch)
+    idx = np.arange(B) if name == "STD128" else np.r_[0:6, B // 2 - 3:B // 2 + 3, B - 6:B]
+    assert np.array_equal(tiled[idx], orc.mkm_switch(np.ascontiguousarray(ext[idx]), fmod))
+
+
+def test_tiled_keyswitch_other_output_moduli(ks_ctx):
+    name, op, ctx, orc = ks_ctx
+    ext = _ext(op, 260, 7)
+    idx = np.r_[0:4, 256:260]
+    for fmod in (2 * op.q, 1 << 20, op.qKS):
+        tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, fmod))
+        assert np.array_equal(tiled[idx], orc.mkm_switch(np.ascontiguousarray(ext[idx]), fmod)), fmod
+
+
+def test_default_threshold_routes_small_batches_to_gather(ks_ctx):
+    """Below the threshold (and for B = 1) the gather runs; results agree across the switch."""
+    name, op, ctx, orc = ks_ctx
+    ext = _ext(op, 255, 9)
+    a = _with_min("256", lambda: ctx.MKMSwitch(ext, op.q))
+    b = _with_min("1", lambda: ctx.MKMSwitch(ext, op.q))
+    assert np.array_equal(a, b)
+    one = _with_min("1", lambda: ctx.MKMSwitch(ext[:1], op.q))
+    assert np.array_equal(one, orc.mkm_switch(np.ascontiguousarray(ext[:1]), op.q))

@@ -64,3 +64,24 @@ def test_errors(arb12):
     ct = np.zeros((2, op.n + 1), dtype=np.uint64)
     with pytest.raises((capi.TfheError, ValueError)):
         ctx.CiphertextMulMatrix(ct, np.zeros((3, 3), dtype=np.int64), 1 << 35)  # rows != ciphertexts
+
+
+@pytest.mark.parametrize("mod", [(1 << 35), (1 << 63) + 29, (1 << 64) - 59])
+def test_extreme_entries(arb12, mod):
+    """INT64_MIN / INT64_MAX entries and u64-wide ciphertext words: operands are reduced
+    into [0, modulus) first, so the sum is exact even where K products of 2^127 would
+    overflow an unreduced 128-bit accumulator.  Per-term reduction is taken
+    when K (modulus-1)^2 >= 2^128 (the two large moduli)."""
+    op, ctx = arb12
+    rs = np.random.default_rng(10)
+    K, cols = 9, 4
+    ct = rs.integers(0, np.iinfo(np.uint64).max, (K, op.n + 1), dtype=np.uint64, endpoint=True)
+    ct[0, :] = np.iinfo(np.uint64).max
+    mat = rs.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, (K, cols), dtype=np.int64, endpoint=True)
+    mat[:, 0] = np.iinfo(np.int64).min
+    mat[:, 1] = np.iinfo(np.int64).max
+    out = ctx.CiphertextMulMatrix(ct, mat, mod)
+    for c in range(cols):
+        for w in (0, 1, op.n // 3, op.n):
+            want = sum(int(mat[k, c]) * int(ct[k, w]) for k in range(K)) % mod
+            assert int(out[c, w]) == want, (c, w)

@@ -230,6 +230,35 @@ def test_device_gate_entry_matches_host_entry(std128):
     assert np.array_equal(do.cpu().numpy().astype(np.uint64), ctx.EvalBinGate("NAND", c1, c2))
 
 
+def test_device_then_host_calls_without_sync(std128):
+    """Device-resident gates on two user streams, then a host-array gate, with no
+    synchronisation between the calls: all three share lane 0's scratch, which the
+    engine orders with an event, so every result equals its sequential run."""
+    import torch
+
+    ctx, cp = std128["ctx"], std128["cp"]
+    rs = np.random.default_rng(13)
+    B = 2048
+    c1, c2 = random_cts(rs, B, cp.n, cp.q), random_cts(rs, B, cp.n, cp.q)
+    h1, h2 = random_cts(rs, 7, cp.n, cp.q), random_cts(rs, 7, cp.n, cp.q)
+    want_dev = ctx.EvalBinGate("NAND", c1, c2)
+    want_dev2 = ctx.EvalBinGate("AND", c2, c1)
+    want_host = ctx.EvalBinGate("OR", h1, h2)
+    d1 = torch.from_numpy(c1.astype(np.int64)).cuda()
+    d2 = torch.from_numpy(c2.astype(np.int64)).cuda()
+    o1, o2 = torch.empty_like(d1), torch.empty_like(d1)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    ctx.EvalBinGateDevice("NAND", B, d1.data_ptr(), d2.data_ptr(), o1.data_ptr(), stream=s1.cuda_stream)
+    ctx.EvalBinGateDevice("AND", B, d2.data_ptr(), d1.data_ptr(), o2.data_ptr(), stream=s2.cuda_stream)
+    got_host = ctx.EvalBinGate("OR", h1, h2)
+    s1.synchronize()
+    s2.synchronize()
+    assert np.array_equal(got_host, want_host)
+    assert np.array_equal(o1.cpu().numpy().astype(np.uint64), want_dev)
+    assert np.array_equal(o2.cpu().numpy().astype(np.uint64), want_dev2)
+
+
 # ---------------------------------------------------------------- batch shapes and edge values
 @pytest.mark.parametrize("B", [1, 2, 3, 130])
 def test_gate_batch_sizes(std128, B):

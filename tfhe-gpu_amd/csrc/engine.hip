@@ -98,6 +98,7 @@ struct Scratch {
     uint64_t* a = nullptr;    // [cap][n]
     uint64_t* ext = nullptr;  // [cap][N+1]
     uint64_t* lwe[6] = {};    // [cap][n+1] each
+    void* ks = nullptr;       // tiled key switch: digit planes (ks_tiled_scratch_bytes)
     size_t cap = 0;
     uint64_t* io = nullptr;   // host-array staging: in1 | in2 | out
     size_t io_words = 0;
@@ -118,11 +119,36 @@ struct Device {
     Scratch sc2;
     void* pin[2] = {};               // pinned staging blocks for the host-array API
     hipEvent_t pin_ev[2] = {};       // last DMA that used each block
+    // Lane 0's scratch (sc) is shared by the host-array path (on `stream`) and the
+    // device-resident entry points (on the caller's stream): every user of sc waits on
+    // this event before its first kernel and records it after its last one, so work
+    // queued on different streams never overlaps on the same scratch.
+    hipEvent_t sc_fence = nullptr;
+};
+
+// hipMalloc'd buffer owned by one scope (error paths free it too)
+struct DevBuf {
+    void* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    template <typename T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
 };
 
 constexpr size_t kStageBytes = (size_t)8 << 20;
 
 }  // namespace
+
+struct tfhe_ctx;
+namespace {
+void free_device(Device& d);
+}
 
 struct tfhe_ctx {
     tfhe_params p{};
@@ -137,6 +163,7 @@ struct tfhe_ctx {
     std::vector<Device> devs;
     std::atomic<uint64_t> bootstraps{0};
     size_t max_chunk = 65536;  // the reference's max_bootstapping_num, bootstrapping.cuh:140
+    ~tfhe_ctx();  // frees every device's arena, scratch, streams (error paths included)
 };
 
 namespace {
@@ -286,6 +313,7 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
 void free_device(Device& d) {
     if (d.id < 0) return;
     hipSetDevice(d.id);
+    if (d.sc_fence) hipEventSynchronize(d.sc_fence), hipEventDestroy(d.sc_fence);
     if (d.stream) hipStreamSynchronize(d.stream);
     hipFree(d.arena);
     hipFree(d.bsk_fast);
@@ -296,6 +324,7 @@ void free_device(Device& d) {
         hipFree(sc->a);
         hipFree(sc->ext);
         for (auto* p : sc->lwe) hipFree(p);
+        hipFree(sc->ks);
         hipFree(sc->io);
     }
     for (int k = 0; k < 2; ++k) {
@@ -311,17 +340,30 @@ void free_device(Device& d) {
 tfhe_status create_streams(Device& d) {
     HCHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HCHECK(hipStreamCreateWithFlags(&d.stream2, hipStreamNonBlocking));
+    HCHECK(hipEventCreateWithFlags(&d.sc_fence, hipEventDisableTiming));
+    return TFHE_OK;
+}
+
+// Order `s` after every earlier user of lane 0's scratch (see Device::sc_fence).
+tfhe_status sc_acquire(Device& d, hipStream_t s) {
+    HCHECK(hipStreamWaitEvent(s, d.sc_fence, 0));
+    return TFHE_OK;
+}
+tfhe_status sc_release(Device& d, hipStream_t s) {
+    HCHECK(hipEventRecord(d.sc_fence, s));
     return TFHE_OK;
 }
 
 tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     if (B <= d.sc.cap) return TFHE_OK;
     const tfhe_params& p = c->p;
+    if (d.sc_fence) HCHECK(hipEventSynchronize(d.sc_fence));  // no queued kernel still uses the old buffers
     const size_t cap = std::max(B, std::min(c->max_chunk, (size_t)1024));
     hipFree(d.sc.acc);
     hipFree(d.sc.a);
     hipFree(d.sc.ext);
     for (auto*& q : d.sc.lwe) hipFree(q), q = nullptr;
+    hipFree(d.sc.ks);
     uint64_t* io = d.sc.io;
     const size_t io_words = d.sc.io_words;
     d.sc = Scratch{};
@@ -330,6 +372,7 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     HCHECK(hipMalloc(&d.sc.a, cap * p.n * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.ext, cap * (p.N + 1) * sizeof(uint64_t)));
     for (auto*& q : d.sc.lwe) HCHECK(hipMalloc(&q, cap * (p.n + 1) * sizeof(uint64_t)));
+    if (ks_tiled_supported(c->ks)) HCHECK(hipMalloc(&d.sc.ks, ks_tiled_scratch_bytes(c->ks, cap)));
     d.sc.cap = cap;
     return TFHE_OK;
 }
@@ -361,8 +404,25 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     return TFHE_OK;
 }
 
+// Smallest batch that takes the tiled key switch (TFHE_KS_TILED_MIN; 0 = never).  Below it
+// the per-ciphertext gather (k_mkm, split over several waves) has the better latency.
+size_t ks_tiled_min() {
+    const char* e = std::getenv("TFHE_KS_TILED_MIN");  // read per call: tests and A/B runs switch it
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256;
+}
+
+// d.sc.ks must be sized for B (ensure_scratch) when the tiled form can run
 tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
     if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
+    const size_t tmin = ks_tiled_min();
+    if (tmin && B >= tmin && d.sc.ks && B <= d.sc.cap) {
+        const hipError_t e = launch_ks_tiled(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb,
+                                             ext, fmod, out, B, d.sc.ks, d.stream);
+        if (e != hipErrorNotSupported) {
+            HCHECK(e);
+            return TFHE_OK;
+        }
+    }
     HCHECK(launch_mkm(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb, ext, fmod, out, B,
                       d.stream));
     return TFHE_OK;
@@ -627,6 +687,7 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
         }
         d.sc = lane[0].sc;  // keep what was (re)allocated
         d.sc2 = lane[1].sc;
+        if (st == TFHE_OK) st = sc_acquire(d, d.stream);
         if (st != TFHE_OK) return st;
         auto d2h = [&](int l, size_t off, size_t b) -> tfhe_status {
             const uint64_t* dout = lane[l].sc.io + sub * (w1 + w_in2);
@@ -694,6 +755,26 @@ tfhe_status create_ctx(const tfhe_params* p, int num_gpus, std::unique_ptr<tfhe_
 
 }  // namespace
 
+tfhe_ctx::~tfhe_ctx() {
+    for (auto& d : devs) free_device(d);
+}
+
+namespace {
+// Every extern "C" body runs under this: no C++ exception crosses the C-ABI.
+template <typename F>
+tfhe_status guarded(F&& body) {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return fail(TFHE_ERR_OUT_OF_MEMORY, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(TFHE_ERR_INTERNAL, std::string("internal error: ") + e.what());
+    } catch (...) {
+        return fail(TFHE_ERR_INTERNAL, "internal error");
+    }
+}
+}  // namespace
+
 // ===========================================================================
 // extern "C" entry points
 // ===========================================================================
@@ -722,25 +803,31 @@ const char* tfhe_status_string(tfhe_status s) {
 }
 
 tfhe_status tfhe_params_from_set(int paramset, tfhe_params* out) {
-    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
-    tfhe_status s = params_from_set(paramset, out);
-    if (s != TFHE_OK) return fail(s, "unknown parameter set");
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+        tfhe_status s = params_from_set(paramset, out);
+        if (s != TFHE_OK) return fail(s, "unknown parameter set");
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_params_from_logq(int paramset, int arb_func, uint32_t logQ, int64_t N, uint32_t baseG,
                                   uint32_t num_digits_to_throw, tfhe_params* out) {
-    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
-    tfhe_status s = params_from_logq(paramset, arb_func, logQ, N, baseG, num_digits_to_throw, out);
-    if (s != TFHE_OK) return fail(s, "unsupported logQ parameter request (STD128/TOY, 11 <= logQ <= 29)");
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+        tfhe_status s = params_from_logq(paramset, arb_func, logQ, N, baseG, num_digits_to_throw, out);
+        if (s != TFHE_OK) return fail(s, "unsupported logQ parameter request (STD128/TOY, 11 <= logQ <= 29)");
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_params_finish(tfhe_params* p) {
-    if (!p) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
-    std::string err;
-    tfhe_status s = params_finish(p, &err);
-    return s == TFHE_OK ? s : fail(s, err);
+    return guarded([&]() -> tfhe_status {
+        if (!p) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
+        std::string err;
+        tfhe_status s = params_finish(p, &err);
+        return s == TFHE_OK ? s : fail(s, err);
+    });
 }
 
 namespace {
@@ -773,30 +860,36 @@ tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* b
 
 tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
                        int num_gpus) {
-    return setup_common(out, p, bsk_coeff, false, ksk, num_gpus);
+    return guarded([&]() -> tfhe_status {
+        return setup_common(out, p, bsk_coeff, false, ksk, num_gpus);
+    });
 }
 
 tfhe_status tfhe_setup_eval(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_eval, const uint64_t* ksk,
                             int num_gpus) {
-    return setup_common(out, p, bsk_eval, true, ksk, num_gpus);
+    return guarded([&]() -> tfhe_status {
+        return setup_common(out, p, bsk_eval, true, ksk, num_gpus);
+    });
 }
 
 tfhe_status tfhe_setup_from_key_image(tfhe_ctx** out, const tfhe_params* p, const void* d_src, size_t bytes,
                                       int device) {
-    if (!out || !d_src) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    *out = nullptr;
-    std::unique_ptr<tfhe_ctx> c;
-    SCHECK(create_ctx(p, 1, c));
-    if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
-    Device& d = c->devs[0];
-    d.id = device;
-    HCHECK(hipSetDevice(device));
-    SCHECK(create_streams(d));
-    HCHECK(hipMalloc(&d.arena, bytes));
-    HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
-    SCHECK(finish_device(c.get(), d));
-    *out = c.release();
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        if (!out || !d_src) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        *out = nullptr;
+        std::unique_ptr<tfhe_ctx> c;
+        SCHECK(create_ctx(p, 1, c));
+        if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+        Device& d = c->devs[0];
+        d.id = device;
+        HCHECK(hipSetDevice(device));
+        SCHECK(create_streams(d));
+        HCHECK(hipMalloc(&d.arena, bytes));
+        HCHECK(hipMemcpy(d.arena, d_src, bytes, hipMemcpyDeviceToDevice));
+        SCHECK(finish_device(c.get(), d));
+        *out = c.release();
+        return TFHE_OK;
+    });
 }
 
 namespace {
@@ -816,378 +909,427 @@ uint64_t fnv1a64(const unsigned char* p, size_t n) {
 }  // namespace
 
 tfhe_status tfhe_save_key_image(tfhe_ctx* c, const char* path) {
-    SCHECK(check_ctx(c));
-    if (!path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null path");
-    std::vector<unsigned char> img(c->layout.total);
-    HCHECK(hipSetDevice(c->devs[0].id));
-    HCHECK(hipStreamSynchronize(c->devs[0].stream));
-    HCHECK(hipMemcpy(img.data(), c->devs[0].arena, img.size(), hipMemcpyDeviceToHost));
-    KeyFileHeader hdr{};
-    std::memcpy(hdr.magic, "TFHEKIMG", 8);
-    hdr.abi = (uint32_t)tfhe_abi_version();
-    hdr.params = c->p;
-    hdr.bytes = img.size();
-    hdr.fnv = fnv1a64(img.data(), img.size());
-    FILE* f = std::fopen(path, "wb");
-    if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
-    const bool ok = std::fwrite(&hdr, sizeof(hdr), 1, f) == 1 && std::fwrite(img.data(), 1, img.size(), f) == img.size();
-    if (std::fclose(f) != 0 || !ok) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("write failed: ") + path);
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (!path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null path");
+        std::vector<unsigned char> img(c->layout.total);
+        HCHECK(hipSetDevice(c->devs[0].id));
+        HCHECK(hipStreamSynchronize(c->devs[0].stream));
+        HCHECK(hipMemcpy(img.data(), c->devs[0].arena, img.size(), hipMemcpyDeviceToHost));
+        KeyFileHeader hdr{};
+        std::memcpy(hdr.magic, "TFHEKIMG", 8);
+        hdr.abi = (uint32_t)tfhe_abi_version();
+        hdr.params = c->p;
+        hdr.bytes = img.size();
+        hdr.fnv = fnv1a64(img.data(), img.size());
+        FILE* f = std::fopen(path, "wb");
+        if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
+        const bool ok = std::fwrite(&hdr, sizeof(hdr), 1, f) == 1 && std::fwrite(img.data(), 1, img.size(), f) == img.size();
+        if (std::fclose(f) != 0 || !ok) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("write failed: ") + path);
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_setup_from_key_file(tfhe_ctx** out, const tfhe_params* p, const char* path, int device) {
-    if (!out || !p || !path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    *out = nullptr;
-    tfhe_params want = *p;
-    std::string err;
-    if (params_finish(&want, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
-    KeyFileHeader hdr{};
-    std::vector<unsigned char> img;
-    tfhe_status st = TFHE_OK;
-    if (std::fread(&hdr, sizeof(hdr), 1, f) != 1 || std::memcmp(hdr.magic, "TFHEKIMG", 8) != 0)
-        st = fail(TFHE_ERR_INVALID_ARGUMENT, "not a key image file");
-    else if (hdr.abi != (uint32_t)tfhe_abi_version())
-        st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image written by another ABI version");
-    else if (std::memcmp(&hdr.params, &want, sizeof(want)) != 0)
-        st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image parameters differ from the requested ones");
-    else {
-        img.resize(hdr.bytes);
-        if (std::fread(img.data(), 1, img.size(), f) != img.size())
-            st = fail(TFHE_ERR_INVALID_ARGUMENT, "truncated key image file");
-        else if (fnv1a64(img.data(), img.size()) != hdr.fnv)
-            st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image checksum mismatch");
-    }
-    std::fclose(f);
-    if (st != TFHE_OK) return st;
-    std::unique_ptr<tfhe_ctx> c;
-    SCHECK(create_ctx(&want, 1, c));
-    if (img.size() != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
-    Device& d = c->devs[0];
-    d.id = device;
-    HCHECK(hipSetDevice(device));
-    SCHECK(create_streams(d));
-    HCHECK(hipMalloc(&d.arena, img.size()));
-    HCHECK(hipMemcpy(d.arena, img.data(), img.size(), hipMemcpyHostToDevice));
-    SCHECK(finish_device(c.get(), d));
-    *out = c.release();
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        if (!out || !p || !path) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        *out = nullptr;
+        tfhe_params want = *p;
+        std::string err;
+        if (params_finish(&want, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
+        FILE* f = std::fopen(path, "rb");
+        if (!f) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("cannot open ") + path);
+        KeyFileHeader hdr{};
+        std::vector<unsigned char> img;
+        tfhe_status st = TFHE_OK;
+        if (std::fread(&hdr, sizeof(hdr), 1, f) != 1 || std::memcmp(hdr.magic, "TFHEKIMG", 8) != 0)
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "not a key image file");
+        else if (hdr.abi != (uint32_t)tfhe_abi_version())
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image written by another ABI version");
+        else if (std::memcmp(&hdr.params, &want, sizeof(want)) != 0)
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image parameters differ from the requested ones");
+        else if (hdr.bytes != arena_layout(want, word_bits_for(want)).total)  // before any allocation
+            st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image size field does not match the parameters");
+        else {
+            img.resize(hdr.bytes);
+            if (std::fread(img.data(), 1, img.size(), f) != img.size())
+                st = fail(TFHE_ERR_INVALID_ARGUMENT, "truncated key image file");
+            else if (fnv1a64(img.data(), img.size()) != hdr.fnv)
+                st = fail(TFHE_ERR_INVALID_ARGUMENT, "key image checksum mismatch");
+        }
+        std::fclose(f);
+        if (st != TFHE_OK) return st;
+        std::unique_ptr<tfhe_ctx> c;
+        SCHECK(create_ctx(&want, 1, c));
+        if (img.size() != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+        Device& d = c->devs[0];
+        d.id = device;
+        HCHECK(hipSetDevice(device));
+        SCHECK(create_streams(d));
+        HCHECK(hipMalloc(&d.arena, img.size()));
+        HCHECK(hipMemcpy(d.arena, img.data(), img.size(), hipMemcpyHostToDevice));
+        SCHECK(finish_device(c.get(), d));
+        *out = c.release();
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_export_key_image(tfhe_ctx* c, void* d_dst, size_t bytes, void* stream) {
-    SCHECK(check_ctx(c));
-    if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
-    HCHECK(hipSetDevice(c->devs[0].id));
-    hipStream_t s = stream ? (hipStream_t)stream : c->devs[0].stream;
-    HCHECK(hipMemcpyAsync(d_dst, c->devs[0].arena, bytes, hipMemcpyDeviceToDevice, s));
-    HCHECK(hipStreamSynchronize(s));
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (bytes != c->layout.total) return fail(TFHE_ERR_INVALID_ARGUMENT, "key image size mismatch");
+        HCHECK(hipSetDevice(c->devs[0].id));
+        hipStream_t s = stream ? (hipStream_t)stream : c->devs[0].stream;
+        HCHECK(hipMemcpyAsync(d_dst, c->devs[0].arena, bytes, hipMemcpyDeviceToDevice, s));
+        HCHECK(hipStreamSynchronize(s));
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_clean(tfhe_ctx* c) {
-    if (!c) return TFHE_OK;
-    for (auto& d : c->devs) free_device(d);
-    delete c;
+    delete c;  // ~tfhe_ctx frees every device
     return TFHE_OK;
 }
 
 tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
-    SCHECK(check_ctx(c));
-    if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
-    out->num_devices = (int)c->devs.size();
-    out->word_bits = c->word_bits;
-    out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0) +
-                            (c->use_f64 ? bsk_f64_bytes(c->br) : 0);
-    out->ksk_device_bytes = c->layout.total - c->layout.ksk;
-    out->bootstraps = c->bootstraps.load();
-    out->key_image_bytes = c->layout.total;
-    out->br_kernel = c->use_fast ? TFHE_BR_FAST : c->use_f64 ? (c->f64_fold ? TFHE_BR_F64_FOLD : TFHE_BR_F64) : TFHE_BR_GENERIC;
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+        out->num_devices = (int)c->devs.size();
+        out->word_bits = c->word_bits;
+        out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0) +
+                                (c->use_f64 ? bsk_f64_bytes(c->br) : 0);
+        out->ksk_device_bytes = c->layout.total - c->layout.ksk;
+        out->bootstraps = c->bootstraps.load();
+        out->key_image_bytes = c->layout.total;
+        out->br_kernel = c->use_fast ? TFHE_BR_FAST : c->use_f64 ? (c->f64_fold ? TFHE_BR_F64_FOLD : TFHE_BR_F64) : TFHE_BR_GENERIC;
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_mod, uint64_t* acc) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return TFHE_OK;
-    if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const tfhe_params& p = c->p;
-    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        const size_t chunk = std::min(cnt, c->max_chunk);
-        SCHECK(ensure_scratch(c, d, chunk));
-        for (size_t off = lo; off < lo + cnt; off += chunk) {
-            const size_t b = std::min(chunk, lo + cnt - off);
-            HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
-            HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * 2 * p.N, b * 2 * p.N * 8, hipMemcpyHostToDevice, d.stream));
-            SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
-            HCHECK(hipMemcpyAsync(acc + off * 2 * p.N, d.sc.acc, b * 2 * p.N * 8, hipMemcpyDeviceToHost, d.stream));
-            HCHECK(hipStreamSynchronize(d.stream));
-        }
-        return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const tfhe_params& p = c->p;
+        return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+            const size_t chunk = std::min(cnt, c->max_chunk);
+            SCHECK(ensure_scratch(c, d, chunk));
+            SCHECK(sc_acquire(d, d.stream));
+            for (size_t off = lo; off < lo + cnt; off += chunk) {
+                const size_t b = std::min(chunk, lo + cnt - off);
+                HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
+                HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * 2 * p.N, b * 2 * p.N * 8, hipMemcpyHostToDevice, d.stream));
+                SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
+                HCHECK(hipMemcpyAsync(acc + off * 2 * p.N, d.sc.acc, b * 2 * p.N * 8, hipMemcpyDeviceToHost, d.stream));
+                HCHECK(hipStreamSynchronize(d.stream));
+            }
+            return TFHE_OK;
+        });
     });
 }
 
 tfhe_status tfhe_eval_acc_device(tfhe_ctx* c, size_t B, const uint64_t* d_a, uint64_t a_mod, uint64_t* d_acc,
                                  void* stream) {
-    SCHECK(check_ctx(c));
-    Device& d = c->devs[0];
-    HCHECK(hipSetDevice(d.id));
-    hipStream_t saved = d.stream;
-    if (stream) d.stream = (hipStream_t)stream;
-    tfhe_status st = dev_blind_rotate(c, d, d_a, a_mod, d_acc, B);
-    d.stream = saved;
-    return st;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        Device& d = c->devs[0];
+        HCHECK(hipSetDevice(d.id));
+        hipStream_t saved = d.stream;
+        if (stream) d.stream = (hipStream_t)stream;
+        tfhe_status st = dev_blind_rotate(c, d, d_a, a_mod, d_acc, B);
+        d.stream = saved;
+        return st;
+    });
 }
 
 tfhe_status tfhe_mkm_switch(tfhe_ctx* c, size_t B, const uint64_t* ct_ext, uint64_t fmod, uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return TFHE_OK;
-    if (!ct_ext || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const tfhe_params& p = c->p;
-    return run_lwe_batch(c, B, ct_ext, p.N + 1, nullptr, 0, out, p.n + 1,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
-                             return dev_mkm(c, d, i1, fmod, o, b);
-                         });
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!ct_ext || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const tfhe_params& p = c->p;
+        return run_lwe_batch(c, B, ct_ext, p.N + 1, nullptr, 0, out, p.n + 1,
+                             [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
+                                 return dev_mkm(c, d, i1, fmod, o, b);
+                             });
+    });
 }
 
 tfhe_status tfhe_mkm_switch_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct_ext, uint64_t fmod, uint64_t* d_out,
                                    void* stream) {
-    SCHECK(check_ctx(c));
-    Device& d = c->devs[0];
-    HCHECK(hipSetDevice(d.id));
-    hipStream_t saved = d.stream;
-    if (stream) d.stream = (hipStream_t)stream;
-    tfhe_status st = dev_mkm(c, d, d_ct_ext, fmod, d_out, B);
-    d.stream = saved;
-    return st;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!d_ct_ext || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        Device& d = c->devs[0];
+        HCHECK(hipSetDevice(d.id));
+        SCHECK(ensure_scratch(c, d, B));  // the tiled key switch's digit planes
+        hipStream_t saved = d.stream;
+        if (stream) d.stream = (hipStream_t)stream;
+        tfhe_status st = sc_acquire(d, d.stream);
+        if (st == TFHE_OK) st = dev_mkm(c, d, d_ct_ext, fmod, d_out, B);
+        const tfhe_status rel = sc_release(d, d.stream);
+        d.stream = saved;
+        return st != TFHE_OK ? st : rel;
+    });
 }
 
 tfhe_status tfhe_eval_bin_gate(tfhe_ctx* c, int gate, size_t B, const uint64_t* ct1, const uint64_t* ct2, uint64_t q,
                                uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalBinGate: input vector is empty");
-    if (!ct1 || !ct2 || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    if (ct1 == ct2) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts should be independant");
-    if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
-    const size_t w = c->p.n + 1;
-    return run_lwe_batch(c, B, ct1, w, ct2, w, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
-                             return dev_gate(c, d, gate, i1, i2, q, o, b);
-                         });
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalBinGate: input vector is empty");
+        if (!ct1 || !ct2 || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        if (ct1 == ct2) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts should be independant");
+        if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
+        const size_t w = c->p.n + 1;
+        return run_lwe_batch(c, B, ct1, w, ct2, w, out, w,
+                             [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
+                                 return dev_gate(c, d, gate, i1, i2, q, o, b);
+                             });
+    });
 }
 
 tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* c, int gate, size_t B, const uint64_t* d_ct1, const uint64_t* d_ct2,
                                       uint64_t q, uint64_t* d_out, void* stream) {
-    SCHECK(check_ctx(c));
-    if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
-    Device& d = c->devs[0];
-    HCHECK(hipSetDevice(d.id));
-    SCHECK(ensure_scratch(c, d, B));
-    hipStream_t saved = d.stream;
-    if (stream) d.stream = (hipStream_t)stream;
-    tfhe_status st = dev_gate(c, d, gate, d_ct1, d_ct2, q, d_out, B);
-    d.stream = saved;
-    return st;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
+        if (B == 0) return TFHE_OK;
+        if (!d_ct1 || !d_ct2 || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        Device& d = c->devs[0];
+        HCHECK(hipSetDevice(d.id));
+        SCHECK(ensure_scratch(c, d, B));
+        hipStream_t saved = d.stream;
+        if (stream) d.stream = (hipStream_t)stream;
+        tfhe_status st = sc_acquire(d, d.stream);
+        if (st == TFHE_OK) st = dev_gate(c, d, gate, d_ct1, d_ct2, q, d_out, B);
+        const tfhe_status rel = sc_release(d, d.stream);  // even after a failed launch: later users wait on it
+        d.stream = saved;
+        return st != TFHE_OK ? st : rel;
+    });
 }
 
 tfhe_status tfhe_eval_func(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t q, const uint64_t* lut, int per_ct_lut,
                            uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFunc: input vector is empty");
-    if (!ct || !lut || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    if (q < 4 || (2ull * c->p.N) % q) return fail(TFHE_ERR_INVALID_ARGUMENT, "q must divide 2N");
-    // LUT classification uses the first LUT, as the reference (binfhe-base-scheme.cpp:697-698, 815-816)
-    const int prop = check_input_function(lut, q, q);
-    const size_t w = c->p.n + 1;
-    const uint64_t stride = per_ct_lut ? q : 0;
-    // LUTs go to every device once (all of them when per ciphertext), then the batch runs
-    // through the pipelined host-array runner
-    const size_t D = c->devs.size();
-    std::vector<uint64_t*> d_lut(D, nullptr);
-    const size_t lut_words = per_ct_lut ? B * q : q;
-    tfhe_status st = TFHE_OK;
-    for (size_t g = 0; g < D && st == TFHE_OK; ++g) {
-        if (hipSetDevice(c->devs[g].id) != hipSuccess || hipMalloc(&d_lut[g], lut_words * 8) != hipSuccess ||
-            hipMemcpy(d_lut[g], lut, lut_words * 8, hipMemcpyHostToDevice) != hipSuccess)
-            st = fail(TFHE_ERR_OUT_OF_MEMORY, "LUT upload failed");
-    }
-    if (st == TFHE_OK)
-        st = run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
-                           [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t off) {
-                               size_t g = 0;
-                               while (c->devs[g].id != d.id) ++g;
-                               return dev_func(c, d, prop, i1, q, d_lut[g] + (per_ct_lut ? off * q : 0), stride, o, b);
-                           });
-    for (size_t g = 0; g < D; ++g)
-        if (d_lut[g]) hipSetDevice(c->devs[g].id), hipFree(d_lut[g]);
-    return st;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFunc: input vector is empty");
+        if (!ct || !lut || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        if (q < 4 || (2ull * c->p.N) % q) return fail(TFHE_ERR_INVALID_ARGUMENT, "q must divide 2N");
+        // LUT classification uses the first LUT, as the reference (binfhe-base-scheme.cpp:697-698, 815-816)
+        const int prop = check_input_function(lut, q, q);
+        const size_t w = c->p.n + 1;
+        const uint64_t stride = per_ct_lut ? q : 0;
+        // LUTs go to every device once (all of them when per ciphertext), then the batch runs
+        // through the pipelined host-array runner
+        const size_t D = c->devs.size();
+        std::vector<uint64_t*> d_lut(D, nullptr);
+        const size_t lut_words = per_ct_lut ? B * q : q;
+        tfhe_status st = TFHE_OK;
+        for (size_t g = 0; g < D && st == TFHE_OK; ++g) {
+            if (hipSetDevice(c->devs[g].id) != hipSuccess || hipMalloc(&d_lut[g], lut_words * 8) != hipSuccess ||
+                hipMemcpy(d_lut[g], lut, lut_words * 8, hipMemcpyHostToDevice) != hipSuccess)
+                st = fail(TFHE_ERR_OUT_OF_MEMORY, "LUT upload failed");
+        }
+        if (st == TFHE_OK)
+            st = run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                               [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t off) {
+                                   size_t g = 0;
+                                   while (c->devs[g].id != d.id) ++g;
+                                   return dev_func(c, d, prop, i1, q, d_lut[g] + (per_ct_lut ? off * q : 0), stride, o, b);
+                               });
+        for (size_t g = 0; g < D; ++g)
+            if (d_lut[g]) hipSetDevice(c->devs[g].id), hipFree(d_lut[g]);
+        return st;
+    });
 }
 
 tfhe_status tfhe_eval_floor(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint32_t roundbits,
                             uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFloor: input vector is empty");
-    if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const size_t w = c->p.n + 1;
-    return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
-                             return dev_floor(c, d, i1, mod, roundbits, o, b);
-                         });
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalFloor: input vector is empty");
+        if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const size_t w = c->p.n + 1;
+        return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                             [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
+                                 return dev_floor(c, d, i1, mod, roundbits, o, b);
+                             });
+    });
 }
 
 tfhe_status tfhe_eval_sign(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalSign: input vector is empty");
-    if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const size_t w = c->p.n + 1;
-    return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
-                         [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
-                             return dev_sign(c, d, i1, mod, o, b);
-                         });
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalSign: input vector is empty");
+        if (!ct || !out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const size_t w = c->p.n + 1;
+        return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
+                             [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
+                                 return dev_sign(c, d, i1, mod, o, b);
+                             });
+    });
 }
 
 tfhe_status tfhe_eval_decomp(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t mod, uint32_t max_digits,
                              uint64_t* out, uint64_t* moduli, uint32_t* num_digits) {
-    SCHECK(check_ctx(c));
-    if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalDecomp: input vector is empty");
-    if (!ct || !out || !moduli || !num_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const uint64_t q = c->p.q, beta = 128;
-    if (mod <= q) return fail(TFHE_ERR_UNSUPPORTED, "EvalDecomp is only for large precision");
-    // digit count and moduli are data independent (binfhe-base-scheme.cpp:1066-1080)
-    std::vector<uint64_t> mods;
-    for (uint64_t m = mod; m > q; m = m / q * 2 * beta) mods.push_back(q);
-    {
-        uint64_t m = mod;
-        while (m > q) m = m / q * 2 * beta;
-        mods.push_back(m);
-    }
-    if (mods.size() > max_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "max_digits too small");
-    for (size_t i = 0; i < mods.size(); ++i) moduli[i] = mods[i];
-    *num_digits = (uint32_t)mods.size();
-    const uint32_t n = c->p.n;
-    const size_t w = n + 1;
-    return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        const size_t chunk = std::min(cnt, c->max_chunk);
-        SCHECK(ensure_scratch(c, d, chunk));
-        uint64_t *tmp = nullptr, *fl = nullptr, *dig = nullptr;
-        HCHECK(hipMalloc(&tmp, chunk * w * 8));
-        HCHECK(hipMalloc(&fl, chunk * w * 8));
-        HCHECK(hipMalloc(&dig, chunk * w * 8));
-        std::vector<uint64_t> host_digit(chunk * w);
-        tfhe_status st = TFHE_OK;
-        for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
-            const size_t b = std::min(chunk, lo + cnt - off);
-            HCHECK(hipMemcpyAsync(tmp, ct + off * w, b * w * 8, hipMemcpyHostToDevice, d.stream));
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "EvalDecomp: input vector is empty");
+        if (!ct || !out || !moduli || !num_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const uint64_t q = c->p.q, beta = 128;
+        if (mod <= q) return fail(TFHE_ERR_UNSUPPORTED, "EvalDecomp is only for large precision");
+        // digit count and moduli are data independent (binfhe-base-scheme.cpp:1066-1080)
+        std::vector<uint64_t> mods;
+        for (uint64_t m = mod; m > q; m = m / q * 2 * beta) mods.push_back(q);
+        {
             uint64_t m = mod;
-            for (size_t k = 0; k < mods.size() && st == TFHE_OK; ++k) {
-                if (k + 1 < mods.size()) HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, tmp, nullptr, dig, b, d.stream));
-                else HCHECK(hipMemcpyAsync(dig, tmp, b * w * 8, hipMemcpyDeviceToDevice, d.stream));
-                HCHECK(hipMemcpyAsync(host_digit.data(), dig, b * w * 8, hipMemcpyDeviceToHost, d.stream));
-                HCHECK(hipStreamSynchronize(d.stream));
-                for (size_t s = 0; s < b; ++s)
-                    std::memcpy(out + ((off + s) * max_digits + k) * w, host_digit.data() + s * w, w * 8);
-                if (k + 1 < mods.size()) {
-                    st = dev_floor(c, d, tmp, m, 0, fl, b);
-                    const uint64_t nm = m / q * 2 * beta;
-                    HCHECK(launch_lwe_op(LWE_MODSWITCH, n, nm, m, fl, nullptr, tmp, b, d.stream));
-                    m = nm;
+            while (m > q) m = m / q * 2 * beta;
+            mods.push_back(m);
+        }
+        if (mods.size() > max_digits) return fail(TFHE_ERR_INVALID_ARGUMENT, "max_digits too small");
+        for (size_t i = 0; i < mods.size(); ++i) moduli[i] = mods[i];
+        *num_digits = (uint32_t)mods.size();
+        const uint32_t n = c->p.n;
+        const size_t w = n + 1;
+        return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+            const size_t chunk = std::min(cnt, c->max_chunk);
+            SCHECK(ensure_scratch(c, d, chunk));
+            SCHECK(sc_acquire(d, d.stream));
+            DevBuf tmp_b, fl_b, dig_b;
+            HCHECK(hipMalloc(&tmp_b.p, chunk * w * 8));
+            HCHECK(hipMalloc(&fl_b.p, chunk * w * 8));
+            HCHECK(hipMalloc(&dig_b.p, chunk * w * 8));
+            uint64_t *tmp = tmp_b.as<uint64_t>(), *fl = fl_b.as<uint64_t>(), *dig = dig_b.as<uint64_t>();
+            std::vector<uint64_t> host_digit(chunk * w);
+            tfhe_status st = TFHE_OK;
+            // every exit below leaves the stream drained before the DevBufs free their memory
+            struct Drain {
+                hipStream_t s;
+                ~Drain() { hipStreamSynchronize(s); }
+            } drain{d.stream};
+            for (size_t off = lo; off < lo + cnt && st == TFHE_OK; off += chunk) {
+                const size_t b = std::min(chunk, lo + cnt - off);
+                HCHECK(hipMemcpyAsync(tmp, ct + off * w, b * w * 8, hipMemcpyHostToDevice, d.stream));
+                uint64_t m = mod;
+                for (size_t k = 0; k < mods.size() && st == TFHE_OK; ++k) {
+                    if (k + 1 < mods.size()) HCHECK(launch_lwe_op(LWE_SET_MOD, n, q, 0, tmp, nullptr, dig, b, d.stream));
+                    else HCHECK(hipMemcpyAsync(dig, tmp, b * w * 8, hipMemcpyDeviceToDevice, d.stream));
+                    HCHECK(hipMemcpyAsync(host_digit.data(), dig, b * w * 8, hipMemcpyDeviceToHost, d.stream));
+                    HCHECK(hipStreamSynchronize(d.stream));
+                    for (size_t s = 0; s < b; ++s)
+                        std::memcpy(out + ((off + s) * max_digits + k) * w, host_digit.data() + s * w, w * 8);
+                    if (k + 1 < mods.size()) {
+                        st = dev_floor(c, d, tmp, m, 0, fl, b);
+                        if (st != TFHE_OK) break;
+                        const uint64_t nm = m / q * 2 * beta;
+                        HCHECK(launch_lwe_op(LWE_MODSWITCH, n, nm, m, fl, nullptr, tmp, b, d.stream));
+                        m = nm;
+                    }
                 }
             }
-        }
-        hipStreamSynchronize(d.stream);
-        hipFree(tmp);
-        hipFree(fl);
-        hipFree(dig);
-        return st;
+            return st;
+        });
     });
 }
 
 tfhe_status tfhe_ciphertext_mul_matrix(tfhe_ctx* c, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
                                        uint64_t modulus, uint64_t* out) {
-    SCHECK(check_ctx(c));
-    if (K == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts are empty.");
-    if (cols == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input matrix is empty.");
-    if (!ct || !matrix || !out || modulus == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-    const uint32_t w = c->p.n + 1;
-    Device& d = c->devs[0];
-    HCHECK(hipSetDevice(d.id));
-    uint64_t *dct = nullptr, *dout = nullptr;
-    int64_t* dm = nullptr;
-    HCHECK(hipMalloc(&dct, K * w * 8));
-    HCHECK(hipMalloc(&dm, K * cols * 8));
-    HCHECK(hipMalloc(&dout, cols * w * 8));
-    HCHECK(hipMemcpyAsync(dct, ct, K * w * 8, hipMemcpyHostToDevice, d.stream));
-    HCHECK(hipMemcpyAsync(dm, matrix, K * cols * 8, hipMemcpyHostToDevice, d.stream));
-    HCHECK(launch_ct_mul_matrix(w, K, dct, cols, dm, modulus, dout, d.stream));
-    HCHECK(hipMemcpyAsync(out, dout, cols * w * 8, hipMemcpyDeviceToHost, d.stream));
-    HCHECK(hipStreamSynchronize(d.stream));
-    hipFree(dct);
-    hipFree(dm);
-    hipFree(dout);
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (K == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input ciphertexts are empty.");
+        if (cols == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "Input matrix is empty.");
+        if (!ct || !matrix || !out || modulus == 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const uint32_t w = c->p.n + 1;
+        Device& d = c->devs[0];
+        HCHECK(hipSetDevice(d.id));
+        DevBuf dct, dm, dout;
+        HCHECK(hipMalloc(&dct.p, K * w * 8));
+        HCHECK(hipMalloc(&dm.p, K * cols * 8));
+        HCHECK(hipMalloc(&dout.p, cols * w * 8));
+        struct Drain {
+            hipStream_t s;
+            ~Drain() { hipStreamSynchronize(s); }
+        } drain{d.stream};
+        HCHECK(hipMemcpyAsync(dct.p, ct, K * w * 8, hipMemcpyHostToDevice, d.stream));
+        HCHECK(hipMemcpyAsync(dm.p, matrix, K * cols * 8, hipMemcpyHostToDevice, d.stream));
+        HCHECK(launch_ct_mul_matrix(w, K, dct.as<uint64_t>(), cols, dm.as<int64_t>(), modulus, dout.as<uint64_t>(),
+                                    d.stream));
+        HCHECK(hipMemcpyAsync(out, dout.p, cols * w * 8, hipMemcpyDeviceToHost, d.stream));
+        HCHECK(hipStreamSynchronize(d.stream));
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_lwe_gpu_setup(int num_gpus) {
-    int count = 0;
-    HCHECK(hipGetDeviceCount(&count));
-    if (num_gpus > count) return fail(TFHE_ERR_INVALID_ARGUMENT, "not enough GPUs");
-    return TFHE_OK;
+    return guarded([&]() -> tfhe_status {
+        int count = 0;
+        HCHECK(hipGetDeviceCount(&count));
+        if (num_gpus > count) return fail(TFHE_ERR_INVALID_ARGUMENT, "not enough GPUs");
+        return TFHE_OK;
+    });
 }
 
 tfhe_status tfhe_lwe_gpu_clean(void) { return TFHE_OK; }
 
 tfhe_status tfhe_host_selftest(const tfhe_params* pin) {
-    if (!pin) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
-    tfhe_params p = *pin;
-    std::string err;
-    if (params_finish(&p, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
-    NttTables t = make_ntt_tables(p.Q, p.N);
-    // (1) forward/inverse round trip and (2) product vs schoolbook on a pseudo-random pair
-    std::vector<uint64_t> a(p.N), b(p.N), ref(p.N, 0);
-    uint64_t s = 0x1234567;
-    for (uint32_t i = 0; i < p.N; ++i) {
-        s = s * 6364136223846793005ull + 1442695040888963407ull;
-        a[i] = (s >> 7) % p.Q;
-        s = s * 6364136223846793005ull + 1442695040888963407ull;
-        b[i] = (s >> 7) % p.Q;
-    }
-    for (uint32_t i = 0; i < p.N; ++i)
-        for (uint32_t j = 0; j < p.N; ++j) {
-            uint64_t v = mulmod(a[i], b[j], p.Q);
-            if (i + j < p.N) ref[i + j] = addmod(ref[i + j], v, p.Q);
-            else ref[i + j - p.N] = submod(ref[i + j - p.N], v, p.Q);
+    return guarded([&]() -> tfhe_status {
+        if (!pin) return fail(TFHE_ERR_INVALID_ARGUMENT, "null params");
+        tfhe_params p = *pin;
+        std::string err;
+        if (params_finish(&p, &err) != TFHE_OK) return fail(TFHE_ERR_INVALID_ARGUMENT, err);
+        NttTables t = make_ntt_tables(p.Q, p.N);
+        // (1) forward/inverse round trip and (2) product vs schoolbook on a pseudo-random pair
+        std::vector<uint64_t> a(p.N), b(p.N), ref(p.N, 0);
+        uint64_t s = 0x1234567;
+        for (uint32_t i = 0; i < p.N; ++i) {
+            s = s * 6364136223846793005ull + 1442695040888963407ull;
+            a[i] = (s >> 7) % p.Q;
+            s = s * 6364136223846793005ull + 1442695040888963407ull;
+            b[i] = (s >> 7) % p.Q;
         }
-    std::vector<uint64_t> A = a, Bv = b;
-    host_ntt_fwd(t, A.data());
-    host_ntt_fwd(t, Bv.data());
-    for (uint32_t i = 0; i < p.N; ++i) A[i] = mulmod(A[i], Bv[i], p.Q);
-    host_ntt_inv(t, A.data(), true);
-    if (A != ref) return fail(TFHE_ERR_INTERNAL, "host NTT product mismatch");
-    // (3) monomial table: NTT(X^m)[x] = psi^(e_x * m)
-    for (uint32_t m : {1u, 3u, p.N - 1, p.N + 5, 2 * p.N - 1}) {
-        std::vector<uint64_t> mon(p.N, 0);
-        if (m < p.N) mon[m] = 1;
-        else mon[m - p.N] = p.Q - 1;
-        host_ntt_fwd(t, mon.data());
+        for (uint32_t i = 0; i < p.N; ++i)
+            for (uint32_t j = 0; j < p.N; ++j) {
+                uint64_t v = mulmod(a[i], b[j], p.Q);
+                if (i + j < p.N) ref[i + j] = addmod(ref[i + j], v, p.Q);
+                else ref[i + j - p.N] = submod(ref[i + j - p.N], v, p.Q);
+            }
+        std::vector<uint64_t> A = a, Bv = b;
+        host_ntt_fwd(t, A.data());
+        host_ntt_fwd(t, Bv.data());
+        for (uint32_t i = 0; i < p.N; ++i) A[i] = mulmod(A[i], Bv[i], p.Q);
+        host_ntt_inv(t, A.data(), true);
+        if (A != ref) return fail(TFHE_ERR_INTERNAL, "host NTT product mismatch");
+        // (3) monomial table: NTT(X^m)[x] = psi^(e_x * m)
+        for (uint32_t m : {1u, 3u, p.N - 1, p.N + 5, 2 * p.N - 1}) {
+            std::vector<uint64_t> mon(p.N, 0);
+            if (m < p.N) mon[m] = 1;
+            else mon[m - p.N] = p.Q - 1;
+            host_ntt_fwd(t, mon.data());
+            for (uint32_t x = 0; x < p.N; ++x) {
+                uint32_t idx = (uint32_t)(((uint64_t)t.eidx[x] * m) % (2ull * p.N));
+                if (mon[x] != addmod(t.mono[idx], 1, p.Q)) return fail(TFHE_ERR_INTERNAL, "monomial table mismatch");
+            }
+        }
+        // (3b) the slot exponents are 2 bitrev(x) + 1 (the fast kernel relies on it)
+        for (uint32_t x = 0; x < p.N; ++x)
+            if (t.eidx[x] != 2 * bitrev(x, t.logN) + 1) return fail(TFHE_ERR_INTERNAL, "eidx is not 2 bitrev(x) + 1");
+        // (4) Shoup companions at the chosen word width
+        const int wb = word_bits_for(p);
+        const u128 R = (u128)1 << wb;
         for (uint32_t x = 0; x < p.N; ++x) {
-            uint32_t idx = (uint32_t)(((uint64_t)t.eidx[x] * m) % (2ull * p.N));
-            if (mon[x] != addmod(t.mono[idx], 1, p.Q)) return fail(TFHE_ERR_INTERNAL, "monomial table mismatch");
+            const uint64_t w = t.psi_br[x], wp = shoup_companion(w, p.Q, wb);
+            const uint64_t aa = a[x] | (wb == 32 ? 0x80000000ull : 0x8000000000000000ull);
+            const uint64_t mask = wb == 32 ? 0xFFFFFFFFull : ~0ull;
+            const uint64_t qt = (uint64_t)(((u128)aa * wp) >> wb);
+            const uint64_t r = (uint64_t)(((u128)aa * w - (u128)qt * p.Q) % R) & mask;
+            if (r >= 2 * p.Q || r % p.Q != mulmod(aa % p.Q, w, p.Q)) return fail(TFHE_ERR_INTERNAL, "Shoup bound");
         }
-    }
-    // (3b) the slot exponents are 2 bitrev(x) + 1 (the fast kernel relies on it)
-    for (uint32_t x = 0; x < p.N; ++x)
-        if (t.eidx[x] != 2 * bitrev(x, t.logN) + 1) return fail(TFHE_ERR_INTERNAL, "eidx is not 2 bitrev(x) + 1");
-    // (4) Shoup companions at the chosen word width
-    const int wb = word_bits_for(p);
-    const u128 R = (u128)1 << wb;
-    for (uint32_t x = 0; x < p.N; ++x) {
-        const uint64_t w = t.psi_br[x], wp = shoup_companion(w, p.Q, wb);
-        const uint64_t aa = a[x] | (wb == 32 ? 0x80000000ull : 0x8000000000000000ull);
-        const uint64_t mask = wb == 32 ? 0xFFFFFFFFull : ~0ull;
-        const uint64_t qt = (uint64_t)(((u128)aa * wp) >> wb);
-        const uint64_t r = (uint64_t)(((u128)aa * w - (u128)qt * p.Q) % R) & mask;
-        if (r >= 2 * p.Q || r % p.Q != mulmod(aa % p.Q, w, p.Q)) return fail(TFHE_ERR_INTERNAL, "Shoup bound");
-    }
-    return TFHE_OK;
+        return TFHE_OK;
+    });
 }
 
 }  // extern "C"

@@ -75,6 +75,13 @@ struct KSParams {
 };
 hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
                       uint64_t fmod, uint64_t* out, size_t B, hipStream_t s);
+// Batch-tiled form of the same (ks_tiled.hip): the KSK is staged in LDS once per tile of
+// up to 1024 ciphertexts instead of gathered per ciphertext.  scratch: ks_tiled_scratch_bytes
+// (transposed digit planes).  hipErrorNotSupported when dKS > 16 or baseKS too large.
+size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B);
+bool ks_tiled_supported(const KSParams& P);
+hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s);
 
 // ---- test vectors, extraction and LWE glue (binfhe-base-scheme.cpp) ----
 enum TvMode : uint32_t {
@@ -117,8 +124,9 @@ enum LweOp : uint32_t {
 hipError_t launch_lwe_op(uint32_t op, uint32_t n, uint64_t m, uint64_t c, const uint64_t* x, const uint64_t* y,
                          uint64_t* out, size_t B, hipStream_t s);
 
-// CiphertextMulMatrix: out[c][w] = sum_k matrix[k][c] * ct[k][w] mod modulus
-hipError_t launch_ct_mul_matrix(uint32_t width, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
+// CiphertextMulMatrix: out[c][w] = sum_k matrix[k][c] * ct[k][w] mod modulus.
+// ct and matrix are device copies the launch reduces in place into [0, modulus).
+hipError_t launch_ct_mul_matrix(uint32_t width, size_t K, uint64_t* ct, size_t cols, int64_t* matrix,
                                 uint64_t modulus, uint64_t* out, hipStream_t s);
 
 }  // namespace tfhe

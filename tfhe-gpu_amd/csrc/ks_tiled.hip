@@ -1,0 +1,264 @@
+// ks_tiled.hip -- batch-tiled key switch (the KeySwitch of MKM, lwe-pke.cpp:299-321;
+// reference kernel MKMSwitchKernel bootstrapping.cu:73-118).
+//
+// out[ct][k] = RoundqQ(-sum_{i<N, j<dKS} A[i][d_j(ct, i)][j][k] mod qKS, fmod, qKS)
+// with d_j(ct, i) the j-th base-baseKS digit of RoundqQ(ext[ct][i], qKS, Q), and the
+// same for the B column (b - sum).
+//
+// The gather form (k_mkm, one wavefront per ciphertext) reads N*dKS KSK rows per
+// ciphertext: B times the rows, from L2/MALL/HBM.  Here a workgroup owns a tile of
+// T = 256*CTS ciphertexts and CT columns, and for every (i, j) stages the baseKS row
+// segments A[i][0..baseKS)[j][c0..c0+CT) in LDS once; its T ciphertexts then pick
+// their rows from LDS.  The KSK leaves HBM ceil(B/T) times instead of B times
+// (C3, qKS = 2^35: 4.8 GB KSK, 150 MB of gathered rows per ciphertext).
+//
+// Two launches:
+//   k_ks_digits  RoundqQ + digits of every coefficient, transposed to
+//                dig[(i*dKS + j)][ct] (u8) so a tile's digits for one (i, j) are one
+//                contiguous run; bq[ct] = RoundqQ(b).
+//   k_ks_tiled   the tiled accumulation; one workgroup barrier per (i, j): the next
+//                step's row segments and digits are loaded into registers while this
+//                step's are summed, then stored into the other LDS buffer.
+#include "device_math.hpp"
+#include "kernels.hpp"
+
+#include <cstdlib>
+
+namespace tfhe {
+namespace {
+
+constexpr int KT = 256;         // threads per workgroup
+constexpr int DIG_TILE = 64;    // ciphertexts x coefficients per k_ks_digits block
+constexpr int G = 4;            // (i, j) steps per LDS stage (one barrier each)
+constexpr uint32_t KS_MAX_DKS = 16;
+
+// Digit planes: dig[(s / 4) * Bp + ct] holds the digits of steps s = 4g .. 4g+3 of one
+// ciphertext (s = i*dKS + j, byte s % 4), so one u32 load gives a stage's digits.
+__global__ void __launch_bounds__(256) k_ks_digits(KSParams P, const uint64_t* __restrict__ ext,
+                                                   uint32_t* __restrict__ dig, uint64_t* __restrict__ bq, size_t B,
+                                                   size_t Bp) {
+    extern __shared__ __align__(16) unsigned char tile[];  // [64 coefficients * dKS steps][64 ciphertexts]
+    const uint32_t N = P.N, dks = P.dKS, bks = P.baseKS;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t ct0 = (size_t)blockIdx.x * DIG_TILE;
+    const uint32_t i0 = blockIdx.y * DIG_TILE;
+    const uint32_t i = i0 + lane;
+    for (uint32_t r = 0; r < DIG_TILE / 4; ++r) {
+        const uint32_t cl = w * (DIG_TILE / 4) + r;
+        const size_t ct = ct0 + cl;
+        uint64_t x = 0;
+        if (ct < B && i <= N) x = round_qQ(ext[ct * (N + 1) + i], P.qKS, P.Q);  // row ct: 64 consecutive words
+        if (i == N) {
+            if (ct < B) bq[ct] = x;
+        } else {
+            for (uint32_t j = 0; j < dks; ++j, x /= bks) tile[(lane * dks + j) * DIG_TILE + cl] = (uint8_t)(x % bks);
+        }
+    }
+    __syncthreads();
+    // the tile's 64*dKS steps start at step i0*dKS (a multiple of 4): words of 4 steps
+    const uint32_t ni = min(DIG_TILE, (int)(N - min(N, i0)));
+    const uint32_t groups = ni * dks / 4;
+    const size_t g0 = (size_t)i0 * dks / 4;
+    for (uint32_t wd = threadIdx.x; wd < groups * DIG_TILE; wd += 256) {
+        const uint32_t g = wd / DIG_TILE, cl = wd % DIG_TILE;
+        const unsigned char* t = tile + (size_t)g * 4 * DIG_TILE + cl;
+        const uint32_t v = t[0] | (t[DIG_TILE] << 8) | (t[2 * DIG_TILE] << 16) | ((uint32_t)t[3 * DIG_TILE] << 24);
+        dig[(g0 + g) * Bp + ct0 + cl] = v;
+    }
+}
+
+// ACC: exact per-column sum type (u32 when N*dKS*(qKS-1) < 2^32).  Workgroup = T = 256*CTS
+// ciphertexts x CT columns.  Block mapping: blocks b and b + 8 run on one XCD (round-robin
+// dealing), so consecutive blocks of one XCD take the ciphertext tiles of ONE column tile:
+// they stream the same KSK segments at about the same time and share them in that XCD's L2.
+template <typename KW, typename ACC, int CT, int CTS, int MAXL>
+__global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __restrict__ kska,
+                                                 const KW* __restrict__ kskb, const uint32_t* __restrict__ dig,
+                                                 const uint64_t* __restrict__ bq, size_t B, size_t Bp, uint32_t nct,
+                                                 uint32_t ncol, uint64_t fmod, uint64_t* __restrict__ out) {
+    constexpr int VEC = 16 / sizeof(KW);           // KSK words per 16-byte piece
+    constexpr int PIECES = CT / VEC;               // pieces per row segment
+    constexpr int STRIDE = CT * sizeof(KW) + 16;   // LDS row pitch: consecutive rows start 4 banks apart
+    // MAXL: staged 16-byte pieces per thread and stage, ceil(G * baseKS * PIECES / KT)
+    static_assert(CT % VEC == 0, "column tile is whole pieces");
+    extern __shared__ __align__(16) unsigned char sm[];
+    const uint32_t bks = P.baseKS, dks = P.dKS, npad = P.n_pad, n = P.n;
+    const uint32_t th = threadIdx.x;
+    const uint32_t L = blockIdx.x, k = L >> 3;
+    const uint32_t col_tile = (k / nct) * 8 + (L & 7), ct_tile = k % nct;
+    if (col_tile >= ncol) return;  // whole workgroup
+    const uint32_t c0 = col_tile * CT;
+    const size_t t0 = (size_t)ct_tile * KT * CTS;
+    const bool bcol = col_tile == 0;  // this column tile also sums the B column
+    const uint32_t step_bytes = bks * STRIDE;
+    const uint32_t stage_bytes = G * step_bytes;
+    KW* bb = reinterpret_cast<KW*>(sm + 2 * stage_bytes);  // [2][G][baseKS] B entries
+    const uint32_t npieces = bks * PIECES;                  // per step
+    const uint32_t total = G * npieces;                     // per stage
+
+    uint4 stg[MAXL];
+    KW bstg[G];
+    auto load = [&](uint32_t g) {  // stage g = steps 4g .. 4g+3
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l) {
+            const uint32_t idx = th + l * KT;
+            if (idx < total) {
+                const uint32_t st = idx / npieces, r = idx - st * npieces;
+                const uint32_t v = r / PIECES, pc = r - v * PIECES;
+                const uint32_t s = g * G + st, i = s / dks, j = s - i * dks;
+                const uint32_t col = c0 + pc * VEC;
+                const size_t row = ((size_t)i * bks + v) * dks + j;
+                stg[l] = col < npad ? *reinterpret_cast<const uint4*>(kska + row * npad + col) : make_uint4(0, 0, 0, 0);
+            }
+        }
+        if (bcol && th < bks) {
+#pragma unroll
+            for (int st = 0; st < G; ++st) {
+                const uint32_t s = g * G + st, i = s / dks, j = s - i * dks;
+                bstg[st] = kskb[((size_t)i * bks + th) * dks + j];
+            }
+        }
+    };
+    auto store = [&](uint32_t g) {
+        unsigned char* b = sm + (g & 1) * stage_bytes;
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l) {
+            const uint32_t idx = th + l * KT;
+            if (idx < total) {
+                const uint32_t st = idx / npieces, r = idx - st * npieces;
+                const uint32_t v = r / PIECES, pc = r - v * PIECES;
+                *reinterpret_cast<uint4*>(b + st * step_bytes + v * STRIDE + pc * 16) = stg[l];
+            }
+        }
+        if (bcol && th < bks) {
+#pragma unroll
+            for (int st = 0; st < G; ++st) bb[((g & 1) * G + st) * bks + th] = bstg[st];
+        }
+    };
+
+    ACC acc[CTS][CT];
+    uint64_t bsum[CTS];
+    uint32_t dg[CTS], dgn[CTS];
+#pragma unroll
+    for (int c = 0; c < CTS; ++c) {
+        bsum[c] = 0;
+#pragma unroll
+        for (int kk = 0; kk < CT; ++kk) acc[c][kk] = 0;
+        dg[c] = dig[t0 + th + KT * c];  // stage 0; dig is padded to Bp >= the grid's tiles
+    }
+    const uint32_t stages = P.N * dks / G;
+    load(0);
+    for (uint32_t g = 0; g < stages; ++g) {
+        store(g);
+        if (g + 1 < stages) {
+            load(g + 1);
+#pragma unroll
+            for (int c = 0; c < CTS; ++c) dgn[c] = dig[(size_t)(g + 1) * Bp + t0 + th + KT * c];
+        }
+        __syncthreads();
+        const unsigned char* b = sm + (g & 1) * stage_bytes;
+#pragma unroll 1  // one step's row reads in flight at a time: bounded registers
+        for (int st = 0; st < G; ++st) {
+#pragma unroll
+            for (int c = 0; c < CTS; ++c) {
+                const uint32_t d = (dg[c] >> (8 * st)) & 0xff;
+                const unsigned char* r = b + st * step_bytes + d * STRIDE;
+#pragma unroll
+                for (int p = 0; p < PIECES; ++p) {
+                    const uint4 u = *reinterpret_cast<const uint4*>(r + p * 16);
+                    const KW* vals = reinterpret_cast<const KW*>(&u);
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) acc[c][p * VEC + v] += (ACC)vals[v];
+                }
+                if (bcol) bsum[c] += (uint64_t)bb[((g & 1) * G + st) * bks + d];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) dg[c] = dgn[c];
+    }
+
+    const uint64_t qks = P.qKS;
+#pragma unroll
+    for (int c = 0; c < CTS; ++c) {
+        const size_t ct = t0 + th + KT * c;
+        if (ct >= B) continue;
+        uint64_t* o = out + ct * (size_t)(n + 1);
+#pragma unroll
+        for (int kk = 0; kk < CT; ++kk) {
+            const uint32_t col = c0 + kk;
+            if (col < n) {
+                const uint64_t r = (uint64_t)acc[c][kk] % qks;
+                o[col] = round_qQ(r == 0 ? 0 : qks - r, fmod, qks);  // 0 - sum
+            }
+        }
+        if (bcol) {
+            const uint64_t r = bsum[c] % qks, x = bq[ct];
+            o[n] = round_qQ(x >= r ? x - r : x + (qks - r), fmod, qks);  // b - sum
+        }
+    }
+}
+
+template <typename KW, typename ACC, int CT, int CTS>
+hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, const uint32_t* dig,
+                        const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, hipStream_t s) {
+    constexpr int STRIDE = CT * sizeof(KW) + 16;
+    const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
+    const size_t lpt = ((size_t)G * P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT;
+    if (lds > 80 * 1024 || lpt > 8) return hipErrorNotSupported;
+    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4>
+                                                                  : k_ks_tiled<KW, ACC, CT, CTS, 8>;
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
+    const uint32_t ncol = (P.n_pad + CT - 1) / CT;
+    const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp, nct,
+                       ncol, fmod, out);
+    return hipGetLastError();
+}
+
+constexpr size_t kTileMax = 4 * KT;  // the largest ciphertext tile of the builds below
+
+size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; }
+
+}  // namespace
+
+size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
+    const size_t Bp = ks_tiled_bp(B);
+    return (size_t)P.N * P.dKS * Bp + Bp * sizeof(uint64_t);
+}
+
+bool ks_tiled_supported(const KSParams& P) {
+    return P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (4 * G) == 0;
+}
+
+hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (!ks_tiled_supported(P)) return hipErrorNotSupported;
+    const size_t Bp = ks_tiled_bp(B);
+    uint32_t* dig = static_cast<uint32_t*>(scratch);
+    uint64_t* bq = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)P.N * P.dKS * Bp);
+    const size_t lds_dig = (size_t)P.dKS * DIG_TILE * DIG_TILE;
+    hipFuncSetAttribute((const void*)k_ks_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig);
+    // every ciphertext tile of Bp gets digits (zeros past B), so k_ks_tiled reads no garbage
+    const dim3 g1((unsigned)(Bp / DIG_TILE), (P.N + 1 + DIG_TILE - 1) / DIG_TILE);
+    hipLaunchKernelGGL(k_ks_digits, g1, dim3(256), lds_dig, s, P, ext, dig, bq, B, Bp);
+    const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
+    const char* e = std::getenv("TFHE_KS_CTS");  // ciphertexts per thread (A/B runs)
+    const int cts = e ? std::atoi(e) : 1;
+    switch (ksk_bits) {
+        case 16:
+            return launch_tiled<uint16_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+        case 32:
+            if (acc32)
+                return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
+                                : launch_tiled<uint32_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+            return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
+                            : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+        default:
+            return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
+                            : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+    }
+}
+
+}  // namespace tfhe

@@ -262,26 +262,60 @@ hipError_t launch_lwe_op(uint32_t op, uint32_t n, uint64_t m, uint64_t c, const 
 
 // ---------------------------------------------------------------------------
 // CiphertextMulMatrix: the reference computes the product as an FP64 DGEMM and
-// fmod (lwe-operation.cu:106-111), exact only while |sums| < 2^53; here the sum
-// is exact (__int128) and reduced to [0, modulus).
+// fmod (lwe-operation.cu:106-111), exact only while |sums| < 2^53 and non-negative;
+// here every operand is first reduced into [0, modulus) (signed matrix entries by
+// their mathematical residue), then the sum is exact: unreduced u128 accumulation
+// when K (modulus-1)^2 < 2^128, else a modular add per term.
 // ---------------------------------------------------------------------------
+__global__ void k_reduce_signed(int64_t* __restrict__ v, size_t count, uint64_t modulus) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    __int128 r = (__int128)v[i] % (__int128)modulus;
+    if (r < 0) r += modulus;
+    reinterpret_cast<uint64_t*>(v)[i] = (uint64_t)r;
+}
+
+__global__ void k_reduce_unsigned(uint64_t* __restrict__ v, size_t count, uint64_t modulus) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    v[i] %= modulus;
+}
+
+template <bool PER_TERM>
 __global__ void k_ct_mul_matrix(uint32_t width, size_t K, const uint64_t* __restrict__ ct, size_t cols,
-                                const int64_t* __restrict__ mat, uint64_t modulus, uint64_t* __restrict__ out) {
+                                const uint64_t* __restrict__ mat, uint64_t modulus, uint64_t* __restrict__ out) {
     const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t c = blockIdx.y;
     if (w >= width) return;
-    __int128 acc = 0;
-    for (size_t k = 0; k < K; ++k) acc += (__int128)mat[k * cols + c] * (__int128)ct[k * width + w];
-    __int128 r = acc % (__int128)modulus;
-    if (r < 0) r += modulus;
-    out[c * width + w] = (uint64_t)r;
+    unsigned __int128 acc = 0;
+    for (size_t k = 0; k < K; ++k) {
+        const unsigned __int128 t = (unsigned __int128)mat[k * cols + c] * ct[k * width + w];
+        if (PER_TERM) {
+            acc += t % modulus;  // acc < modulus before, so no overflow
+            if (acc >= modulus) acc -= modulus;
+        } else {
+            acc += t;
+        }
+    }
+    out[c * width + w] = (uint64_t)(acc % modulus);
 }
 
-hipError_t launch_ct_mul_matrix(uint32_t width, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
+hipError_t launch_ct_mul_matrix(uint32_t width, size_t K, uint64_t* ct, size_t cols, int64_t* matrix,
                                 uint64_t modulus, uint64_t* out, hipStream_t s) {
     if (K == 0 || cols == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ct_mul_matrix, dim3((width + 255) / 256, (unsigned)cols), dim3(256), 0, s, width, K, ct,
-                       cols, matrix, modulus, out);
+    if (modulus == 0) return hipErrorInvalidValue;
+    const size_t nm = K * cols, nc = K * (size_t)width;
+    hipLaunchKernelGGL(k_reduce_signed, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s, matrix, nm, modulus);
+    hipLaunchKernelGGL(k_reduce_unsigned, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, ct, nc, modulus);
+    const unsigned __int128 sq = (unsigned __int128)(modulus - 1) * (modulus - 1);
+    const bool per_term = sq != 0 && sq > ~(unsigned __int128)0 / K;
+    const uint64_t* m = reinterpret_cast<const uint64_t*>(matrix);
+    if (per_term)
+        hipLaunchKernelGGL(k_ct_mul_matrix<true>, dim3((width + 255) / 256, (unsigned)cols), dim3(256), 0, s, width,
+                           K, ct, cols, m, modulus, out);
+    else
+        hipLaunchKernelGGL(k_ct_mul_matrix<false>, dim3((width + 255) / 256, (unsigned)cols), dim3(256), 0, s,
+                           width, K, ct, cols, m, modulus, out);
     return hipGetLastError();
 }
 

@@ -15,6 +15,17 @@ def _u64(x):
     return np.ascontiguousarray(x, dtype=np.uint64)
 
 
+def _rows(x, width: int, what: str):
+    """[B][width] view of a ciphertext batch (a single ciphertext becomes B = 1); the
+    C-ABI takes bare pointers, so every shape is checked here before a call."""
+    x = _u64(x)
+    if x.ndim == 1:
+        x = x[None]
+    if x.ndim != 2 or x.shape[1] != width:
+        raise ValueError(f"{what}: expected shape (B, {width}), got {x.shape}")
+    return x
+
+
 class BinFHEContextHIP:
     BETA = 128  # BinFHEContext::GetBeta, binfhecontext.h:348-350
 
@@ -90,22 +101,29 @@ class BinFHEContextHIP:
     # -- reference boundary calls --
     def EvalAcc(self, a, a_mod, acc):
         """EvalAcc_CUDA: a[B][n] mod a_mod, acc[B][2][N] -> new acc (acc0 transposed)."""
+        n, N = self.params.n, self.params.N
         a = _u64(a)
         out = np.array(acc, dtype=np.uint64, copy=True, order="C")
-        B = a.size // self.params.n
+        if a.size == 0 or a.size % n:
+            raise ValueError(f"EvalAcc: a must hold B*n words (n = {n}), got {a.size}")
+        B = a.size // n
+        if out.size != B * 2 * N:
+            raise ValueError(f"EvalAcc: acc must hold B*2*N = {B * 2 * N} words, got {out.size}")
         check(lib().tfhe_eval_acc(self._h, B, a.ravel(), a_mod, out.ravel()), "tfhe_eval_acc")
         return out
 
     def MKMSwitch(self, ct_ext, fmod):
-        ct_ext = _u64(ct_ext)
-        B = ct_ext.size // (self.params.N + 1)
+        ct_ext = _rows(ct_ext, self.params.N + 1, "MKMSwitch")
+        B = ct_ext.shape[0]
         out = np.empty((B, self.params.n + 1), dtype=np.uint64)
         check(lib().tfhe_mkm_switch(self._h, B, ct_ext.ravel(), fmod, out.ravel()), "tfhe_mkm_switch")
         return out
 
     def CiphertextMulMatrix(self, ct, matrix, modulus):
-        ct = _u64(ct)
+        ct = _rows(ct, self.params.n + 1, "CiphertextMulMatrix")
         m = np.ascontiguousarray(matrix, dtype=np.int64)
+        if m.ndim != 2:
+            raise ValueError("CiphertextMulMatrix: matrix must be 2-D [K][cols]")
         K, cols = m.shape
         if ct.size != K * (self.params.n + 1):  # lwe-operation.cu:66-69
             raise ValueError("The number of rows of the matrix must be equal to the number of input ciphertexts.")
@@ -115,15 +133,15 @@ class BinFHEContextHIP:
         return out
 
     # -- vector BinFHEContext surface --
-    def _batch(self, ct):
-        ct = _u64(ct)
-        if ct.ndim == 1:
-            ct = ct[None]
+    def _batch(self, ct, what="ciphertexts"):
+        ct = _rows(ct, self.params.n + 1, what)
         return ct, ct.shape[0]
 
     def EvalBinGate(self, gate, ct1, ct2, q=None):
-        ct1, B = self._batch(ct1)
-        ct2, _ = self._batch(ct2)
+        ct1, B = self._batch(ct1, "EvalBinGate ct1")
+        ct2, B2 = self._batch(ct2, "EvalBinGate ct2")
+        if B != B2:  # binfhe-base-scheme.cpp:607
+            raise ValueError(f"EvalBinGate: input ciphertexts size unmatched ({B} vs {B2})")
         g = BINGATE[gate] if isinstance(gate, str) else int(gate)
         out = np.empty((B, self.params.n + 1), dtype=np.uint64)
         check(lib().tfhe_eval_bin_gate(self._h, g, B, ct1.ravel(), ct2.ravel(), q or self.params.q, out.ravel()),
@@ -131,27 +149,30 @@ class BinFHEContextHIP:
         return out
 
     def EvalFunc(self, ct, lut, q=None):
-        ct, B = self._batch(ct)
+        ct, B = self._batch(ct, "EvalFunc")
         lut = _u64(lut)
+        qq = q or self.params.q
+        if not (lut.shape == (qq,) or lut.shape == (B, qq)):
+            raise ValueError(f"EvalFunc: LUT must have shape ({qq},) or ({B}, {qq}), got {lut.shape}")
         out = np.empty((B, self.params.n + 1), dtype=np.uint64)
-        check(lib().tfhe_eval_func(self._h, B, ct.ravel(), q or self.params.q, lut.ravel(), int(lut.ndim == 2),
+        check(lib().tfhe_eval_func(self._h, B, ct.ravel(), qq, lut.ravel(), int(lut.ndim == 2),
                                    out.ravel()), "tfhe_eval_func")
         return out
 
     def EvalFloor(self, ct, mod, roundbits=0):
-        ct, B = self._batch(ct)
+        ct, B = self._batch(ct, "EvalFloor")
         out = np.empty((B, self.params.n + 1), dtype=np.uint64)
         check(lib().tfhe_eval_floor(self._h, B, ct.ravel(), mod, roundbits, out.ravel()), "tfhe_eval_floor")
         return out
 
     def EvalSign(self, ct, mod):
-        ct, B = self._batch(ct)
+        ct, B = self._batch(ct, "EvalSign")
         out = np.empty((B, self.params.n + 1), dtype=np.uint64)
         check(lib().tfhe_eval_sign(self._h, B, ct.ravel(), mod, out.ravel()), "tfhe_eval_sign")
         return out
 
     def EvalDecomp(self, ct, mod, max_digits=16):
-        ct, B = self._batch(ct)
+        ct, B = self._batch(ct, "EvalDecomp")
         out = np.zeros((B, max_digits, self.params.n + 1), dtype=np.uint64)
         moduli = np.zeros(max_digits, dtype=np.uint64)
         nd = C.c_uint32()

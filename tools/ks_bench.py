@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Key-switch (MKM) kernel A/B on one MI355X: the per-ciphertext gather (k_mkm) against
+the batch-tiled form (ks_tiled.hip), device-resident inputs, HIP events on the launch
+stream.  Both outputs must be equal.  One JSON line per configuration.
+Usage: python3 tools/ks_bench.py [STD128 STD192 STD128Q ARB12 LOGQ23] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+
+CONFIGS = {  # name: (params, batch of the BASELINE configuration that uses it)
+    "STD128": (lambda c: c.params_from_set("STD128"), 8192),
+    "STD192": (lambda c: c.params_from_set("STD192"), 8192),
+    "STD128Q": (lambda c: c.params_from_set("STD128Q"), 1024),
+    "ARB12": (lambda c: c.params_from_logq("STD128", True, 12, 0, 0, 1), 4096),
+    "LOGQ23": (lambda c: c.params_from_logq("STD128", False, 23, 0, 0, 1), 1024),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=list(CONFIGS))
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=0, help="override the batch")
+    args = ap.parse_args()
+    import torch
+
+    import tfhe_amd
+    from tfhe_amd import capi
+
+    for name in args.configs:
+        mk, B = CONFIGS[name]
+        B = args.batch or B
+        p = mk(capi)
+        rs = np.random.default_rng(3)
+        bsk = rs.integers(0, p.Q, p.bsk_words(), dtype=np.uint64)
+        ksk = rs.integers(0, p.qKS, p.ksk_words(), dtype=np.uint64)
+        ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+        del bsk, ksk
+        ext = torch.from_numpy(rs.integers(0, p.Q, (B, p.N + 1), dtype=np.uint64).view(np.int64)).cuda()
+        outs = {}
+        res = {"config": name, "batch": B, "N": p.N, "n": p.n, "qKS": p.qKS, "baseKS": p.baseKS, "dKS": p.dKS}
+        s = torch.cuda.Stream()
+        for mode, tmin in (("gather", "0"), ("tiled", "1")):
+            os.environ["TFHE_KS_TILED_MIN"] = tmin
+            out = torch.empty((B, p.n + 1), dtype=torch.int64, device="cuda")
+            call = lambda: capi.check(capi.lib().tfhe_mkm_switch_device(ctx.handle, B, ext.data_ptr(), p.q,
+                                                                        out.data_ptr(), s.cuda_stream), "mkm")
+            call()
+            s.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(args.reps):
+                call()
+            e1.record(s)
+            s.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            outs[mode] = out.cpu().numpy()
+            res[f"{mode}_ms"] = round(ms, 3)
+        os.environ.pop("TFHE_KS_TILED_MIN", None)
+        res["equal"] = bool(np.array_equal(outs["gather"], outs["tiled"]))
+        res["speedup"] = round(res["gather_ms"] / res["tiled_ms"], 2)
+        print(json.dumps(res), flush=True)
+        ctx.GPUClean()
+        del ext
+
+
+if __name__ == "__main__":
+    main()
