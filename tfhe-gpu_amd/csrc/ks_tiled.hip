@@ -23,13 +23,16 @@
 #include "kernels.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace tfhe {
 namespace {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a native vector: stays in registers
+
 constexpr int KT = 256;         // threads per workgroup
 constexpr int DIG_TILE = 64;    // ciphertexts x coefficients per k_ks_digits block
-constexpr int G = 4;            // (i, j) steps per LDS stage (one barrier each)
+constexpr int GMAX = 4;         // (i, j) steps per LDS stage (one barrier each): 2 or 4
 constexpr uint32_t KS_MAX_DKS = 16;
 
 // Digit planes: dig[(s / 4) * Bp + ct] holds the digits of steps s = 4g .. 4g+3 of one
@@ -67,11 +70,29 @@ __global__ void __launch_bounds__(256) k_ks_digits(KSParams P, const uint64_t* _
     }
 }
 
+// v-th KW word of a 16-byte piece (v a compile-time constant after unrolling)
+template <typename KW>
+__device__ __forceinline__ KW word_of(const u32x4& u, int v);
+template <>
+__device__ __forceinline__ uint16_t word_of<uint16_t>(const u32x4& u, int v) {
+    const uint32_t w = v < 2 ? u.x : v < 4 ? u.y : v < 6 ? u.z : u.w;
+    return (uint16_t)(w >> (16 * (v & 1)));
+}
+template <>
+__device__ __forceinline__ uint32_t word_of<uint32_t>(const u32x4& u, int v) {
+    return v == 0 ? u.x : v == 1 ? u.y : v == 2 ? u.z : u.w;
+}
+template <>
+__device__ __forceinline__ uint64_t word_of<uint64_t>(const u32x4& u, int v) {
+    return v == 0 ? ((uint64_t)u.y << 32 | u.x) : ((uint64_t)u.w << 32 | u.z);
+}
+
 // ACC: exact per-column sum type (u32 when N*dKS*(qKS-1) < 2^32).  Workgroup = T = 256*CTS
-// ciphertexts x CT columns.  Block mapping: blocks b and b + 8 run on one XCD (round-robin
+// ciphertexts x CT columns; G (i, j) steps per LDS stage; MAXL staged 16-byte pieces per
+// thread and stage.  Block mapping: blocks b and b + 8 run on one XCD (round-robin
 // dealing), so consecutive blocks of one XCD take the ciphertext tiles of ONE column tile:
 // they stream the same KSK segments at about the same time and share them in that XCD's L2.
-template <typename KW, typename ACC, int CT, int CTS, int MAXL>
+template <typename KW, typename ACC, int CT, int CTS, int MAXL, int G>
 __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __restrict__ kska,
                                                  const KW* __restrict__ kskb, const uint32_t* __restrict__ dig,
                                                  const uint64_t* __restrict__ bq, size_t B, size_t Bp, uint32_t nct,
@@ -79,8 +100,8 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     constexpr int VEC = 16 / sizeof(KW);           // KSK words per 16-byte piece
     constexpr int PIECES = CT / VEC;               // pieces per row segment
     constexpr int STRIDE = CT * sizeof(KW) + 16;   // LDS row pitch: consecutive rows start 4 banks apart
-    // MAXL: staged 16-byte pieces per thread and stage, ceil(G * baseKS * PIECES / KT)
     static_assert(CT % VEC == 0, "column tile is whole pieces");
+    static_assert(G == 2 || G == 4, "a stage is half or all of a digit word");
     extern __shared__ __align__(16) unsigned char sm[];
     const uint32_t bks = P.baseKS, dks = P.dKS, npad = P.n_pad, n = P.n;
     const uint32_t th = threadIdx.x;
@@ -96,86 +117,98 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     const uint32_t npieces = bks * PIECES;                  // per step
     const uint32_t total = G * npieces;                     // per stage
 
-    uint4 stg[MAXL];
-    KW bstg[G];
-    auto load = [&](uint32_t g) {  // stage g = steps 4g .. 4g+3
-#pragma unroll
-        for (int l = 0; l < MAXL; ++l) {
-            const uint32_t idx = th + l * KT;
-            if (idx < total) {
-                const uint32_t st = idx / npieces, r = idx - st * npieces;
-                const uint32_t v = r / PIECES, pc = r - v * PIECES;
-                const uint32_t s = g * G + st, i = s / dks, j = s - i * dks;
-                const uint32_t col = c0 + pc * VEC;
-                const size_t row = ((size_t)i * bks + v) * dks + j;
-                stg[l] = col < npad ? *reinterpret_cast<const uint4*>(kska + row * npad + col) : make_uint4(0, 0, 0, 0);
-            }
-        }
-        if (bcol && th < bks) {
-#pragma unroll
-            for (int st = 0; st < G; ++st) {
-                const uint32_t s = g * G + st, i = s / dks, j = s - i * dks;
-                bstg[st] = kskb[((size_t)i * bks + th) * dks + j];
-            }
-        }
-    };
-    auto store = [&](uint32_t g) {
-        unsigned char* b = sm + (g & 1) * stage_bytes;
-#pragma unroll
-        for (int l = 0; l < MAXL; ++l) {
-            const uint32_t idx = th + l * KT;
-            if (idx < total) {
-                const uint32_t st = idx / npieces, r = idx - st * npieces;
-                const uint32_t v = r / PIECES, pc = r - v * PIECES;
-                *reinterpret_cast<uint4*>(b + st * step_bytes + v * STRIDE + pc * 16) = stg[l];
-            }
-        }
-        if (bcol && th < bks) {
-#pragma unroll
-            for (int st = 0; st < G; ++st) bb[((g & 1) * G + st) * bks + th] = bstg[st];
-        }
-    };
+    // Staging is branch-free (clamped addresses, no exec-masked loads), so the compiler's
+    // wait counters stay exact, and written without lambdas, so the staging registers are not
+    // demoted to scratch.  Two register sets (X, Y) alternate: the rows of stage g+2 are issued
+    // while those of g+1 are in flight.  Pieces past n_pad read in-row words of another column
+    // instead of zeros: those columns (>= n_pad >= n) are never written out.
+#define KS_LOAD(STG, BSTG, DGV, gg)                                                                 \
+    do {                                                                                            \
+        _Pragma("unroll") for (int c = 0; c < CTS; ++c)                                             \
+            DGV[c] = dig[(size_t)((gg) * G / 4) * Bp + t0 + th + KT * c] >> (8 * (((gg) * G) % 4)); \
+        _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
+            const uint32_t idx = min(th + l * KT, total - 1);                                       \
+            const uint32_t st = idx / npieces, r = idx - st * npieces;                              \
+            const uint32_t v = r / PIECES, pc = r - v * PIECES;                                     \
+            const uint32_t s_ = (gg) * G + st, i = s_ / dks, j = s_ - i * dks;                      \
+            const uint32_t col = min(c0 + pc * VEC, npad - VEC);                                    \
+            STG[l] = *reinterpret_cast<const u32x4*>(kska + (((size_t)i * bks + v) * dks + j) * npad + col); \
+        }                                                                                           \
+        if (bcol) {                                                                                 \
+            const uint32_t v = min(th, bks - 1);                                                    \
+            _Pragma("unroll") for (int st = 0; st < G; ++st) {                                      \
+                const uint32_t s_ = (gg) * G + st, i = s_ / dks, j = s_ - i * dks;                  \
+                BSTG[st] = kskb[((size_t)i * bks + v) * dks + j];                                   \
+            }                                                                                       \
+        }                                                                                           \
+    } while (0)
+#define KS_STORE(STG, BSTG, gg)                                                                     \
+    do {                                                                                            \
+        unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                          \
+        _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
+            const uint32_t idx = th + l * KT;                                                       \
+            const uint32_t st = idx / npieces, r = idx - st * npieces;                              \
+            const uint32_t v = r / PIECES, pc = r - v * PIECES;                                     \
+            if (idx < total) *reinterpret_cast<u32x4*>(b_ + st * step_bytes + v * STRIDE + pc * 16) = STG[l]; \
+        }                                                                                           \
+        if (bcol && th < bks) {                                                                     \
+            _Pragma("unroll") for (int st = 0; st < G; ++st) bb[(((gg) & 1) * G + st) * bks + th] = BSTG[st]; \
+        }                                                                                           \
+    } while (0)
+#define KS_SUM(DGV, gg)                                                                             \
+    do {                                                                                            \
+        const unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                    \
+        _Pragma("unroll 1") for (int st = 0; st < G; ++st) {                                        \
+            _Pragma("unroll") for (int c = 0; c < CTS; ++c) {                                       \
+                const uint32_t d = (DGV[c] >> (8 * st)) & 0xff;                                     \
+                const unsigned char* r = b_ + st * step_bytes + d * STRIDE;                         \
+                _Pragma("unroll") for (int p = 0; p < PIECES; ++p) {                                \
+                    const u32x4 u = *reinterpret_cast<const u32x4*>(r + p * 16);                    \
+                    _Pragma("unroll") for (int v = 0; v < VEC; ++v)                                 \
+                        acc[c][p * VEC + v] += (ACC)word_of<KW>(u, v);                              \
+                }                                                                                   \
+                if (bcol) bsum[c] += (uint64_t)bb[(((gg) & 1) * G + st) * bks + d];                 \
+            }                                                                                       \
+        }                                                                                           \
+    } while (0)
 
+    using BW = typename std::conditional<sizeof(KW) == 8, uint64_t, uint32_t>::type;  // B entries, widened
+    u32x4 stgX[MAXL], stgY[MAXL];
+    BW bX[G], bY[G];
+    uint32_t dX[CTS], dY[CTS];
     ACC acc[CTS][CT];
     uint64_t bsum[CTS];
-    uint32_t dg[CTS], dgn[CTS];
 #pragma unroll
     for (int c = 0; c < CTS; ++c) {
         bsum[c] = 0;
 #pragma unroll
         for (int kk = 0; kk < CT; ++kk) acc[c][kk] = 0;
-        dg[c] = dig[t0 + th + KT * c];  // stage 0; dig is padded to Bp >= the grid's tiles
     }
-    const uint32_t stages = P.N * dks / G;
-    load(0);
-    for (uint32_t g = 0; g < stages; ++g) {
-        store(g);
-        if (g + 1 < stages) {
-            load(g + 1);
 #pragma unroll
-            for (int c = 0; c < CTS; ++c) dgn[c] = dig[(size_t)(g + 1) * Bp + t0 + th + KT * c];
-        }
+    for (int st = 0; st < G; ++st) bX[st] = bY[st] = 0;
+    const uint32_t stages = P.N * dks / G;  // even (ks_tiled_supported)
+    KS_LOAD(stgX, bX, dX, 0u);
+    KS_LOAD(stgY, bY, dY, 1u);
+    for (uint32_t g = 0; g < stages; g += 2) {
+        // the last two stages reload their own rows (unconditional loads keep the counts exact)
+        KS_STORE(stgX, bX, g);
+        uint32_t dXc[CTS];
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) dXc[c] = dX[c];
+        KS_LOAD(stgX, bX, dX, min(g + 2, stages - 2));
         __syncthreads();
-        const unsigned char* b = sm + (g & 1) * stage_bytes;
-#pragma unroll 1  // one step's row reads in flight at a time: bounded registers
-        for (int st = 0; st < G; ++st) {
+        KS_SUM(dXc, g);
+        KS_STORE(stgY, bY, g + 1);
+        uint32_t dYc[CTS];
 #pragma unroll
-            for (int c = 0; c < CTS; ++c) {
-                const uint32_t d = (dg[c] >> (8 * st)) & 0xff;
-                const unsigned char* r = b + st * step_bytes + d * STRIDE;
-#pragma unroll
-                for (int p = 0; p < PIECES; ++p) {
-                    const uint4 u = *reinterpret_cast<const uint4*>(r + p * 16);
-                    const KW* vals = reinterpret_cast<const KW*>(&u);
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) acc[c][p * VEC + v] += (ACC)vals[v];
-                }
-                if (bcol) bsum[c] += (uint64_t)bb[((g & 1) * G + st) * bks + d];
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < CTS; ++c) dg[c] = dgn[c];
+        for (int c = 0; c < CTS; ++c) dYc[c] = dY[c];
+        KS_LOAD(stgY, bY, dY, min(g + 3, stages - 1));
+        __syncthreads();
+        KS_SUM(dYc, g + 1);
     }
+#undef KS_LOAD
+#undef KS_STORE
+#undef KS_SUM
 
     const uint64_t qks = P.qKS;
 #pragma unroll
@@ -198,16 +231,17 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     }
 }
 
-template <typename KW, typename ACC, int CT, int CTS>
+template <typename KW, typename ACC, int CT, int CTS, int G = 4>
 hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, const uint32_t* dig,
                         const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, hipStream_t s) {
     constexpr int STRIDE = CT * sizeof(KW) + 16;
     const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
     const size_t lpt = ((size_t)G * P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT;
     if (lds > 80 * 1024 || lpt > 8) return hipErrorNotSupported;
-    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4>
-                                                                  : k_ks_tiled<KW, ACC, CT, CTS, 8>;
-    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2, G> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4, G>
+                                                                     : k_ks_tiled<KW, ACC, CT, CTS, 8, G>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = (P.n_pad + CT - 1) / CT;
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
@@ -228,7 +262,7 @@ size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
 }
 
 bool ks_tiled_supported(const KSParams& P) {
-    return P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (4 * G) == 0;
+    return P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (8 * GMAX) == 0;  // even stage count
 }
 
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
@@ -239,16 +273,17 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     uint32_t* dig = static_cast<uint32_t*>(scratch);
     uint64_t* bq = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)P.N * P.dKS * Bp);
     const size_t lds_dig = (size_t)P.dKS * DIG_TILE * DIG_TILE;
-    hipFuncSetAttribute((const void*)k_ks_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig);
+    hipError_t e = hipFuncSetAttribute((const void*)k_ks_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig);
+    if (e != hipSuccess) return e;
     // every ciphertext tile of Bp gets digits (zeros past B), so k_ks_tiled reads no garbage
     const dim3 g1((unsigned)(Bp / DIG_TILE), (P.N + 1 + DIG_TILE - 1) / DIG_TILE);
     hipLaunchKernelGGL(k_ks_digits, g1, dim3(256), lds_dig, s, P, ext, dig, bq, B, Bp);
     const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
-    const char* e = std::getenv("TFHE_KS_CTS");  // ciphertexts per thread (A/B runs)
-    const int cts = e ? std::atoi(e) : 1;
+    const char* ev = std::getenv("TFHE_KS_CTS");  // ciphertexts per thread (A/B runs)
+    const int cts = ev ? std::atoi(ev) : 1;
     switch (ksk_bits) {
-        case 16:
-            return launch_tiled<uint16_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+        case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
+            return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
         case 32:
             if (acc32)
                 return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
