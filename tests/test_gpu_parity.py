@@ -298,6 +298,43 @@ def test_batch_above_chunk_size(std128):
     assert np.array_equal(out[idx], orc.eval_bin_gate("OR", c1[idx], c2[idx]))
 
 
+@pytest.mark.parametrize("parts", ["1", "2", "3", "7"])
+def test_host_pipeline_sub_batches(std128, parts):
+    """The host-array runner cuts a shard into sub-batches whose copies (copy stream) overlap
+    the kernels (compute stream) through two alternating device I/O sets; every split --
+    ragged last sub-batch included -- gives the device-resident result, which equals the
+    oracle on a sample.  EvalFunc (one input array, a LUT) and EvalBinGate (two) both."""
+    import torch
+
+    if std128["path"] != "fast":
+        pytest.skip("one kernel is enough for the pipelining logic")
+    op, cp, ctx, orc = std128["op"], std128["cp"], std128["ctx"], std128["orc"]
+    rs = np.random.default_rng(17)
+    B = 1803
+    c1, c2 = random_cts(rs, B, cp.n, cp.q), random_cts(rs, B, cp.n, cp.q)
+    d1 = torch.from_numpy(c1.astype(np.int64)).cuda()
+    d2 = torch.from_numpy(c2.astype(np.int64)).cuda()
+    do = torch.empty_like(d1)
+    ctx.EvalBinGateDevice("AND", B, d1.data_ptr(), d2.data_ptr(), do.data_ptr())
+    torch.cuda.synchronize()
+    want = do.cpu().numpy().astype(np.uint64)
+    lut = np.array([(x * 3) % 4 * (cp.q // 4) for x in range(cp.q)], dtype=np.uint64) % cp.q
+    old = os.environ.get("TFHE_HOST_PARTS")
+    os.environ["TFHE_HOST_PARTS"] = parts
+    try:
+        got = ctx.EvalBinGate("AND", c1, c2)
+        fgot = ctx.EvalFunc(c1, lut)
+    finally:
+        if old is None:
+            os.environ.pop("TFHE_HOST_PARTS")
+        else:
+            os.environ["TFHE_HOST_PARTS"] = old
+    assert np.array_equal(got, want)
+    idx = [0, 1, B // 2, B - 2, B - 1]
+    assert np.array_equal(got[idx], orc.eval_bin_gate("AND", c1[idx], c2[idx]))
+    assert np.array_equal(fgot[idx], orc.eval_func(np.ascontiguousarray(c1[idx]), lut))
+
+
 def test_std128_opt_uses_fast_kernel_exactly(capi, oracle):
     """STD128_OPT (n=502) runs on the specialised kernel too: blind rotation parity with
     random keys (validity is irrelevant for bit-exactness)."""

@@ -104,9 +104,10 @@ struct Scratch {
     size_t io_words = 0;
 };
 
-// A device holds two (stream, scratch) lanes: host-array calls alternate sub-batches
-// between them so PCIe copies of one overlap the kernels of the other.  Device-pointer
-// entry points use lane 0 (or the caller's stream).
+// A device has a compute stream (`stream`, scratch `sc`) and a copy stream (`stream2`):
+// host-array calls pipeline their sub-batches' PCIe copies on the copy stream against the
+// kernels on the compute stream, through two device I/O sets (sc.io, sc2.io).  Device-pointer
+// entry points use the compute scratch on the caller's stream (or `stream`).
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
@@ -115,8 +116,8 @@ struct Device {
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
     Scratch sc;
     DevTables tables{};
-    hipStream_t stream2 = nullptr;  // lane 1
-    Scratch sc2;
+    hipStream_t stream2 = nullptr;  // copy stream of the host-array runner
+    Scratch sc2;                    // only its io set is used
     void* pin[2] = {};               // pinned staging blocks for the host-array API
     hipEvent_t pin_ev[2] = {};       // last DMA that used each block
     // Lane 0's scratch (sc) is shared by the host-array path (on `stream`) and the
@@ -124,6 +125,8 @@ struct Device {
     // this event before its first kernel and records it after its last one, so work
     // queued on different streams never overlaps on the same scratch.
     hipEvent_t sc_fence = nullptr;
+    hipEvent_t h2d_ev[2] = {};  // host-array runner: input of I/O set k landed
+    hipEvent_t k_ev[2] = {};    // host-array runner: kernels that use I/O set k done
 };
 
 // hipMalloc'd buffer owned by one scope (error paths free it too)
@@ -330,6 +333,8 @@ void free_device(Device& d) {
     for (int k = 0; k < 2; ++k) {
         if (d.pin_ev[k]) hipEventSynchronize(d.pin_ev[k]), hipEventDestroy(d.pin_ev[k]);
         if (d.pin[k]) hipHostFree(d.pin[k]);
+        if (d.h2d_ev[k]) hipEventDestroy(d.h2d_ev[k]);
+        if (d.k_ev[k]) hipEventDestroy(d.k_ev[k]);
     }
     if (d.stream) hipStreamDestroy(d.stream);
     if (d.stream2) hipStreamDestroy(d.stream2);
@@ -377,15 +382,6 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     return TFHE_OK;
 }
 
-tfhe_status ensure_io(Device& d, size_t words) {
-    if (words <= d.sc.io_words) return TFHE_OK;
-    hipFree(d.sc.io);
-    d.sc.io = nullptr, d.sc.io_words = 0;
-    HCHECK(hipMalloc(&d.sc.io, words * sizeof(uint64_t)));
-    d.sc.io_words = words;
-    return TFHE_OK;
-}
-
 // ---------------------------------------------------------------------------
 // device pipelines (one device, one stream, B <= scratch capacity)
 // ---------------------------------------------------------------------------
@@ -404,17 +400,21 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     return TFHE_OK;
 }
 
-// Smallest batch that takes the tiled key switch (TFHE_KS_TILED_MIN; 0 = never).  Below it
-// the per-ciphertext gather (k_mkm, split over several waves) has the better latency.
-size_t ks_tiled_min() {
+// Smallest batch that takes the tiled key switch (TFHE_KS_TILED_MIN overrides; 0 = never).
+// Below it the per-ciphertext gather (k_mkm, split over several waves) has the better
+// latency: the tiled kernel's workgroups each sweep all N dKS rows, ~1 ms for STD128 at any
+// batch up to 8192, while the u16 gather costs 1.87 ms per 8192 (crossover ~4400); for
+// u32/u64 keys the gather is 2-10x slower already at 1024 (profiles/r02_ks).
+size_t ks_tiled_min(int ksk_bits) {
     const char* e = std::getenv("TFHE_KS_TILED_MIN");  // read per call: tests and A/B runs switch it
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256;
+    if (e) return (size_t)std::strtoull(e, nullptr, 10);
+    return ksk_bits == 16 ? 4096 : 256;
 }
 
 // d.sc.ks must be sized for B (ensure_scratch) when the tiled form can run
 tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
     if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
-    const size_t tmin = ks_tiled_min();
+    const size_t tmin = ks_tiled_min(c->ksk_bits);
     if (tmin && B >= tmin && d.sc.ks && B <= d.sc.cap) {
         const hipError_t e = launch_ks_tiled(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb,
                                              ext, fmod, out, B, d.sc.ks, d.stream);
@@ -661,70 +661,82 @@ tfhe_status d2h_staged(Device& d, void* dst, const void* src, size_t bytes, hipS
 }
 
 // Host-array runner: in-arrays are [B][in_words] (up to 2), out [B][out_words].  Each
-// device's shard is cut into sub-batches that alternate between the device's two lanes:
-// sub-batch k's H2D copy and kernels are queued on its lane before the host waits for
-// sub-batch k-1's D2H, so the PCIe traffic of one overlaps the kernels of the other.
-// op(lane, in1, in2, out, count, index of the first ciphertext).
-constexpr size_t kMinSub = 1536;  // below this a sub-batch no longer fills the GPU
+// device's shard is cut into sub-batches.  Kernels run in order on the device's compute
+// stream (lane-0 scratch); copies run on its copy stream (stream2) into two alternating
+// device I/O sets, ordered by events: the kernels of k wait for H2D(k), D2H(k) waits for the
+// kernels of k, and H2D(k+2) follows D2H(k) on the copy stream (so it reuses k's I/O set only
+// after k's kernels and D2H are done).  The host queues H2D(k+1) and the kernels of k+1
+// before it drains D2H(k): the compute stream waits for PCIe only for the first sub-batch's
+// input and the last one's output.  op(device, in1, in2, out, count, index of the first
+// ciphertext) queues its kernels on d.stream.
+// Sub-batches per shard: 1 unless TFHE_HOST_PARTS asks for more.  Measured (STD128 NAND,
+// 8192, profiles/r02_host): one sub-batch 45.0 ms, 2: 46.2, 4: 51.5, 8: 59.7 -- the split
+// blind rotations (2048 workgroups each: a launch tail apiece), the key switches (~1 ms each at
+// any batch) and the runtime's blit kernels for the sub-8 MiB copies, which run beside the
+// blind rotation, cost more than the 3.4 ms of PCIe they hide.
+size_t host_parts(size_t cnt) {
+    const char* e = std::getenv("TFHE_HOST_PARTS");  // read per call (A/B runs)
+    const size_t want = e ? (size_t)std::max(1, std::atoi(e)) : 1;
+    return std::min(want, std::max<size_t>(1, cnt / 256));
+}
+
+tfhe_status ensure_io_set(Scratch& sc, size_t words) {
+    if (words <= sc.io_words) return TFHE_OK;
+    hipFree(sc.io);
+    sc.io = nullptr, sc.io_words = 0;
+    HCHECK(hipMalloc(&sc.io, words * sizeof(uint64_t)));
+    sc.io_words = words;
+    return TFHE_OK;
+}
+
 template <typename Op>
 tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
                           uint64_t* out, size_t wo, Op&& op) {
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        static const size_t max_parts = [] {
-            const char* e = std::getenv("TFHE_HOST_PARTS");
-            return e ? std::max(1, std::atoi(e)) : 1;  // measured: splitting loses more kernel efficiency than it hides
-        }();
-        const size_t parts = cnt >= 2 * kMinSub ? std::min<size_t>(max_parts, cnt / kMinSub) : 1;
+        const size_t parts = host_parts(cnt);
         const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
-        Device lane[2] = {d, d};
-        lane[1].stream = d.stream2, lane[1].sc = d.sc2;
-        const int nl = parts > 1 ? 2 : 1;
-        const size_t w_in2 = in2 ? w2 : 0;
-        tfhe_status st = TFHE_OK;
-        for (int l = 0; l < nl && st == TFHE_OK; ++l) {
-            st = ensure_scratch(c, lane[l], sub);
-            if (st == TFHE_OK) st = ensure_io(lane[l], sub * (w1 + w_in2 + wo));
-        }
-        d.sc = lane[0].sc;  // keep what was (re)allocated
-        d.sc2 = lane[1].sc;
-        if (st == TFHE_OK) st = sc_acquire(d, d.stream);
-        if (st != TFHE_OK) return st;
-        auto d2h = [&](int l, size_t off, size_t b) -> tfhe_status {
-            const uint64_t* dout = lane[l].sc.io + sub * (w1 + w_in2);
-            return d2h_staged(d, out + off * wo, dout, b * wo * 8, lane[l].stream);
-        };
+        const size_t w_in2 = in2 ? w2 : 0, io_words = sub * (w1 + w_in2 + wo);
+        SCHECK(ensure_scratch(c, d, sub));
+        SCHECK(ensure_io_set(d.sc, io_words));
+        SCHECK(ensure_io_set(d.sc2, io_words));
+        for (hipEvent_t* e : {&d.h2d_ev[0], &d.h2d_ev[1], &d.k_ev[0], &d.k_ev[1]})
+            if (!*e) HCHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        SCHECK(sc_acquire(d, d.stream));
+        const hipStream_t cs = d.stream, xs = d.stream2;
+        uint64_t* io[2] = {d.sc.io, d.sc2.io};
         static const bool trace = std::getenv("TFHE_TRACE") != nullptr;
         auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double t0 = trace ? now() : 0;
-        double t_h2d = 0, t_op = 0;
-        size_t prev_off = 0, prev_b = 0;
-        int prev_l = -1;
-        for (size_t k = 0, off = lo; off < lo + cnt && st == TFHE_OK; ++k, off += sub) {
-            const int l = (int)(k % nl);
-            const size_t b = std::min(sub, lo + cnt - off);
-            Device& L = lane[l];
-            if (prev_l == l) {  // one lane: its previous output must leave before its buffers are reused
-                st = d2h(prev_l, prev_off, prev_b);
-                prev_l = -1;
-                if (st != TFHE_OK) break;
-            }
-            uint64_t *din1 = L.sc.io, *din2 = in2 ? L.sc.io + sub * w1 : nullptr, *dout = L.sc.io + sub * (w1 + w_in2);
-            st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, L.stream);
-            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, L.stream);
+        auto dout_of = [&](int set) { return io[set] + sub * (w1 + w_in2); };
+        // D2H of sub-batch k (set k & 1): after its kernels, drained into `out` by the host
+        auto d2h = [&](size_t k) -> tfhe_status {
+            const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
+            const int set = (int)(k & 1);
+            HCHECK(hipStreamWaitEvent(xs, d.k_ev[set], 0));
+            return d2h_staged(d, out + off * wo, dout_of(set), b * wo * 8, xs);
+        };
+        tfhe_status st = TFHE_OK;
+        const size_t n_sub = (cnt + sub - 1) / sub;
+        for (size_t k = 0; k < n_sub && st == TFHE_OK; ++k) {
+            const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
+            const int set = (int)(k & 1);
+            uint64_t *din1 = io[set], *din2 = in2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
+            st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, xs);
+            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, xs);
             if (st != TFHE_OK) break;
-            if (trace) hipStreamSynchronize(L.stream), t_h2d = now() - t0;
-            st = op(L, din1, din2, dout, b, off);
-            if (trace) hipStreamSynchronize(L.stream), t_op = now() - t0;
+            HCHECK(hipEventRecord(d.h2d_ev[set], xs));
+            HCHECK(hipStreamWaitEvent(cs, d.h2d_ev[set], 0));
+            st = op(d, din1, din2, dout, b, off);
             if (st != TFHE_OK) break;
-            if (prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
-            prev_l = l, prev_off = off, prev_b = b;
+            HCHECK(hipEventRecord(d.k_ev[set], cs));
+            if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu queued at %.2f ms\n", k, now() - t0);
+            if (k > 0) st = d2h(k - 1);
         }
-        if (st == TFHE_OK && prev_l >= 0) st = d2h(prev_l, prev_off, prev_b);
-        hipStreamSynchronize(d.stream);
-        if (d.stream2) hipStreamSynchronize(d.stream2);
-        if (trace)
-            std::fprintf(stderr, "[tfhe] host batch %zu: h2d done %.2f ms, kernels done %.2f ms, d2h done %.2f ms\n", cnt,
-                         t_h2d, t_op, now() - t0);
+        if (st == TFHE_OK && n_sub > 0) st = d2h(n_sub - 1);
+        const hipError_t e1 = hipStreamSynchronize(cs), e2 = hipStreamSynchronize(xs);
+        if (trace) std::fprintf(stderr, "[tfhe] host batch %zu in %zu sub-batches: done %.2f ms\n", cnt, n_sub, now() - t0);
+        if (st == TFHE_OK && (e1 != hipSuccess || e2 != hipSuccess))
+            st = fail(TFHE_ERR_DEVICE, std::string("host batch: ") + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
         return st;
     });
 }
