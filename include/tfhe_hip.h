@@ -106,6 +106,7 @@ typedef struct tfhe_info {
 #define TFHE_BR_FAST 1         /* specialised STD128 kernel, blind_rotate_fast4.hip */
 #define TFHE_BR_F64 2          /* exact-FP64 kernel, blind_rotate_f64.hip */
 #define TFHE_BR_F64_FOLD 3     /* exact-FP64 kernel, top digit's transforms eliminated */
+#define TFHE_BR_RNS 4          /* four-prime RNS kernel (2^53 < Q < 2^58), blind_rotate_rns.hip */
 
 typedef struct tfhe_ctx tfhe_ctx;
 

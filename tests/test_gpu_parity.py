@@ -407,6 +407,39 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
 
 
 
+@pytest.mark.parametrize("arb,logq,path,kernel", [(True, 12, "rns", 4), (False, 23, "rns", 4), (True, 12, "generic", 0),
+                                                   (False, 23, "generic", 0)])
+def test_rns_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
+    """The logQ contexts (Q = 2^54 - 77823, N = 2048, throw = 1: C3 logQ=12 with one 27-bit digit
+    per polynomial, C5b logQ=23 with two 18-bit digits) run on the four-prime RNS kernel with
+    TFHE_RNS=1 (exact integer ring product, Garner CRT, Q's special form) and on the default
+    kernel otherwise; both equal the oracle, for accumulator boundary values (0, Q-1, the
+    centring threshold, the largest top digits) and several a-moduli."""
+    op = oracle.params_from_logq("STD128", arb, logq, 0, 0, 1)
+    cp = capi.params_from_logq("STD128", arb, logq, 0, 0, 1)
+    rs = np.random.default_rng(logq)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    bsk[: 4 * op.N] = np.array([0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1], dtype=np.uint64).repeat(op.N)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    if path == "rns":
+        os.environ["TFHE_RNS"] = "1"
+    try:
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    finally:
+        os.environ.pop("TFHE_RNS", None)
+    assert ctx.info().br_kernel == kernel
+    B = 3
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    half = op.Q >> 1
+    acc[0, :, :8] = [0, op.Q - 1, half, half + 1, half - 1, 1, op.Q - 2, half + 2]
+    acc[1] = np.where(rs.integers(0, 2, (2, op.N)) == 1, half, half + 1).astype(np.uint64)  # extreme digits
+    for amod in (op.q, 2 * op.N):
+        a = rs.integers(0, amod, (B, op.n), dtype=np.uint64)
+        assert np.array_equal(ctx.EvalAcc(a, amod, acc), orc.eval_acc(a, amod, acc))
+    ctx.GPUClean()
+    orc.close()
+
+
 @pytest.mark.parametrize("pset", ["STD128Q", "STD128Q_OPT"])
 def test_wrap_correction_late_round(capi, oracle, pset):
     """The STD128Q fold's WRAP correction in the LAST round (vote flag of round parity

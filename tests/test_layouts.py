@@ -31,3 +31,10 @@ def test_fast4_exchange_layouts():
     out = run_tool("lds_layouts4.py")
     ways = [int(w) for w in re.findall(r"max (\d+)-way", out)]
     assert len(ways) == 8 and max(ways) == 1, out
+
+
+def test_rns_kernel_magnitudes():
+    """blind_rotate_rns.hip: every int32 residue of the schedule stays below 2^31 and the CRT
+    range covers the exact ring product for the logQ contexts (C3, C5b)."""
+    out = run_tool("bounds_rns.py")
+    assert out.count("CRT range ok, int32 bounds ok") == 2, out

@@ -251,7 +251,11 @@ __device__ __forceinline__ uint32_t f64_tau() {
     return tau;
 }
 
-template <uint32_t TH, bool RED>
+template <bool NB>
+__device__ __forceinline__ void xbar() {
+    if constexpr (!NB) __syncthreads();
+}
+template <uint32_t TH, bool RED, bool NB = false>
 __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], const double* psi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
@@ -264,19 +268,19 @@ __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], con
 #pragma unroll
         for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
     }
-    __syncthreads();
+    xbar<NB>();
     {
         uint32_t ad[8];
         ad_B(tau, ad);
         f64_r8_fwd<RED>(p, ad, 8, tau >> 5, psi, K);
     }
-    __syncthreads();
+    xbar<NB>();
     {
         uint32_t ad[8];
         ad_C(tau, ad);
         f64_r8_fwd<RED>(p, ad, 64, tau >> 2, psi, K);
     }
-    __syncthreads();
+    xbar<NB>();
 #pragma unroll
     for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
         const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
@@ -288,10 +292,10 @@ __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], con
         if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
     }
-    __syncthreads();
+    xbar<NB>();
 }
 
-template <uint32_t TH, bool RED>
+template <uint32_t TH, bool RED, bool NB = false>
 __device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], const double* ipsi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
@@ -308,19 +312,19 @@ __device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], con
         if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
     }
-    __syncthreads();
+    xbar<NB>();
     {
         uint32_t ad[8];
         ad_C(tau, ad);
         f64_r8_inv<RED>(p, ad, 256, tau >> 2, ipsi, K);
     }
-    __syncthreads();
+    xbar<NB>();
     {
         uint32_t ad[8];
         ad_B(tau, ad);
         f64_r8_inv<RED>(p, ad, 32, tau >> 5, ipsi, K);
     }
-    __syncthreads();
+    xbar<NB>();
     {  // pass A: v = elements tau + 256k of polynomial t >> 8, left in registers
         uint32_t ad[8];
         ad_A(tau, ad);
@@ -344,7 +348,9 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 // instead (thread t: polynomial t >> 8, coefficients (t & 255) + 256q, q < 8), so the digits
 // enter the forward transform and the inverse transform's output enters the accumulator
 // update in registers; the products (C', sums, monomials) keep the slot layout.
-template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false>
+// EXP (timing experiments, results invalid): 1 = every round reads the keys of round i & 7
+// (L2-resident), 2 = of round i & 63 (MALL-resident), 4 = no barriers inside the transforms
+template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, int EXP = 0>
 __global__ void __launch_bounds__(TH, 4)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -425,7 +431,8 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0.0;
-        const double* ek = bsk + (size_t)i * round_words;
+        const uint32_t ki = EXP == 1 ? (i & 7) : EXP == 2 ? (i & 63) : i;
+        const double* ek = bsk + (size_t)ki * round_words;
         // One digit: extraction (registers), forward transform, products with rows 2l, 2l+1.
         // CHECK (WRAP, digit 0): also raise the round's vote, wflag[i & 1], published by the
         // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
@@ -465,7 +472,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             }
             if constexpr (AM) {
                 // no barrier before: pass A writes this thread's own entries
-                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
+                f64_ntt_fwd2048<TH, RED, (EXP & 4) != 0>(buf, v, psi, K);
             } else {
                 __syncthreads();
                 f64_ntt_fwd<N, TH, RED>(buf, psi, K);
@@ -540,7 +547,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         }
         __syncthreads();
         double v[8];
-        if constexpr (AM) f64_ntt_inv2048<TH, RED>(buf, v, ipsi, K);
+        if constexpr (AM) f64_ntt_inv2048<TH, RED, (EXP & 4) != 0>(buf, v, ipsi, K);
         else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
@@ -683,6 +690,18 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
                            amod, acc);
     };
     const bool red = P.Q >= (1ull << 40);
+    // TFHE_F64_EXP (timing only, TFHE_TIMING_EXPERIMENTS=1): key-stream locality experiments, N = 2048
+    static const int exp = [] {
+        const char* e = std::getenv("TFHE_F64_EXP");
+        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+        return (e && x && x[0] == '1') ? std::atoi(e) : 0;
+    }();
+    if (exp && P.N == 2048) {
+        if (wrap && red) exp == 1 ? go(k_blind_rotate_f64<512, 4, true, true, true, 1>) : exp == 2 ? go(k_blind_rotate_f64<512, 4, true, true, true, 2>) : go(k_blind_rotate_f64<512, 4, true, true, true, 4>);
+        else if (fold && !red) exp == 1 ? go(k_blind_rotate_f64<512, 4, false, true, false, 1>) : exp == 2 ? go(k_blind_rotate_f64<512, 4, false, true, false, 2>) : go(k_blind_rotate_f64<512, 4, false, true, false, 4>);
+        else return hipErrorNotSupported;
+        return hipGetLastError();
+    }
     if (wrap) {
         if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, true, true>) : go(k_blind_rotate_f64<256, 4, false, true, true>);
         else red ? go(k_blind_rotate_f64<512, 4, true, true, true>) : go(k_blind_rotate_f64<512, 4, false, true, true>);

@@ -527,7 +527,9 @@ __device__ __forceinline__ void g3_ntt_inv(W* buf, W (&v)[8], const G3Tw<W>& T, 
     g3_inv_core(v, 4, 0, T, Q2, Q);
 }
 
-template <typename W>
+// EXP (timing experiments, results invalid): 1 = every round reads the keys of round i & 7
+// (L2-resident), 2 = of round i & 63
+template <typename W, int EXP = 0>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__ psi_sh,
                     const W* __restrict__ ipsi, const W* __restrict__ ipsi_sh,
@@ -574,8 +576,9 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0;
-        const W* ek = bsk + (size_t)i * round_words;
-        const W* eks = bsk_sh + (size_t)i * round_words;
+        const uint32_t ki = EXP == 1 ? (i & 7) : EXP == 2 ? (i & 63) : i;
+        const W* ek = bsk + (size_t)ki * round_words;
+        const W* eks = bsk_sh + (size_t)ki * round_words;
         for (uint32_t l = 0; l < P.digits; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
@@ -674,9 +677,14 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
     }();
     if (!v1 && !no_gen3 && P.N == G3_N) {
         const size_t lds = (size_t)4 * G3_N * wb;  // two polynomials + forward twiddles
+        static const int exp = [] {  // TFHE_GEN3_EXP: timing only (TFHE_TIMING_EXPERIMENTS=1)
+            const char* e = std::getenv("TFHE_GEN3_EXP");
+            const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+            return (e && x && x[0] == '1') ? std::atoi(e) : 0;
+        }();
         auto go3 = [&](auto tag) {
             using W = decltype(tag);
-            auto kern = k_blind_rotate_gen3<W>;
+            auto kern = exp == 1 ? k_blind_rotate_gen3<W, 1> : exp == 2 ? k_blind_rotate_gen3<W, 2> : k_blind_rotate_gen3<W, 0>;
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, (const W*)T.psi, (const W*)T.psi_sh,
                                (const W*)T.ipsi, (const W*)T.ipsi_sh, (const W*)T.mono, (const W*)T.mono_sh, T.eidx,
