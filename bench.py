@@ -296,7 +296,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "data": "synthetic",
             "dtype": {0: "u32" if int(ctx.info().word_bits) == 32 else "u64", 1: "u32", 2: "f64",
-                      3: "f64", 4: "i32"}[int(ctx.info().br_kernel)],
+                      3: "f64", 4: "i32", 5: "u64"}[int(ctx.info().br_kernel)],
             "config": {"workload": f"{args.params} GINX EvalBinGate(NAND), inputs resident in HBM",
                        "global_batch": B * world, "batch_per_gpu": B, "n": p.n, "N": p.N, "Q": p.Q,
                        "dG2": p.dG2, "parallelism": f"shard{world}"},

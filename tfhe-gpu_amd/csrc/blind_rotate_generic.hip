@@ -660,6 +660,283 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// gen3sf: gen3 for Q = 2^54 - c, c < 2^20 (the logQ / arbFunc contexts, Q = 2^54 - 77823: C3,
+// C5b).  Every constant w (twiddle, key, monomial) is held as W0 = w and W1 = w 2^31 mod Q (the
+// same 16 bytes as a word and its Shoup companion), and a product of a lazily reduced
+// a < 2^61 with w is
+//     a w = a0 W0 + a1 W1 (mod Q),  a0 = a mod 2^31, a1 = a >> 31:   S = H 2^32 + P.lo < 2^86
+//     r = (S mod 2^54) + (S >> 54) c  < 2^54 + 2^32 c
+// -- five v_mad_u64_u32 and no quotient estimate, against ten multiplies for the u64 Shoup
+// product.  Values stay unsigned and lazy: the forward transform needs no reduction at all
+// (y' = x + 2Q - v, 11 stages < 23 Q), the inverse folds its pure sums once per pass
+// (x -> (x mod 2^54) + (x >> 54) c, one mad), the accumulator update folds once and subtracts
+// Q at most once.  tools/bounds_sf.py checks every bound of this schedule.
+constexpr uint32_t SF_K = 54;
+
+struct SfC {
+    uint64_t Q, Q2, Q9;  // Q, 2Q (forward offset), 9Q (inverse offset)
+    uint32_t c;
+};
+
+__device__ __forceinline__ uint64_t sf_mul(uint64_t a, uint64_t w0, uint64_t w1, uint32_t c) {
+    const uint32_t a0 = (uint32_t)a & 0x7fffffffu, a1 = (uint32_t)(a >> 31);  // a1 < 2^30
+    uint64_t P = (uint64_t)a0 * (uint32_t)w0;
+    P += (uint64_t)a1 * (uint32_t)w1;                                        // < 2^64
+    uint64_t H = (uint64_t)a0 * (uint32_t)(w0 >> 32) + (P >> 32);
+    H += (uint64_t)a1 * (uint32_t)(w1 >> 32);                                // < 2^54
+    const uint32_t hs = (uint32_t)(H >> (SF_K - 32));
+    const uint64_t L = ((H & ((1ull << (SF_K - 32)) - 1)) << 32) | (uint32_t)P;
+    return L + (uint64_t)hs * c;
+}
+__device__ __forceinline__ uint64_t sf_fold(uint64_t x, uint32_t c) {
+    return (x & ((1ull << SF_K) - 1)) + (uint64_t)(uint32_t)(x >> SF_K) * c;
+}
+
+struct SfTw {
+    const uint64_t* __restrict__ w0;
+    const uint64_t* __restrict__ w1;
+};
+
+__device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const SfTw& T, uint32_t i, const SfC& K) {
+    const uint64_t v = sf_mul(y, T.w0[i], T.w1[i], K.c);
+    y = x + (K.Q2 - v);
+    x = x + v;
+}
+template <bool FOLD = false>
+__device__ __forceinline__ void sf_gs(uint64_t& x, uint64_t& y, const SfTw& T, uint32_t i, const SfC& K) {
+    const uint64_t d = x + (K.Q9 - y), s = x + y;
+    x = FOLD ? sf_fold(s, K.c) : s;
+    y = sf_mul(d, T.w0[i], T.w1[i], K.c);
+}
+
+__device__ __forceinline__ void sf_fwd_core(uint64_t (&v)[8], uint32_t m0, uint32_t g, const SfTw& T, const SfC& K) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sf_ct(v[k], v[k + 4], T, m0 + g, K);
+    sf_ct(v[0], v[2], T, 2 * m0 + 2 * g, K), sf_ct(v[1], v[3], T, 2 * m0 + 2 * g, K);
+    sf_ct(v[4], v[6], T, 2 * m0 + 2 * g + 1, K), sf_ct(v[5], v[7], T, 2 * m0 + 2 * g + 1, K);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sf_ct(v[2 * j], v[2 * j + 1], T, 4 * m0 + 4 * g + j, K);
+}
+// FOLD: fold the last stage's sums (inverse passes C and B; bounds_sf.py INV_FOLD_PASS)
+template <bool FOLD>
+__device__ __forceinline__ void sf_inv_core(uint64_t (&v)[8], uint32_t m, uint32_t g, const SfTw& T, const SfC& K) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sf_gs(v[2 * j], v[2 * j + 1], T, m + 4 * g + j, K);
+    sf_gs(v[0], v[2], T, (m >> 1) + 2 * g, K), sf_gs(v[1], v[3], T, (m >> 1) + 2 * g, K);
+    sf_gs(v[4], v[6], T, (m >> 1) + 2 * g + 1, K), sf_gs(v[5], v[7], T, (m >> 1) + 2 * g + 1, K);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sf_gs<FOLD>(v[k], v[k + 4], T, (m >> 2) + g, K);
+}
+
+__device__ __forceinline__ void sf_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], const SfTw& T, const SfC& K) {
+    constexpr uint32_t N = G3_N;
+    const uint32_t tau = g3_tau();
+    uint64_t* p = buf + (threadIdx.x >> 8) * N;
+    {
+        uint32_t ad[8];
+        g3_ad(0, tau, ad);
+        sf_fwd_core(v, 1, 0, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 1; pass <= 2; ++pass) {
+        uint32_t ad[8];
+        g3_ad(pass, tau, ad);
+        uint64_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = p[ad[k]];
+        if (pass == 1) sf_fwd_core(w, 8, tau >> 5, T, K);
+        else sf_fwd_core(w, 64, tau >> 2, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = w[k];
+        __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
+        const uint32_t u = tau + 256 * r, u0 = g3_swz(4 * u);
+        uint64_t v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        sf_ct(v0, v2, T, N / 4 + u, K), sf_ct(v1, v3, T, N / 4 + u, K);
+        sf_ct(v0, v1, T, N / 2 + 2 * u, K), sf_ct(v2, v3, T, N / 2 + 2 * u + 1, K);
+        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void sf_ntt_inv(uint64_t* buf, uint64_t (&v)[8], const SfTw& T, const SfC& K) {
+    constexpr uint32_t N = G3_N;
+    const uint32_t tau = g3_tau();
+    uint64_t* p = buf + (threadIdx.x >> 8) * N;
+#pragma unroll
+    for (uint32_t r = 0; r < 2; ++r) {  // h = 1 then h = 2 on units 4u .. 4u+3; the second stage's sums folded
+        const uint32_t u = tau + 256 * r, u0 = g3_swz(4 * u);
+        uint64_t v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
+        sf_gs(v0, v1, T, N / 2 + 2 * u, K), sf_gs(v2, v3, T, N / 2 + 2 * u + 1, K);
+        sf_gs<true>(v0, v2, T, N / 4 + u, K), sf_gs<true>(v1, v3, T, N / 4 + u, K);
+        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 2; pass >= 1; --pass) {
+        uint32_t ad[8];
+        g3_ad(pass, tau, ad);
+        uint64_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = p[ad[k]];
+        if (pass == 2) sf_inv_core<true>(w, 256, tau >> 2, T, K);
+        else sf_inv_core<true>(w, 32, tau >> 5, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = w[k];
+        __syncthreads();
+    }
+    uint32_t ad[8];
+    g3_ad(0, tau, ad);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
+    sf_inv_core<false>(v, 4, 0, T, K);  // outputs < 8.2 Q: the accumulator update folds
+}
+
+// keys / monomials / inverse twiddles: W0 = the generic arena's words, W1 from sf1 (the same
+// layout); forward twiddles (W0, W1) in LDS
+__global__ void __launch_bounds__(G3_TH, 4)
+k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
+                      const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                      const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                      const uint32_t* __restrict__ eidx, const uint64_t* __restrict__ bsk,
+                      const uint64_t* __restrict__ bsk1, const uint64_t* __restrict__ a, uint64_t amod,
+                      uint64_t* __restrict__ acc_io) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = G3_N, TH = G3_TH, CN = G3_CN;
+    uint64_t* buf = reinterpret_cast<uint64_t*>(smem);  // [2][N], swizzled
+    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const uint32_t ts = g3_swz(t);
+    const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    uint64_t* psi_l = buf + 2 * N;
+    uint64_t* psi1_l = psi_l + N;
+    for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
+    const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
+    uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
+    const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
+    const uint64_t scale = (uint64_t)twoN / amod;
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
+
+    uint64_t acc[2][CN];  // canonical [0, Q)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint64_t v = g[lpos(p, k)];
+            acc[p][k] = v >= Q ? v % Q : v;
+        }
+    __syncthreads();  // forward twiddles in LDS
+
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        uint64_t A[2][2][CN];  // A_kj per owned slot (< 2.1 Q per digit)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) A[kk][j][k] = 0;
+        const uint64_t* ek = bsk + (size_t)i * round_words;
+        const uint64_t* ek1 = bsk1 + (size_t)i * round_words;
+        for (uint32_t l = 0; l < P.digits; ++l) {
+            const uint32_t lt = l + P.thr, shift = lt * logG;
+            int64_t Kd = 0;
+            for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
+            uint64_t v[8];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const uint64_t x = acc[p][k];
+                    const int64_t c = x < Qhalf ? (int64_t)x : (int64_t)x - Qs;
+                    const int64_t d = (c + Kd) >> shift;
+                    int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    if (r < 0) r += Qs;
+                    v[p * CN + k] = (uint64_t)r;
+                }
+            sf_ntt_fwd(buf, v, TF, K);  // pass A writes this thread's own entries: no barrier before
+            // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both columns; group g = (slot k, key kk)
+            // holds 4 (W0, W1) key pairs, the next group's are loaded before this group's arithmetic
+            constexpr int NG = CN * 2;
+            auto kload = [&](int g, uint64_t (&kv)[8]) {
+                const uint32_t x = t + TH * (g >> 1), kk = g & 1;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const size_t o = ((size_t)(kk * P.dG2 + 2 * l + r) * 2 + j) * N + x;
+                        kv[(j * 2 + r) * 2] = ek[o];
+                        kv[(j * 2 + r) * 2 + 1] = ek1[o];
+                    }
+            };
+            uint64_t kv[2][8];
+            kload(0, kv[0]);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g + 1 < NG) kload(g + 1, kv[(g + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int k = g >> 1, kk = g & 1;
+                const uint64_t d0 = buf[ts + TH * k], d1 = buf[N + ts + TH * k];
+                const uint64_t(&c)[8] = kv[g & 1];
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    A[kk][j][k] += sf_mul(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], K.c) +
+                                   sf_mul(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], K.c);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();  // the next pass A rewrites entries other threads' products read
+        }
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint32_t x = t + TH * k;
+            const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
+            const uint64_t mp = mono[ip], mp1 = mono1[ip], mn = mono[in], mn1 = mono1[in];
+            buf[ts + TH * k] = sf_mul(A[0][0][k], mp, mp1, K.c) + sf_mul(A[1][0][k], mn, mn1, K.c);
+            buf[N + ts + TH * k] = sf_mul(A[0][1][k], mp, mp1, K.c) + sf_mul(A[1][1][k], mn, mn1, K.c);
+        }
+        __syncthreads();
+        uint64_t v[8];
+        sf_ntt_inv(buf, v, TI, K);  // outputs < 8.2 Q
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const uint64_t x = sf_fold(acc[p][k] + v[p * CN + k], K.c);  // < 2Q
+                acc[p][k] = x >= Q ? x - Q : x;
+            }
+    }
+    __syncthreads();  // every last inverse pass has read its entries
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = acc[p][k];
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
+        const uint64_t v = buf[k == 0 ? 0 : N - k];
+        g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+        g[N + k] = buf[N + k];
+    }
+}
+
+// W1 = w 2^31 mod Q for w < Q: w 2^31 = (w >> 23) 2^54 + (w mod 2^23) 2^31
+__global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ in, size_t words,
+                          uint64_t* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= words) return;
+    const uint64_t w = in[i] % Q;
+    const uint64_t x = ((w & ((1ull << (SF_K - 31)) - 1)) << 31) + (w >> (SF_K - 31)) * c;
+    out[i] = x >= Q ? x - Q : x;
+}
+
 }  // namespace
 
 hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const DevTables& T, const void* bsk,
@@ -728,6 +1005,47 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
                            (const uint64_t*)T.mono_sh, T.eidx, (const uint64_t*)bsk, (const uint64_t*)bsk_sh, a, amod,
                            acc);
     }
+    return hipGetLastError();
+}
+
+}  // namespace tfhe
+
+namespace tfhe {
+
+bool sf_path_supported(const BRParams& P, int word_bits) {
+    return word_bits == 64 && P.N == G3_N && P.Q < (1ull << SF_K) && P.Q > (1ull << SF_K) - (1ull << 20) &&
+           P.logG < 64 && P.n > 0;
+}
+
+// W1 arrays behind the arena's W0 ones: psi [N], ipsi [N], mono [2N], bsk [n][2][dG2][2][N]
+size_t sf_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
+
+hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s) {
+    if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
+    const uint32_t c = (uint32_t)((1ull << SF_K) - P.Q);
+    uint64_t* o = (uint64_t*)out;
+    const size_t words = (size_t)P.n * 4 * P.dG2 * P.N;
+    struct Part { const void* src; size_t n; size_t off; } parts[] = {
+        {T.psi, P.N, 0}, {T.ipsi, P.N, P.N}, {T.mono, 2ull * P.N, 2ull * P.N}, {bsk, words, 4ull * P.N}};
+    for (const Part& q : parts)
+        hipLaunchKernelGGL(k_pack_sf, dim3((unsigned)((q.n + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, c,
+                           (const uint64_t*)q.src, q.n, o + q.off);
+    return hipGetLastError();
+}
+
+hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
+                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
+    SfC K;
+    K.Q = P.Q, K.Q2 = 2 * P.Q, K.Q9 = 9 * P.Q;
+    K.c = (uint32_t)((1ull << SF_K) - P.Q);
+    const uint64_t* w1 = (const uint64_t*)sf;
+    const size_t lds = (size_t)4 * G3_N * 8;  // two polynomials + forward twiddles (W0, W1)
+    (void)hipFuncSetAttribute((const void*)k_blind_rotate_gen3sf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_blind_rotate_gen3sf, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
+                       (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N, T.eidx,
+                       (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
     return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ struct Device {
     void* bsk_fast = nullptr;
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
     void* keys_rns = nullptr;  // RNS path: prime tables + residue BSK
+    void* keys_sf = nullptr;   // special-form path: W1 = w 2^31 mod Q of the arena's tables and BSK
     Scratch sc;
     DevTables tables{};
     hipStream_t stream2 = nullptr;  // copy stream of the host-array runner
@@ -161,7 +162,8 @@ struct tfhe_ctx {
     bool use_fast = false;
     bool use_f64 = false;
     bool f64_fold = false;  // exact-FP64 kernel with the top digit's transforms eliminated
-    bool use_rns = false;   // four-prime RNS kernel (logQ / arbFunc contexts)
+    bool use_rns = false;   // four-prime RNS kernel (logQ / arbFunc contexts, opt-in)
+    bool use_sf = false;    // special-form u64 kernel (logQ / arbFunc contexts, default)
     BRParams br{};
     KSParams ks{};
     ArenaLayout layout{};
@@ -206,6 +208,10 @@ tfhe_status init_derived(tfhe_ctx* c) {
     const char* rns = std::getenv("TFHE_RNS");
     c->use_rns = !c->use_fast && !c->use_f64 && c->word_bits == 64 && rns_path_supported(c->br) &&
                  !(force && force[0] == '1') && rns && rns[0] == '1';
+    // Q = 2^54 - c: the special-form kernel (TFHE_SF=0 keeps the Shoup gen3 kernel)
+    const char* sfe = std::getenv("TFHE_SF");
+    c->use_sf = !c->use_fast && !c->use_f64 && !c->use_rns && sf_path_supported(c->br, c->word_bits) &&
+                !(force && force[0] == '1') && !(sfe && sfe[0] == '0');
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
         return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
     if (p.baseKS > 256) return fail(TFHE_ERR_UNSUPPORTED, "baseKS > 256 not supported");
@@ -317,6 +323,11 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
         HCHECK(launch_pack_bsk_f64(c->br, d.tables, d.arena + c->layout.bsk, c->f64_fold, d.keys_f64, d.stream));
         HCHECK(hipStreamSynchronize(d.stream));
     }
+    if (c->use_sf) {
+        HCHECK(hipMalloc(&d.keys_sf, sf_bytes(c->br)));
+        HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
+        HCHECK(hipStreamSynchronize(d.stream));
+    }
     if (c->use_rns) {
         HCHECK(hipMalloc(&d.keys_rns, rns_keys_bytes(c->br)));
         HCHECK(launch_pack_bsk_rns(c->br, d.tables, d.arena + c->layout.bsk, d.keys_rns, d.stream));
@@ -334,6 +345,7 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     hipFree(d.keys_rns);
+    hipFree(d.keys_sf);
     if (d.stream2) hipStreamSynchronize(d.stream2);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
@@ -407,6 +419,8 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
         HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream));
     } else if (c->use_rns) {
         HCHECK(launch_blind_rotate_rns(c->br, d.tables, d.keys_rns, a, amod, acc, B, d.stream));
+    } else if (c->use_sf) {
+        HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
                                            amod, acc, B, d.stream));
@@ -1025,13 +1039,15 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
         out->num_devices = (int)c->devs.size();
         out->word_bits = c->word_bits;
         out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0) +
-                                (c->use_f64 ? bsk_f64_bytes(c->br) : 0) + (c->use_rns ? rns_keys_bytes(c->br) : 0);
+                                (c->use_f64 ? bsk_f64_bytes(c->br) : 0) + (c->use_rns ? rns_keys_bytes(c->br) : 0) +
+                                (c->use_sf ? sf_bytes(c->br) : 0);
         out->ksk_device_bytes = c->layout.total - c->layout.ksk;
         out->bootstraps = c->bootstraps.load();
         out->key_image_bytes = c->layout.total;
         out->br_kernel = c->use_fast  ? TFHE_BR_FAST
                          : c->use_f64 ? (c->f64_fold ? TFHE_BR_F64_FOLD : TFHE_BR_F64)
                          : c->use_rns ? TFHE_BR_RNS
+                         : c->use_sf  ? TFHE_BR_SF
                                       : TFHE_BR_GENERIC;
         return TFHE_OK;
     });

@@ -65,6 +65,15 @@ hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold, const uint64_t* a,
                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
 
+// Special-form u64 blind rotation (gen3sf, blind_rotate_generic.hip) for N = 2048 and
+// Q = 2^54 - c, c < 2^20 (the logQ / arbFunc contexts): constants as (w, w 2^31 mod Q), five
+// multiplies per product.  sf: the W1 arrays (psi, ipsi, mono, bsk) derived on device.
+bool sf_path_supported(const BRParams& P, int word_bits);
+size_t sf_bytes(const BRParams& P);
+hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
+hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
+                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+
 // RNS blind rotation (blind_rotate_rns.hip) for N = 2048, 2^53 < Q < 2^58 of the form 2^k - c (the
 // logQ / arbFunc contexts): four 26-bit NTT primes, signed 32-bit Montgomery arithmetic, exact
 // integer ring product, Garner CRT back to Q.  Keys derived on device from the generic u64 arena.

@@ -75,7 +75,7 @@ def main():
         print(json.dumps({
             "config": name, "op": op, "batch": B, "params": {"n": p.n, "N": p.N, "Q": p.Q, "dG2": p.dG2,
                                                               "baseG": p.baseG, "qKS": p.qKS},
-            "kernel": ["generic", "fast", "f64", "f64-fold", "rns"][info.br_kernel],
+            "kernel": ["generic", "fast", "f64", "f64-fold", "rns", "sf"][info.br_kernel],
             "bootstraps_per_call": nb // args.reps, "bootstraps_per_s": round(nb / dt, 1),
             "calls_per_s": round(args.reps / dt, 3), "note": "host-array API, PCIe transfers included",
             "setup_s": round(setup_s, 1)}), flush=True)
