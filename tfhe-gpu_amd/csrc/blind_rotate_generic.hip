@@ -927,6 +927,229 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     }
 }
 
+// ---------------------------------------------------------------------------
+// sf2: gen3sf with wave-local passes.  Wave w (of 8) owns the 256-element block w of BOTH
+// polynomials after the forward transform's first pass: pass A (stages 0-2, elements
+// tau + 256k) is the only exchange across wavefronts; passes B (3-5) and C (6-8) and the units
+// (9-10) of block w run in wave w (lane l: polynomial l >> 5, sub-block index 32w + (l & 31);
+// units u = 64w + l of both polynomials), with no workgroup barrier in between.  The units leave
+// slots 4u .. 4u+3 of both polynomials in registers, so the products, the monomial factors and
+// the inverse units run in registers (the key rows are 32 contiguous bytes per lane), and the
+// inverse mirrors it: units, passes C and B in wave w, one barrier, pass A.  Barriers per round:
+// one per forward transform, one more before each further digit's pass A (other waves may still
+// read their blocks), one per inverse -- 2 for C3 and 4 for C5b instead of 9 and 14.
+// tools/lds_layouts_wl.py checks the index algebra, the wave-locality and the banks.
+__device__ __forceinline__ void wl_sync() {  // order this wave's LDS accesses (in-order LDS unit)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// forward: pass A from registers (polynomial t >> 8), barrier, B and C wave-local; then the units
+// of u = 64w + l for both polynomials into d[p][j] = slot 4u + j
+__device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uint64_t (&d)[2][4], const SfTw& T,
+                                            const SfC& K) {
+    constexpr uint32_t N = G3_N;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    {
+        const uint32_t tau = g3_tau();
+        uint64_t* p = buf + (t >> 8) * N;
+        uint32_t ad[8];
+        g3_ad(0, tau, ad);
+        sf_fwd_core(v, 1, 0, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = v[k];
+    }
+    __syncthreads();
+    uint32_t tw = (w << 5) | (l & 31);
+    asm volatile("" : "+v"(tw));
+    uint64_t* p = buf + (l >> 5) * N;
+#pragma unroll
+    for (int pass = 1; pass <= 2; ++pass) {
+        uint32_t ad[8];
+        g3_ad(pass, tw, ad);
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = p[ad[k]];
+        if (pass == 1) sf_fwd_core(x, 8, tw >> 5, T, K);
+        else sf_fwd_core(x, 64, tw >> 2, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = x[k];
+        wl_sync();
+    }
+    const uint32_t u = (w << 6) | l, u0 = g3_swz(4 * u);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // stages 9 (h = 2) and 10 (h = 1) on slots 4u .. 4u+3
+        const uint64_t* pq = buf + q * N;
+        uint64_t v0 = pq[u0], v1 = pq[u0 ^ 1], v2 = pq[u0 ^ 2], v3 = pq[u0 ^ 3];
+        sf_ct(v0, v2, T, N / 4 + u, K), sf_ct(v1, v3, T, N / 4 + u, K);
+        sf_ct(v0, v1, T, N / 2 + 2 * u, K), sf_ct(v2, v3, T, N / 2 + 2 * u + 1, K);
+        d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+    }
+}
+
+// inverse: units of slots 4u .. 4u+3 from registers (second stage's sums folded), C and B
+// wave-local (last stage's sums folded), barrier, pass A into v (polynomial t >> 8, < 8.2 Q)
+__device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], uint64_t (&v)[8], const SfTw& T,
+                                            const SfC& K) {
+    constexpr uint32_t N = G3_N;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t u = (w << 6) | l, u0 = g3_swz(4 * u);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        uint64_t* pq = buf + q * N;
+        uint64_t v0 = s[q][0], v1 = s[q][1], v2 = s[q][2], v3 = s[q][3];
+        sf_gs(v0, v1, T, N / 2 + 2 * u, K), sf_gs(v2, v3, T, N / 2 + 2 * u + 1, K);
+        sf_gs<true>(v0, v2, T, N / 4 + u, K), sf_gs<true>(v1, v3, T, N / 4 + u, K);
+        pq[u0] = v0, pq[u0 ^ 1] = v1, pq[u0 ^ 2] = v2, pq[u0 ^ 3] = v3;
+    }
+    wl_sync();
+    uint32_t tw = (w << 5) | (l & 31);
+    asm volatile("" : "+v"(tw));
+    uint64_t* p = buf + (l >> 5) * N;
+#pragma unroll
+    for (int pass = 2; pass >= 1; --pass) {
+        uint32_t ad[8];
+        g3_ad(pass, tw, ad);
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = p[ad[k]];
+        if (pass == 2) sf_inv_core<true>(x, 256, tw >> 2, T, K);
+        else sf_inv_core<true>(x, 32, tw >> 5, T, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = x[k];
+        if (pass == 2) wl_sync();
+    }
+    __syncthreads();
+    const uint32_t tau = g3_tau();
+    const uint64_t* pa = buf + (t >> 8) * N;
+    uint32_t ad[8];
+    g3_ad(0, tau, ad);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = pa[ad[k]];
+    sf_inv_core<false>(v, 4, 0, T, K);
+}
+
+template <int DIG>
+__global__ void __launch_bounds__(G3_TH, 4)
+k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
+                   const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                   const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                   const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
+                   const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = G3_N, TH = G3_TH, CN = G3_CN;
+    uint64_t* buf = reinterpret_cast<uint64_t*>(smem);  // [2][N], swizzled
+    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    uint64_t* psi_l = buf + 2 * N;
+    uint64_t* psi1_l = psi_l + N;
+    for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
+    const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
+    uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
+    const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
+    const uint64_t scale = (uint64_t)twoN / amod;
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
+    uint32_t ex[4];  // slot x evaluates at psi^(2 bitrev(x) + 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ex[j] = 2 * (__builtin_bitreverse32(u4 + j) >> 21) + 1;
+    auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
+
+    uint64_t acc[2][CN];  // canonical [0, Q), pass A's layout
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint64_t v = g[lpos(p, k)];
+            acc[p][k] = v >= Q ? v % Q : v;
+        }
+    __syncthreads();  // forward twiddles in LDS
+
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        uint64_t A[2][2][4];  // A_kj of slots u4 + j (< 2.1 Q per digit)
+        const uint64_t* ek = bsk + (size_t)i * round_words + u4;
+        const uint64_t* ek1 = bsk1 + (size_t)i * round_words + u4;
+#pragma unroll
+        for (int l = 0; l < DIG; ++l) {
+            const uint32_t lt = l + P.thr, shift = lt * logG;
+            int64_t Kd = 0;
+            for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
+            uint64_t v[8];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const uint64_t x = acc[p][k];
+                    const int64_t c = x < Qhalf ? (int64_t)x : (int64_t)x - Qs;
+                    const int64_t d = (c + Kd) >> shift;
+                    int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    if (r < 0) r += Qs;
+                    v[p * CN + k] = (uint64_t)r;
+                }
+            if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
+            uint64_t D[2][4];
+            sf2_ntt_fwd(buf, v, D, TF, K);
+            // products: group g = (key kk, column j, row r = 2l + polynomial) = 4 slots x (W0, W1);
+            // the next group's words are loaded before this group's arithmetic
+            auto kload = [&](int g, uint64_t (&kw)[8]) {
+                const uint32_t kk = g >> 2, j = (g >> 1) & 1, r = g & 1;
+                const size_t o = ((size_t)(kk * P.dG2 + 2 * l + r) * 2 + j) * N;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) kw[s] = ek[o + s], kw[4 + s] = ek1[o + s];
+            };
+            uint64_t kw[2][8];
+            kload(0, kw[0]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (g + 1 < 8) kload(g + 1, kw[(g + 1) & 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                const int kk = g >> 2, j = (g >> 1) & 1, r = g & 1;
+                const uint64_t(&c)[8] = kw[g & 1];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const uint64_t prod = sf_mul(D[r][s], c[s], c[4 + s], K.c);
+                    A[kk][j][s] = (l == 0 && r == 0) ? prod : A[kk][j][s] + prod;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        uint64_t S[2][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t ip = (ex[s] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
+            const uint64_t mp = mono[ip], mp1 = mono1[ip], mn = mono[in], mn1 = mono1[in];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                S[j][s] = sf_mul(A[0][j][s], mp, mp1, K.c) + sf_mul(A[1][j][s], mn, mn1, K.c);
+        }
+        uint64_t v[8];
+        sf2_ntt_inv(buf, S, v, TI, K);  // outputs < 8.2 Q
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const uint64_t x = sf_fold(acc[p][k] + v[p * CN + k], K.c);  // < 2Q
+                acc[p][k] = x >= Q ? x - Q : x;
+            }
+    }
+    __syncthreads();  // every last inverse pass has read its entries
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = acc[p][k];
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
+        const uint64_t v = buf[k == 0 ? 0 : N - k];
+        g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+        g[N + k] = buf[N + k];
+    }
+}
+
 // W1 = w 2^31 mod Q for w < Q: w 2^31 = (w >> 23) 2^54 + (w mod 2^23) 2^31
 __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ in, size_t words,
                           uint64_t* __restrict__ out) {
@@ -1042,6 +1265,20 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     const uint64_t* w1 = (const uint64_t*)sf;
     const size_t lds = (size_t)4 * G3_N * 8;  // two polynomials + forward twiddles (W0, W1)
+    static const bool no_sf2 = [] {
+        const char* e = std::getenv("TFHE_SF2");
+        return e && e[0] == '0';
+    }();
+    if (!no_sf2 && P.digits == 1) {
+        auto go = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
+                               (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
+                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
+        };
+        go(k_blind_rotate_sf2<1>);
+        return hipGetLastError();
+    }
     (void)hipFuncSetAttribute((const void*)k_blind_rotate_gen3sf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_blind_rotate_gen3sf, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
                        (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N, T.eidx,
