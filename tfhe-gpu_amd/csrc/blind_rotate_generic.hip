@@ -698,6 +698,26 @@ struct SfTw {
     const uint64_t* __restrict__ w1;
 };
 
+// Monomial factors from two 64-entry LDS tables instead of gathers from the 2N-entry table in
+// memory (those missed the cache and stalled every round, profiles/r02z): T[j] = psi^(64 j),
+// T[64 + j] = psi^j as (W0, W1) pairs, built from mono = psi^k - 1 at kernel start, and
+//     A (psi^e - 1) = sf(sf(A, T[e >> 6]), T[64 + (e & 63)]) + (9Q - A)      (A < 9Q)
+constexpr uint32_t SF_MT = 256;  // u64 words of the two tables
+__device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __restrict__ mono,
+                                               const uint64_t* __restrict__ mono1, uint64_t Q) {
+    for (uint32_t k = threadIdx.x; k < 128; k += blockDim.x) {
+        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        const uint64_t w0 = mono[e] + 1, w1 = mono1[e] + (1ull << 31);  // psi^e, psi^e 2^31
+        T[2 * k] = w0 >= Q ? w0 - Q : w0;
+        T[2 * k + 1] = w1 >= Q ? w1 - Q : w1;
+    }
+}
+__device__ __forceinline__ uint64_t sf_mono_mul(uint64_t A, uint32_t e, const uint64_t* T, const SfC& K) {
+    const uint64_t* th = T + 2 * (e >> 6);
+    const uint64_t* tl = T + 2 * (64 + (e & 63));
+    return sf_mul(sf_mul(A, th[0], th[1], K.c), tl[0], tl[1], K.c) + (K.Q9 - A);
+}
+
 __device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const SfTw& T, uint32_t i, const SfC& K) {
     const uint64_t v = sf_mul(y, T.w0[i], T.w1[i], K.c);
     y = x + (K.Q2 - v);
@@ -818,6 +838,8 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
+    uint64_t* mt = psi1_l + N;  // monomial tables
+    sf_mono_tables(mt, mono, mono1, Q);
     const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
@@ -899,9 +921,9 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
         for (int k = 0; k < CN; ++k) {
             const uint32_t x = t + TH * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            const uint64_t mp = mono[ip], mp1 = mono1[ip], mn = mono[in], mn1 = mono1[in];
-            buf[ts + TH * k] = sf_mul(A[0][0][k], mp, mp1, K.c) + sf_mul(A[1][0][k], mn, mn1, K.c);
-            buf[N + ts + TH * k] = sf_mul(A[0][1][k], mp, mp1, K.c) + sf_mul(A[1][1][k], mn, mn1, K.c);
+            buf[ts + TH * k] = sf_fold(sf_mono_mul(A[0][0][k], ip, mt, K) + sf_mono_mul(A[1][0][k], in, mt, K), K.c);
+            buf[N + ts + TH * k] =
+                sf_fold(sf_mono_mul(A[0][1][k], ip, mt, K) + sf_mono_mul(A[1][1][k], in, mt, K), K.c);
         }
         __syncthreads();
         uint64_t v[8];
@@ -1030,7 +1052,9 @@ __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], 
     sf_inv_core<false>(v, 4, 0, T, K);
 }
 
-template <int DIG>
+// EXP (timing experiments, results invalid): 1 = keys of round 0 only (cache-resident), 4 = inverse
+// twiddles from the forward table in LDS
+template <int DIG, int EXP = 0>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
@@ -1047,7 +1071,9 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
-    const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
+    uint64_t* mt = psi1_l + N;  // monomial tables
+    sf_mono_tables(mt, mono, mono1, Q);
+    const SfTw TF{psi_l, psi1_l}, TI = (EXP & 4) ? SfTw{psi_l, psi1_l} : SfTw{ipsi, ipsi1};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
@@ -1072,8 +1098,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
         uint64_t A[2][2][4];  // A_kj of slots u4 + j (< 2.1 Q per digit)
-        const uint64_t* ek = bsk + (size_t)i * round_words + u4;
-        const uint64_t* ek1 = bsk1 + (size_t)i * round_words + u4;
+        const uint64_t* ek = bsk + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
+        const uint64_t* ek1 = bsk1 + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
@@ -1122,10 +1148,9 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const uint32_t ip = (ex[s] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            const uint64_t mp = mono[ip], mp1 = mono1[ip], mn = mono[in], mn1 = mono1[in];
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                S[j][s] = sf_mul(A[0][j][s], mp, mp1, K.c) + sf_mul(A[1][j][s], mn, mn1, K.c);
+                S[j][s] = sf_fold(sf_mono_mul(A[0][j][s], ip, mt, K) + sf_mono_mul(A[1][j][s], in, mt, K), K.c);
         }
         uint64_t v[8];
         sf2_ntt_inv(buf, S, v, TI, K);  // outputs < 8.2 Q
@@ -1264,10 +1289,15 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     K.Q = P.Q, K.Q2 = 2 * P.Q, K.Q9 = 9 * P.Q;
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     const uint64_t* w1 = (const uint64_t*)sf;
-    const size_t lds = (size_t)4 * G3_N * 8;  // two polynomials + forward twiddles (W0, W1)
+    const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8;  // two polynomials, forward twiddles, monomial tables
     static const bool no_sf2 = [] {
         const char* e = std::getenv("TFHE_SF2");
         return e && e[0] == '0';
+    }();
+    static const int exp = [] {  // TFHE_SF2_EXP: timing only (TFHE_TIMING_EXPERIMENTS=1)
+        const char* e = std::getenv("TFHE_SF2_EXP");
+        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+        return (e && x && x[0] == '1') ? std::atoi(e) : 0;
     }();
     if (!no_sf2 && P.digits == 1) {
         auto go = [&](auto kern) {
@@ -1276,7 +1306,12 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
                                (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
-        go(k_blind_rotate_sf2<1>);
+        switch (exp) {
+            case 1: go(k_blind_rotate_sf2<1, 1>); break;
+            case 4: go(k_blind_rotate_sf2<1, 4>); break;
+            case 5: go(k_blind_rotate_sf2<1, 5>); break;
+            default: go(k_blind_rotate_sf2<1>); break;
+        }
         return hipGetLastError();
     }
     (void)hipFuncSetAttribute((const void*)k_blind_rotate_gen3sf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -126,7 +126,11 @@ def model(rows):
     D = max(fwd_r4(x))
     print(f"  forward outputs < {D / Q:.1f} Q")
     A = rows * 2 * mulw(D)      # rows digits x 2 polynomials per (key, column)
-    S = mulw(A) + mulw(A)       # A0j mp + A1j mn
+    # A0j (X^a' - 1) + A1j (X^-a' - 1) with two LDS table factors per monomial:
+    # sf(sf(A, T_hi), T_lo) + (9Q - A) per term, the sum folded
+    if A > OFF_GS:
+        fail("monomial offset 9Q below the product sum bound")
+    S = fold(2 * (mulw(mulw(A)) + OFF_GS))
     print(f"  products < {A / Q:.2f} Q, S < {S / Q:.2f} Q")
     x = max(inv_r4(S, INV_FOLD_UNITS))
     x = max(inv_r8(x, INV_FOLD_PASS))
