@@ -350,7 +350,8 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 // update in registers; the products (C', sums, monomials) keep the slot layout.
 // EXP (timing experiments, results invalid): 1 = every round reads the keys of round i & 7
 // (L2-resident), 2 = of round i & 63 (MALL-resident), 4 = no barriers inside the transforms
-template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, int EXP = 0>
+// MT: monomial factors from the two LDS tables (mt) instead of the 2N-entry table in memory
+template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, int EXP = 0, bool MT = !RED>
 __global__ void __launch_bounds__(TH, 4)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -360,6 +361,10 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     double* psi = lds_d;
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
+    // monomial factors from two 64-entry tables instead of gathers from the 2N-entry table in
+    // memory (cache misses in every round): mt[j] = psi^(64 j), mt[64 + j] = psi^j (centred), and
+    //     A (psi^e - 1) = fmodmul(fmodmul(A, mt[e >> 6]), mt[64 + (e & 63)]) - A
+    double* mt = lds_d + 4 * N;
     __shared__ int wflag[2];  // WRAP vote of round i in wflag[i & 1], published by the round's first barrier
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t ts = bidx<N>(t);  // swz(t + TH k) = swz(t) + TH k (TH a multiple of 256)
@@ -371,6 +376,14 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     };
     for (uint32_t k = t; k < twoN; k += F64_THREADS) lds_d[k] = tabs[k];
     const double* mono = tabs + twoN;
+    constexpr uint32_t SH = 6, LM = 63;  // e = 64 hi + lo, hi < 2N / 64 <= 64
+    for (uint32_t k = t; k < 128; k += F64_THREADS) {
+        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        if (e < twoN) {
+            const double v = __dadd_rn(mono[e], 1.0);  // psi^e, centred
+            mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
+        }
+    }
     const double* bsk = tabs + 2 * twoN;
     const uint64_t Qhalf = P.Q >> 1;
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
@@ -538,9 +551,17 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         for (int k = 0; k < CN; ++k) {
             const uint32_t x = t + F64_THREADS * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            const double mp = mono[ip], mn = mono[in];
-            const double s0 = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
-            const double s1 = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
+            double s0, s1;
+            if constexpr (MT) {
+                const double hp = mt[ip >> SH], lp = mt[64 + (ip & LM)], hn = mt[in >> SH], ln = mt[64 + (in & LM)];
+                auto mm = [&](double a, double h, double lo) { return __dsub_rn(fmodmul(fmodmul(a, h, K), lo, K), a); };
+                s0 = fred(__dadd_rn(mm(A[0][0][k], hp, lp), mm(A[1][0][k], hn, ln)), K);
+                s1 = fred(__dadd_rn(mm(A[0][1][k], hp, lp), mm(A[1][1][k], hn, ln)), K);
+            } else {
+                const double mp = mono[ip], mn = mono[in];
+                s0 = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
+                s1 = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
+            }
             buf[ts + F64_THREADS * k] = s0;
             buf[N + ts + F64_THREADS * k] = s1;
             if constexpr (FOLD) Cn[0][k] = fred(__dadd_rn(Cn[0][k], s0), K), Cn[1][k] = fred(__dadd_rn(Cn[1][k], s1), K);
@@ -683,13 +704,27 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const bool wrap = fold && !fold_exact(P);
-    const size_t lds = (size_t)4 * P.N * sizeof(double);  // psi, ipsi, two polynomials
+    const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double);  // psi, ipsi, two polynomials, monomial tables
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
                            amod, acc);
     };
     const bool red = P.Q >= (1ull << 40);
+    // TFHE_F64_MT (A/B runs): 1 = LDS monomial tables for every set, 0 = gathers for every set;
+    // default: tables for Q < 2^40 (STD192 class), gathers for the reducing sets (STD128Q class)
+    static const int mt_mode = [] {
+        const char* e = std::getenv("TFHE_F64_MT");
+        return e && e[0] ? e[0] - '0' : 2;
+    }();
+    if (mt_mode != 2 && P.N == 2048 && fold) {
+        const bool on = mt_mode == 1;
+        if (wrap) red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, true, 0, true>) : go(k_blind_rotate_f64<512, 4, true, true, true, 0, false>))
+                      : (on ? go(k_blind_rotate_f64<512, 4, false, true, true, 0, true>) : go(k_blind_rotate_f64<512, 4, false, true, true, 0, false>));
+        else red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, false, 0, true>) : go(k_blind_rotate_f64<512, 4, true, true, false, 0, false>))
+                 : (on ? go(k_blind_rotate_f64<512, 4, false, true, false, 0, true>) : go(k_blind_rotate_f64<512, 4, false, true, false, 0, false>));
+        return hipGetLastError();
+    }
     // TFHE_F64_EXP (timing only, TFHE_TIMING_EXPERIMENTS=1): key-stream locality experiments, N = 2048
     static const int exp = [] {
         const char* e = std::getenv("TFHE_F64_EXP");
