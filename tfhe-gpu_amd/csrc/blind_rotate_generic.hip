@@ -1097,9 +1097,9 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-        uint64_t A[2][2][4];  // A_kj of slots u4 + j (< 2.1 Q per digit)
         const uint64_t* ek = bsk + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
         const uint64_t* ek1 = bsk1 + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
+        uint64_t D[DIG][2][4];  // forward outputs of every digit: slots u4 + s of both polynomials
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
@@ -1118,39 +1118,43 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                     v[p * CN + k] = (uint64_t)r;
                 }
             if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
-            uint64_t D[2][4];
-            sf2_ntt_fwd(buf, v, D, TF, K);
-            // products: group g = (key kk, column j, row r = 2l + polynomial) = 4 slots x (W0, W1);
-            // the next group's words are loaded before this group's arithmetic
-            auto kload = [&](int g, uint64_t (&kw)[8]) {
-                const uint32_t kk = g >> 2, j = (g >> 1) & 1, r = g & 1;
-                const size_t o = ((size_t)(kk * P.dG2 + 2 * l + r) * 2 + j) * N;
+            sf2_ntt_fwd(buf, v, D[l], TF, K);
+        }
+        // products: group g = (column j, key kk, row r = 2l + polynomial), 4 slots x (W0, W1) of key
+        // words each, the next group's loaded before this group's arithmetic; A_kj of slots u4 + s
+        // (< 2.1 Q per digit); once both keys of column j are summed, its monomial factors
+        constexpr int RW = 2 * DIG, NG = 4 * RW;
+        auto kload = [&](int g, uint64_t (&kw)[8]) {
+            const uint32_t j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
+            const size_t o = ((size_t)(kk * P.dG2 + r) * 2 + j) * N;
 #pragma unroll
-                for (int s = 0; s < 4; ++s) kw[s] = ek[o + s], kw[4 + s] = ek1[o + s];
-            };
-            uint64_t kw[2][8];
-            kload(0, kw[0]);
+            for (int s = 0; s < 4; ++s) kw[s] = ek[o + s], kw[4 + s] = ek1[o + s];
+        };
+        uint32_t ip[4];
 #pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                if (g + 1 < 8) kload(g + 1, kw[(g + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
-                const int kk = g >> 2, j = (g >> 1) & 1, r = g & 1;
-                const uint64_t(&c)[8] = kw[g & 1];
+        for (int s = 0; s < 4; ++s) ip[s] = (ex[s] * ai) & (twoN - 1);
+        uint64_t S[2][4], A[2][4];
+        uint64_t kw[2][8];
+        kload(0, kw[0]);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            if (g + 1 < NG) kload(g + 1, kw[(g + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
+            const uint64_t(&c)[8] = kw[g & 1];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint64_t prod = sf_mul(D[r >> 1][r & 1][s], c[s], c[4 + s], K.c);
+                A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
+            }
+            if (kk == 1 && r == RW - 1) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const uint64_t prod = sf_mul(D[r][s], c[s], c[4 + s], K.c);
-                    A[kk][j][s] = (l == 0 && r == 0) ? prod : A[kk][j][s] + prod;
+                    const uint32_t in = (twoN - ip[s]) & (twoN - 1);
+                    S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip[s], mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
                 }
-                __builtin_amdgcn_sched_barrier(0);
             }
-        }
-        uint64_t S[2][4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const uint32_t ip = (ex[s] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                S[j][s] = sf_fold(sf_mono_mul(A[0][j][s], ip, mt, K) + sf_mono_mul(A[1][j][s], in, mt, K), K.c);
+            __builtin_amdgcn_sched_barrier(0);
         }
         uint64_t v[8];
         sf2_ntt_inv(buf, S, v, TI, K);  // outputs < 8.2 Q
@@ -1299,13 +1303,17 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
         const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
         return (e && x && x[0] == '1') ? std::atoi(e) : 0;
     }();
-    if (!no_sf2 && P.digits == 1) {
+    if (!no_sf2 && (P.digits == 1 || P.digits == 2)) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
                                (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
                                (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
+        if (P.digits == 2) {
+            go(k_blind_rotate_sf2<2>);
+            return hipGetLastError();
+        }
         switch (exp) {
             case 1: go(k_blind_rotate_sf2<1, 1>); break;
             case 4: go(k_blind_rotate_sf2<1, 4>); break;
