@@ -597,6 +597,293 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     }
 }
 
+// ---- N = 2048, wave-local passes (f64w; the sf2 design of blind_rotate_generic.hip) ----------
+// Wave w owns the 256-element block w of both polynomials after pass A: passes B, C and the
+// units run in wave w without workgroup barriers, the units leave slots 4u .. 4u+3 (u = 64w + l)
+// of both polynomials in registers, and the products (32-byte key rows per lane), the C' update,
+// the monomial factors and the inverse units stay in registers.  One barrier per forward
+// transform (plus one before each further digit's pass A), one per inverse.
+__device__ __forceinline__ void f64w_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool RED>
+__device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double (&d)[2][4], const double* psi,
+                                             const F64Const& K) {
+    constexpr uint32_t N = 2048;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    {
+        const uint32_t tau = f64_tau();
+        double* p = buf + (t >> 8) * N;
+        uint32_t ad[8];
+        ad_A(tau, ad);
+        f64_r8_fwd_core(v, 1, 0, psi, K);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
+    }
+    __syncthreads();
+    uint32_t tw = (w << 5) | (l & 31);
+    asm volatile("" : "+v"(tw));
+    double* p = buf + (l >> 5) * N;
+    {
+        uint32_t ad[8];
+        ad_B(tw, ad);
+        f64_r8_fwd<RED>(p, ad, 8, tw >> 5, psi, K);
+    }
+    f64w_sync();
+    {
+        uint32_t ad[8];
+        ad_C(tw, ad);
+        f64_r8_fwd<RED>(p, ad, 64, tw >> 2, psi, K);
+    }
+    f64w_sync();
+    const uint32_t u = (w << 6) | l, u0 = swz(4 * u);
+    const double wa = psi[N / 4 + u];
+    const double2 wb = *(const double2*)(psi + N / 2 + 2 * u);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // stages 9 (h = 2) and 10 (h = 1) on slots 4u .. 4u+3
+        const double* pq = buf + q * N;
+        double v0 = pq[u0], v1 = pq[u0 ^ 1], v2 = pq[u0 ^ 2], v3 = pq[u0 ^ 3];
+        ct_bf(v0, v2, wa, K), ct_bf(v1, v3, wa, K);
+        ct_bf(v0, v1, wb.x, K), ct_bf(v2, v3, wb.y, K);
+        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
+        d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+    }
+}
+
+template <bool RED>
+__device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4], double (&v)[8],
+                                             const double* ipsi, const F64Const& K) {
+    constexpr uint32_t N = 2048;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t u = (w << 6) | l, u0 = swz(4 * u);
+    const double2 wb = *(const double2*)(ipsi + N / 2 + 2 * u);
+    const double wa = ipsi[N / 4 + u];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        double* pq = buf + q * N;
+        double v0 = s[q][0], v1 = s[q][1], v2 = s[q][2], v3 = s[q][3];
+        gs_bf(v0, v1, wb.x, K), gs_bf(v2, v3, wb.y, K);
+        gs_bf(v0, v2, wa, K), gs_bf(v1, v3, wa, K);
+        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K);
+        pq[u0] = v0, pq[u0 ^ 1] = v1, pq[u0 ^ 2] = v2, pq[u0 ^ 3] = v3;
+    }
+    f64w_sync();
+    uint32_t tw = (w << 5) | (l & 31);
+    asm volatile("" : "+v"(tw));
+    double* p = buf + (l >> 5) * N;
+    {
+        uint32_t ad[8];
+        ad_C(tw, ad);
+        f64_r8_inv<RED>(p, ad, 256, tw >> 2, ipsi, K);
+    }
+    f64w_sync();
+    {
+        uint32_t ad[8];
+        ad_B(tw, ad);
+        f64_r8_inv<RED>(p, ad, 32, tw >> 5, ipsi, K);
+    }
+    __syncthreads();
+    const uint32_t tau = f64_tau();
+    const double* pa = buf + (t >> 8) * N;
+    uint32_t ad[8];
+    ad_A(tau, ad);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = pa[ad[k]];
+    f64_r8_inv_core(v, 4, 0, ipsi, K);
+}
+
+// FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64, MT:
+// monomial tables in LDS
+template <bool RED, bool WRAP, int LD, bool MT>
+__global__ void __launch_bounds__(512, 4)
+k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
+                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
+    extern __shared__ __align__(16) double lds_d[];
+    constexpr uint32_t N = 2048, TH = 512, CN = 4;
+    double* psi = lds_d;
+    double* ipsi = lds_d + N;
+    double* buf = lds_d + 2 * N;  // [2][N]
+    double* mt = lds_d + 4 * N;   // monomial tables (k_blind_rotate_f64)
+    __shared__ int wflag[2];
+    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
+    auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
+    for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
+    const double* mono = tabs + twoN;
+    for (uint32_t k = t; k < 128; k += TH) {
+        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        const double v = __dadd_rn(mono[e], 1.0);
+        mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
+    }
+    const double* bsk = tabs + 2 * twoN;
+    const uint64_t Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
+    const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
+    const uint64_t scale = (uint64_t)twoN / amod;
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    uint32_t ex[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ex[s] = 2 * (__builtin_bitreverse32(u4 + s) >> 21) + 1;
+
+    int64_t acc[2][CN];  // canonical [0, Q), pass A's layout
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint64_t v = g[lpos(p, k)];
+            acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
+        }
+    if (WRAP && t < 2) wflag[t] = 0;
+    __syncthreads();
+    double Cn[2][4];  // N^-1 NTT(acc) at slots u4 + s, |Cn| <~ Q/2
+    {
+        double v[8];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k)
+                v[p * CN + k] = (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
+        double d[2][4];
+        f64w_ntt_fwd<RED>(buf, v, d, psi, K);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) Cn[p][s] = fmodmul(d[p][s], K.Ninv, K);
+    }
+    int64_t KdL = 0;  // WRAP: residual after all digits = (c + KdL) >> (L g)
+    for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
+    const uint32_t shiftL = P.digits * logG;
+
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const double* ek = bsk + (size_t)i * round_words + u4;
+        double D[LD][2][4];
+        // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
+        auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4]) {
+            constexpr bool CORR = decltype(corr_c)::value;
+            const uint32_t shift = l * logG;
+            int64_t Kd = 0;
+            for (uint32_t z = 0; z < l; ++z) Kd = (Kd << logG) + Bh;
+            double v[8];
+            bool wv = false;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
+                    if constexpr (CORR) {
+                        v[p * CN + k] = __dmul_rn((double)((c + KdL) >> shiftL), -K.wfac);
+                    } else {
+                        const int64_t dd = (c + Kd) >> shift;
+                        v[p * CN + k] = (double)(int32_t)((int64_t)((uint64_t)dd << sh) >> sh);  // |r| <= B/2
+                    }
+                    if (WRAP && !CORR) wv |= ((c + KdL) >> shiftL) != 0;
+                }
+            if (WRAP && !CORR && l == 0) {
+                // round i - 1 read wflag[(i + 1) & 1] before its inverse barrier; round i + 1
+                // writes it after this round's barriers; the forward barrier publishes the vote
+                if (t == 0) wflag[(i + 1) & 1] = 0;
+                if (wv) wflag[i & 1] = 1;
+            }
+            if (CORR || l > 0) __syncthreads();  // other waves may still read their blocks
+            f64w_ntt_fwd<RED>(buf, v, d, psi, K);
+        };
+        using F_ = std::false_type;
+        using T_ = std::true_type;
+#pragma unroll
+        for (int l = 0; l < LD; ++l) digit(l, F_{}, D[l]);
+        double Cx[2][4];  // C' (+ the WRAP correction)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) Cx[p][s] = Cn[p][s];
+        if constexpr (WRAP) {
+            if (wflag[i & 1]) {
+                double dc[2][4];
+                digit(LD, T_{}, dc);
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) Cx[p][s] = fred(__dadd_rn(Cx[p][s], dc[p][s]), K);
+            }
+        }
+        // products: group g = (column j, key kk, row r), rows 0 .. 2LD-1 the digits', 2LD, 2LD+1
+        // the C' rows; 4 slots of key words each, the next group's loaded first
+        constexpr int RW = 2 * LD + 2, NG = 4 * RW;
+        auto kload = [&](int gi, double (&kv)[4]) {
+            const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
+            const double* kp = ek + ((size_t)(kk * P.dG2 + r) * 2 + j) * N;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) kv[q] = kp[q];
+        };
+        uint32_t ip[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ip[q] = (ex[q] * ai) & (twoN - 1);
+        double S[2][4], A[2][4];
+        double kv[2][4];
+        kload(0, kv[0]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gi + 1 < NG) kload(gi + 1, kv[(gi + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double dv = r < 2 * LD ? D[r >> 1][r & 1][q] : Cx[r & 1][q];
+                const double pr = fmodmul(dv, kv[gi & 1][q], K);
+                A[kk][q] = r == 0 ? pr : __dadd_rn(A[kk][q], pr);
+            }
+            if (kk == 1 && r == RW - 1) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t in = (twoN - ip[q]) & (twoN - 1);
+                    double sv;
+                    if constexpr (MT) {
+                        auto mm = [&](double x, uint32_t e) {
+                            return __dsub_rn(fmodmul(fmodmul(x, mt[e >> 6], K), mt[64 + (e & 63)], K), x);
+                        };
+                        sv = fred(__dadd_rn(mm(A[0][q], ip[q]), mm(A[1][q], in)), K);
+                    } else {
+                        sv = __dadd_rn(fmodmul(A[0][q], mono[ip[q]], K), fmodmul(A[1][q], mono[in], K));
+                    }
+                    S[j][q] = sv;
+                    Cn[j][q] = fred(__dadd_rn(Cn[j][q], sv), K);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        double v[8];
+        f64w_ntt_inv<RED>(buf, S, v, ipsi, K);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const double r = v[p * CN + k];  // |r| < 2^52
+                const double q = __builtin_rint(__dmul_rn(r, K.Qinv));
+                int64_t uu = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
+                uu = uu < 0 ? uu + Qs : uu;
+                acc[p][k] = uu >= Qs ? uu - Qs : uu;
+            }
+    }
+    __syncthreads();  // every last inverse pass has read its entries
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = __builtin_bit_cast(double, acc[p][k]);
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
+        const uint64_t v = __builtin_bit_cast(uint64_t, buf[k == 0 ? 0 : N - k]);
+        g[k] = k == 0 ? v : (v == 0 ? 0 : P.Q - v);
+        g[N + k] = __builtin_bit_cast(uint64_t, buf[N + k]);
+    }
+}
+
 // canonical u64 tables / BSK (generic arena) -> centred doubles
 // a * b mod Q for Q < 2^50 in 12-bit steps (one-time packing only)
 __device__ uint64_t mulmod_slow(uint64_t a, uint64_t b, uint64_t Q) {
@@ -711,6 +998,31 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
                            amod, acc);
     };
     const bool red = P.Q >= (1ull << 40);
+    // wave-local N = 2048 kernel for the folded sets with 2 or 3 digits (TFHE_F64W=0: the
+    // slot-layout kernel below)
+    static const bool no_w = [] {
+        const char* e = std::getenv("TFHE_F64W");
+        return e && e[0] == '0';
+    }();
+    static const int mtw = [] {  // TFHE_F64W_MT: 0 = gathers from the memory table (A/B runs)
+        const char* e = std::getenv("TFHE_F64W_MT");
+        return e && e[0] ? e[0] - '0' : 2;
+    }();
+    if (!no_w && P.N == 2048 && fold && (P.digits == 2 || P.digits == 3)) {
+        const bool m = mtw != 0;  // tables: STD192 474 -> 385 ms, STD128Q 319 -> 288 ms (profiles/r02ae)
+        const int ld = (int)P.digits - 1;
+#define F64W_GO(R, W, L)                                                                     \
+    (m ? go(k_blind_rotate_f64w<R, W, L, true>) : go(k_blind_rotate_f64w<R, W, L, false>))
+        if (red) {
+            if (wrap) ld == 1 ? F64W_GO(true, true, 1) : F64W_GO(true, true, 2);
+            else ld == 1 ? F64W_GO(true, false, 1) : F64W_GO(true, false, 2);
+        } else {
+            if (wrap) ld == 1 ? F64W_GO(false, true, 1) : F64W_GO(false, true, 2);
+            else ld == 1 ? F64W_GO(false, false, 1) : F64W_GO(false, false, 2);
+        }
+#undef F64W_GO
+        return hipGetLastError();
+    }
     // TFHE_F64_MT (A/B runs): 1 = LDS monomial tables for every set, 0 = gathers for every set;
     // default: tables for Q < 2^40 (STD192 class), gathers for the reducing sets (STD128Q class)
     static const int mt_mode = [] {
