@@ -45,3 +45,11 @@ def test_special_form_kernel_bounds():
     partial products, non-negative offset subtractions, one-subtraction accumulator update."""
     out = run_tool("bounds_sf.py")
     assert out.strip().endswith("OK"), out
+
+
+def test_wave_local_transform_schedule():
+    """sf2 / f64w: the wave-local N = 2048 passes equal the stage loops, passes B, C and the
+    units touch only their wave's block of both polynomials, every b64 access is conflict-free."""
+    out = run_tool("lds_layouts_wl.py")
+    assert "wave-locality: passes B, C and the units stay in the wave's block" in out
+    assert out.strip().endswith("OK"), out
