@@ -372,7 +372,9 @@ def test_key_file_roundtrip(std128, capi, tmp_path):
 
 
 @pytest.mark.parametrize("pset,path,kernel", [("STD192", "f64", 3), ("STD192", "f64-nofold", 2), ("STD192", "generic", 0),
-                                              ("STD192Q_OPT", "f64", 3), ("STD128Q", "f64", 3),
+                                              ("STD192", "f64-slot", 3), ("STD192", "f64w-gather", 3),
+                                              ("STD192Q_OPT", "f64", 3), ("STD128Q", "f64", 3), ("STD128Q", "f64-slot", 3),
+                                              ("STD128Q", "f64w-gather", 3),
                                               ("STD128Q", "f64-exactonly", 2), ("STD128Q", "f64-nofold", 2)])
 def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     """STD192 (Q = 2^37 - 2^17 + 1) and STD128Q (Q = 2^50 - 2^14 + 1, the reducing variant),
@@ -388,26 +390,28 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
     env = {"generic": ("TFHE_FORCE_GENERIC", "1"), "f64-nofold": ("TFHE_F64_FOLD", "0"),
-           "f64-exactonly": ("TFHE_F64_FOLD", "1")}.get(path)
+           "f64-exactonly": ("TFHE_F64_FOLD", "1"), "f64-slot": ("TFHE_F64W", "0"),
+           "f64w-gather": ("TFHE_F64W_MT", "0")}.get(path)
     if env:
         os.environ[env[0]] = env[1]
-    try:
+    try:  # setup-time switches are read at setup, launch-time ones (F64W*) at every launch
         ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        assert ctx.info().br_kernel == kernel
+        B = 2
+        a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+        acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+        acc[1, :, :6] = [0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1, (op.Q >> 1) - 1, (op.Q >> 1) - 5000]
+        assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
     finally:
         if env:
             os.environ.pop(env[0], None)
-    assert ctx.info().br_kernel == kernel
-    B = 2
-    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
-    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
-    acc[1, :, :6] = [0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1, (op.Q >> 1) - 1, (op.Q >> 1) - 5000]
-    assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
     ctx.GPUClean()
     orc.close()
 
 
 
-@pytest.mark.parametrize("arb,logq,path,kernel", [(True, 12, "sf", 5), (False, 23, "sf", 5), (True, 12, "rns", 4),
+@pytest.mark.parametrize("arb,logq,path,kernel", [(True, 12, "sf", 5), (False, 23, "sf", 5), (True, 12, "gen3sf", 5),
+                                                   (False, 23, "gen3sf", 5), (True, 12, "rns", 4),
                                                    (False, 23, "rns", 4), (True, 12, "generic", 0),
                                                    (False, 23, "generic", 0)])
 def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
@@ -423,23 +427,23 @@ def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
     bsk[: 4 * op.N] = np.array([0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1], dtype=np.uint64).repeat(op.N)
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
-    env = {"rns": ("TFHE_RNS", "1"), "generic": ("TFHE_SF", "0")}.get(path)
+    env = {"rns": ("TFHE_RNS", "1"), "generic": ("TFHE_SF", "0"), "gen3sf": ("TFHE_SF2", "0")}.get(path)
     if env:
         os.environ[env[0]] = env[1]
-    try:
+    try:  # TFHE_RNS / TFHE_SF are read at setup, TFHE_SF2 at every launch
         ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        assert ctx.info().br_kernel == kernel
+        B = 3
+        acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+        half = op.Q >> 1
+        acc[0, :, :8] = [0, op.Q - 1, half, half + 1, half - 1, 1, op.Q - 2, half + 2]
+        acc[1] = np.where(rs.integers(0, 2, (2, op.N)) == 1, half, half + 1).astype(np.uint64)  # extreme digits
+        for amod in (op.q, 2 * op.N):
+            a = rs.integers(0, amod, (B, op.n), dtype=np.uint64)
+            assert np.array_equal(ctx.EvalAcc(a, amod, acc), orc.eval_acc(a, amod, acc))
     finally:
         if env:
             os.environ.pop(env[0], None)
-    assert ctx.info().br_kernel == kernel
-    B = 3
-    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
-    half = op.Q >> 1
-    acc[0, :, :8] = [0, op.Q - 1, half, half + 1, half - 1, 1, op.Q - 2, half + 2]
-    acc[1] = np.where(rs.integers(0, 2, (2, op.N)) == 1, half, half + 1).astype(np.uint64)  # extreme digits
-    for amod in (op.q, 2 * op.N):
-        a = rs.integers(0, amod, (B, op.n), dtype=np.uint64)
-        assert np.array_equal(ctx.EvalAcc(a, amod, acc), orc.eval_acc(a, amod, acc))
     ctx.GPUClean()
     orc.close()
 

@@ -1000,11 +1000,11 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     const bool red = P.Q >= (1ull << 40);
     // wave-local N = 2048 kernel for the folded sets with 2 or 3 digits (TFHE_F64W=0: the
     // slot-layout kernel below)
-    static const bool no_w = [] {
+    const bool no_w = [] {  // read per launch (tests and A/B runs switch it)
         const char* e = std::getenv("TFHE_F64W");
         return e && e[0] == '0';
     }();
-    static const int mtw = [] {  // TFHE_F64W_MT: 0 = gathers from the memory table (A/B runs)
+    const int mtw = [] {  // TFHE_F64W_MT=0: gathers from the memory table (read per launch)
         const char* e = std::getenv("TFHE_F64W_MT");
         return e && e[0] ? e[0] - '0' : 2;
     }();
@@ -1025,7 +1025,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     }
     // TFHE_F64_MT (A/B runs): 1 = LDS monomial tables for every set, 0 = gathers for every set;
     // default: tables for Q < 2^40 (STD192 class), gathers for the reducing sets (STD128Q class)
-    static const int mt_mode = [] {
+    const int mt_mode = [] {  // read per launch (tests and A/B runs switch it)
         const char* e = std::getenv("TFHE_F64_MT");
         return e && e[0] ? e[0] - '0' : 2;
     }();

@@ -1294,7 +1294,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     const uint64_t* w1 = (const uint64_t*)sf;
     const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8;  // two polynomials, forward twiddles, monomial tables
-    static const bool no_sf2 = [] {
+    const bool no_sf2 = [] {  // read per launch (tests and A/B runs switch it)
         const char* e = std::getenv("TFHE_SF2");
         return e && e[0] == '0';
     }();
