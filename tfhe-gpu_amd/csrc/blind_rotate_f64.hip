@@ -609,7 +609,9 @@ __device__ __forceinline__ void f64w_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool RED>
+// TO_LDS: the units' outputs stay in the buffer (slots 4u .. 4u+3 of the wave's block, read back
+// by the products of this wave) instead of registers
+template <bool RED, bool TO_LDS = false>
 __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double (&d)[2][4], const double* psi,
                                              const F64Const& K) {
     constexpr uint32_t N = 2048;
@@ -649,8 +651,14 @@ __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double
         ct_bf(v0, v2, wa, K), ct_bf(v1, v3, wa, K);
         ct_bf(v0, v1, wb.x, K), ct_bf(v2, v3, wb.y, K);
         if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
-        d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+        if constexpr (TO_LDS) {
+            double* pw = buf + q * N;
+            pw[u0] = v0, pw[u0 ^ 1] = v1, pw[u0 ^ 2] = v2, pw[u0 ^ 3] = v3;
+        } else {
+            d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+        }
     }
+    if constexpr (TO_LDS) f64w_sync();
 }
 
 template <bool RED>
@@ -763,9 +771,9 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
         const double* ek = bsk + (size_t)i * round_words + u4;
-        double D[LD][2][4];
+        double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
-        auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4]) {
+        auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4], bool sync) {
             constexpr bool CORR = decltype(corr_c)::value;
             const uint32_t shift = l * logG;
             int64_t Kd = 0;
@@ -791,13 +799,14 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 if (t == 0) wflag[(i + 1) & 1] = 0;
                 if (wv) wflag[i & 1] = 1;
             }
-            if (CORR || l > 0) __syncthreads();  // other waves may still read their blocks
-            f64w_ntt_fwd<RED>(buf, v, d, psi, K);
+            if (sync) __syncthreads();  // other waves may still read their blocks
+            if (!CORR && l + 1 == LD) f64w_ntt_fwd<RED, true>(buf, v, d, psi, K);
+            else f64w_ntt_fwd<RED>(buf, v, d, psi, K);
         };
         using F_ = std::false_type;
         using T_ = std::true_type;
 #pragma unroll
-        for (int l = 0; l < LD; ++l) digit(l, F_{}, D[l]);
+        for (int l = 0; l < LD; ++l) digit(l, F_{}, D[l], l > 0);
         double Cx[2][4];  // C' (+ the WRAP correction)
 #pragma unroll
         for (int p = 0; p < 2; ++p)
@@ -805,12 +814,15 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             for (int s = 0; s < 4; ++s) Cx[p][s] = Cn[p][s];
         if constexpr (WRAP) {
             if (wflag[i & 1]) {
+                // the correction's transform overwrites the buffer that holds the last digit's
+                // outputs: transform the last digit again afterwards (rare rounds only)
                 double dc[2][4];
-                digit(LD, T_{}, dc);
+                digit(LD, T_{}, dc, true);
 #pragma unroll
                 for (int p = 0; p < 2; ++p)
 #pragma unroll
                     for (int s = 0; s < 4; ++s) Cx[p][s] = fred(__dadd_rn(Cx[p][s], dc[p][s]), K);
+                digit(LD - 1, F_{}, D[LD - 1], true);
             }
         }
         // products: group g = (column j, key kk, row r), rows 0 .. 2LD-1 the digits', 2LD, 2LD+1
@@ -835,7 +847,9 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             const int j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double dv = r < 2 * LD ? D[r >> 1][r & 1][q] : Cx[r & 1][q];
+                const double dv = r < 2 * LD - 2 ? D[r >> 1][r & 1][q]
+                                  : r < 2 * LD   ? buf[(r & 1) * N + (swz(u4) ^ q)]
+                                                 : Cx[r & 1][q];
                 const double pr = fmodmul(dv, kv[gi & 1][q], K);
                 A[kk][q] = r == 0 ? pr : __dadd_rn(A[kk][q], pr);
             }

@@ -969,6 +969,8 @@ __device__ __forceinline__ void wl_sync() {  // order this wave's LDS accesses (
 
 // forward: pass A from registers (polynomial t >> 8), barrier, B and C wave-local; then the units
 // of u = 64w + l for both polynomials into d[p][j] = slot 4u + j
+// TO_LDS: the units' outputs stay in the buffer (read back by this wave's products)
+template <bool TO_LDS = false>
 __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uint64_t (&d)[2][4], const SfTw& T,
                                             const SfC& K) {
     constexpr uint32_t N = G3_N;
@@ -1006,8 +1008,14 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
         uint64_t v0 = pq[u0], v1 = pq[u0 ^ 1], v2 = pq[u0 ^ 2], v3 = pq[u0 ^ 3];
         sf_ct(v0, v2, T, N / 4 + u, K), sf_ct(v1, v3, T, N / 4 + u, K);
         sf_ct(v0, v1, T, N / 2 + 2 * u, K), sf_ct(v2, v3, T, N / 2 + 2 * u + 1, K);
-        d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+        if constexpr (TO_LDS) {
+            uint64_t* pw = buf + q * N;
+            pw[u0] = v0, pw[u0 ^ 1] = v1, pw[u0 ^ 2] = v2, pw[u0 ^ 3] = v3;
+        } else {
+            d[q][0] = v0, d[q][1] = v1, d[q][2] = v2, d[q][3] = v3;
+        }
     }
+    if constexpr (TO_LDS) wl_sync();
 }
 
 // inverse: units of slots 4u .. 4u+3 from registers (second stage's sums folded), C and B
@@ -1099,7 +1107,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
         const uint64_t* ek = bsk + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
         const uint64_t* ek1 = bsk1 + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
-        uint64_t D[DIG][2][4];  // forward outputs of every digit: slots u4 + s of both polynomials
+        uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
@@ -1118,7 +1126,10 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                     v[p * CN + k] = (uint64_t)r;
                 }
             if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
-            sf2_ntt_fwd(buf, v, D[l], TF, K);
+            // one digit: its outputs stay in LDS (frees 16 VGPRs; C3 18.8K -> 20.0K); two digits:
+            // registers (LDS for the second measured 11.4K -> 10.0K on C5b, profiles/r02ah)
+            if (DIG == 1) sf2_ntt_fwd<true>(buf, v, D[l], TF, K);
+            else sf2_ntt_fwd(buf, v, D[l], TF, K);
         }
         // products: group g = (column j, key kk, row r = 2l + polynomial), 4 slots x (W0, W1) of key
         // words each, the next group's loaded before this group's arithmetic; A_kj of slots u4 + s
@@ -1144,7 +1155,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             const uint64_t(&c)[8] = kw[g & 1];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const uint64_t prod = sf_mul(D[r >> 1][r & 1][s], c[s], c[4 + s], K.c);
+                const uint64_t dv = (DIG > 1 || r < RW - 2) ? D[r >> 1][r & 1][s] : buf[(r & 1) * N + (g3_swz(u4) ^ s)];
+                const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c);
                 A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
             }
             if (kk == 1 && r == RW - 1) {
