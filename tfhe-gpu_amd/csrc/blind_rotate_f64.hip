@@ -251,11 +251,7 @@ __device__ __forceinline__ uint32_t f64_tau() {
     return tau;
 }
 
-template <bool NB>
-__device__ __forceinline__ void xbar() {
-    if constexpr (!NB) __syncthreads();
-}
-template <uint32_t TH, bool RED, bool NB = false>
+template <uint32_t TH, bool RED>
 __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], const double* psi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
@@ -268,19 +264,19 @@ __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], con
 #pragma unroll
         for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
     }
-    xbar<NB>();
+    __syncthreads();
     {
         uint32_t ad[8];
         ad_B(tau, ad);
         f64_r8_fwd<RED>(p, ad, 8, tau >> 5, psi, K);
     }
-    xbar<NB>();
+    __syncthreads();
     {
         uint32_t ad[8];
         ad_C(tau, ad);
         f64_r8_fwd<RED>(p, ad, 64, tau >> 2, psi, K);
     }
-    xbar<NB>();
+    __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
         const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
@@ -292,10 +288,10 @@ __device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], con
         if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
     }
-    xbar<NB>();
+    __syncthreads();
 }
 
-template <uint32_t TH, bool RED, bool NB = false>
+template <uint32_t TH, bool RED>
 __device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], const double* ipsi, const F64Const& K) {
     static_assert(TH == 512, "one thread per 8 elements of one polynomial");
     constexpr uint32_t N = 2048;
@@ -312,19 +308,19 @@ __device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], con
         if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K);
         p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
     }
-    xbar<NB>();
+    __syncthreads();
     {
         uint32_t ad[8];
         ad_C(tau, ad);
         f64_r8_inv<RED>(p, ad, 256, tau >> 2, ipsi, K);
     }
-    xbar<NB>();
+    __syncthreads();
     {
         uint32_t ad[8];
         ad_B(tau, ad);
         f64_r8_inv<RED>(p, ad, 32, tau >> 5, ipsi, K);
     }
-    xbar<NB>();
+    __syncthreads();
     {  // pass A: v = elements tau + 256k of polynomial t >> 8, left in registers
         uint32_t ad[8];
         ad_A(tau, ad);
@@ -348,10 +344,8 @@ __device__ __forceinline__ int64_t d2ll(double x) {
 // instead (thread t: polynomial t >> 8, coefficients (t & 255) + 256q, q < 8), so the digits
 // enter the forward transform and the inverse transform's output enters the accumulator
 // update in registers; the products (C', sums, monomials) keep the slot layout.
-// EXP (timing experiments, results invalid): 1 = every round reads the keys of round i & 7
-// (L2-resident), 2 = of round i & 63 (MALL-resident), 4 = no barriers inside the transforms
 // MT: monomial factors from the two LDS tables (mt) instead of the 2N-entry table in memory
-template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, int EXP = 0, bool MT = !RED>
+template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, bool MT = !RED>
 __global__ void __launch_bounds__(TH, 4)
 k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -444,8 +438,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0.0;
-        const uint32_t ki = EXP == 1 ? (i & 7) : EXP == 2 ? (i & 63) : i;
-        const double* ek = bsk + (size_t)ki * round_words;
+        const double* ek = bsk + (size_t)i * round_words;
         // One digit: extraction (registers), forward transform, products with rows 2l, 2l+1.
         // CHECK (WRAP, digit 0): also raise the round's vote, wflag[i & 1], published by the
         // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
@@ -485,7 +478,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
             }
             if constexpr (AM) {
                 // no barrier before: pass A writes this thread's own entries
-                f64_ntt_fwd2048<TH, RED, (EXP & 4) != 0>(buf, v, psi, K);
+                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
             } else {
                 __syncthreads();
                 f64_ntt_fwd<N, TH, RED>(buf, psi, K);
@@ -568,7 +561,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
         }
         __syncthreads();
         double v[8];
-        if constexpr (AM) f64_ntt_inv2048<TH, RED, (EXP & 4) != 0>(buf, v, ipsi, K);
+        if constexpr (AM) f64_ntt_inv2048<TH, RED>(buf, v, ipsi, K);
         else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
@@ -1045,22 +1038,10 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     }();
     if (mt_mode != 2 && P.N == 2048 && fold) {
         const bool on = mt_mode == 1;
-        if (wrap) red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, true, 0, true>) : go(k_blind_rotate_f64<512, 4, true, true, true, 0, false>))
-                      : (on ? go(k_blind_rotate_f64<512, 4, false, true, true, 0, true>) : go(k_blind_rotate_f64<512, 4, false, true, true, 0, false>));
-        else red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, false, 0, true>) : go(k_blind_rotate_f64<512, 4, true, true, false, 0, false>))
-                 : (on ? go(k_blind_rotate_f64<512, 4, false, true, false, 0, true>) : go(k_blind_rotate_f64<512, 4, false, true, false, 0, false>));
-        return hipGetLastError();
-    }
-    // TFHE_F64_EXP (timing only, TFHE_TIMING_EXPERIMENTS=1): key-stream locality experiments, N = 2048
-    static const int exp = [] {
-        const char* e = std::getenv("TFHE_F64_EXP");
-        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
-        return (e && x && x[0] == '1') ? std::atoi(e) : 0;
-    }();
-    if (exp && P.N == 2048) {
-        if (wrap && red) exp == 1 ? go(k_blind_rotate_f64<512, 4, true, true, true, 1>) : exp == 2 ? go(k_blind_rotate_f64<512, 4, true, true, true, 2>) : go(k_blind_rotate_f64<512, 4, true, true, true, 4>);
-        else if (fold && !red) exp == 1 ? go(k_blind_rotate_f64<512, 4, false, true, false, 1>) : exp == 2 ? go(k_blind_rotate_f64<512, 4, false, true, false, 2>) : go(k_blind_rotate_f64<512, 4, false, true, false, 4>);
-        else return hipErrorNotSupported;
+        if (wrap) red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, true, true>) : go(k_blind_rotate_f64<512, 4, true, true, true, false>))
+                      : (on ? go(k_blind_rotate_f64<512, 4, false, true, true, true>) : go(k_blind_rotate_f64<512, 4, false, true, true, false>));
+        else red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, false, true>) : go(k_blind_rotate_f64<512, 4, true, true, false, false>))
+                 : (on ? go(k_blind_rotate_f64<512, 4, false, true, false, true>) : go(k_blind_rotate_f64<512, 4, false, true, false, false>));
         return hipGetLastError();
     }
     if (wrap) {

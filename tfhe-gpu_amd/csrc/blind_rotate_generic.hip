@@ -527,9 +527,7 @@ __device__ __forceinline__ void g3_ntt_inv(W* buf, W (&v)[8], const G3Tw<W>& T, 
     g3_inv_core(v, 4, 0, T, Q2, Q);
 }
 
-// EXP (timing experiments, results invalid): 1 = every round reads the keys of round i & 7
-// (L2-resident), 2 = of round i & 63
-template <typename W, int EXP = 0>
+template <typename W>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__ psi_sh,
                     const W* __restrict__ ipsi, const W* __restrict__ ipsi_sh,
@@ -576,9 +574,8 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) A[kk][j][k] = 0;
-        const uint32_t ki = EXP == 1 ? (i & 7) : EXP == 2 ? (i & 63) : i;
-        const W* ek = bsk + (size_t)ki * round_words;
-        const W* eks = bsk_sh + (size_t)ki * round_words;
+        const W* ek = bsk + (size_t)i * round_words;
+        const W* eks = bsk_sh + (size_t)i * round_words;
         for (uint32_t l = 0; l < P.digits; ++l) {
             const uint32_t lt = l + P.thr, shift = lt * logG;
             int64_t Kd = 0;
@@ -1060,9 +1057,7 @@ __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], 
     sf_inv_core<false>(v, 4, 0, T, K);
 }
 
-// EXP (timing experiments, results invalid): 1 = keys of round 0 only (cache-resident), 4 = inverse
-// twiddles from the forward table in LDS
-template <int DIG, int EXP = 0>
+template <int DIG>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
@@ -1081,7 +1076,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
     uint64_t* mt = psi1_l + N;  // monomial tables
     sf_mono_tables(mt, mono, mono1, Q);
-    const SfTw TF{psi_l, psi1_l}, TI = (EXP & 4) ? SfTw{psi_l, psi1_l} : SfTw{ipsi, ipsi1};
+    const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
@@ -1105,8 +1100,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-        const uint64_t* ek = bsk + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
-        const uint64_t* ek1 = bsk1 + (size_t)((EXP & 1) ? 0 : i) * round_words + u4;
+        const uint64_t* ek = bsk + (size_t)i * round_words + u4;
+        const uint64_t* ek1 = bsk1 + (size_t)i * round_words + u4;
         uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
@@ -1218,14 +1213,9 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
     }();
     if (!v1 && !no_gen3 && P.N == G3_N) {
         const size_t lds = (size_t)4 * G3_N * wb;  // two polynomials + forward twiddles
-        static const int exp = [] {  // TFHE_GEN3_EXP: timing only (TFHE_TIMING_EXPERIMENTS=1)
-            const char* e = std::getenv("TFHE_GEN3_EXP");
-            const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
-            return (e && x && x[0] == '1') ? std::atoi(e) : 0;
-        }();
         auto go3 = [&](auto tag) {
             using W = decltype(tag);
-            auto kern = exp == 1 ? k_blind_rotate_gen3<W, 1> : exp == 2 ? k_blind_rotate_gen3<W, 2> : k_blind_rotate_gen3<W, 0>;
+            auto kern = k_blind_rotate_gen3<W>;
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, (const W*)T.psi, (const W*)T.psi_sh,
                                (const W*)T.ipsi, (const W*)T.ipsi_sh, (const W*)T.mono, (const W*)T.mono_sh, T.eidx,
@@ -1310,11 +1300,6 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
         const char* e = std::getenv("TFHE_SF2");
         return e && e[0] == '0';
     }();
-    static const int exp = [] {  // TFHE_SF2_EXP: timing only (TFHE_TIMING_EXPERIMENTS=1)
-        const char* e = std::getenv("TFHE_SF2_EXP");
-        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
-        return (e && x && x[0] == '1') ? std::atoi(e) : 0;
-    }();
     if (!no_sf2 && (P.digits == 1 || P.digits == 2)) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1322,16 +1307,8 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
                                (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
-        if (P.digits == 2) {
-            go(k_blind_rotate_sf2<2>);
-            return hipGetLastError();
-        }
-        switch (exp) {
-            case 1: go(k_blind_rotate_sf2<1, 1>); break;
-            case 4: go(k_blind_rotate_sf2<1, 4>); break;
-            case 5: go(k_blind_rotate_sf2<1, 5>); break;
-            default: go(k_blind_rotate_sf2<1>); break;
-        }
+        if (P.digits == 2) go(k_blind_rotate_sf2<2>);
+        else go(k_blind_rotate_sf2<1>);
         return hipGetLastError();
     }
     (void)hipFuncSetAttribute((const void*)k_blind_rotate_gen3sf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
