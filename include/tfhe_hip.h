@@ -107,7 +107,7 @@ typedef struct tfhe_info {
 #define TFHE_BR_F64 2          /* exact-FP64 kernel, blind_rotate_f64.hip */
 #define TFHE_BR_F64_FOLD 3     /* exact-FP64 kernel, top digit's transforms eliminated */
 #define TFHE_BR_RNS 4          /* four-prime RNS kernel (2^53 < Q < 2^58), blind_rotate_rns.hip */
-#define TFHE_BR_SF 5           /* special-form u64 kernel (Q = 2^54 - c), blind_rotate_generic.hip gen3sf */
+#define TFHE_BR_SF 5           /* special-form u64 kernel (Q = 2^54 - c), blind_rotate_generic.hip sf2 / gen3sf */
 
 typedef struct tfhe_ctx tfhe_ctx;
 

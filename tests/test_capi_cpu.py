@@ -131,3 +131,21 @@ def test_key_file_size_field_checked_before_allocation(tmp_path):
     f.write_bytes(hdr)
     with pytest.raises(capi.TfheError, match="size field"):
         tfhe_amd.BinFHEContextHIP.from_key_file(p, str(f))
+
+
+def test_cpp_example_builds_and_links(capi, tmp_path):
+    """examples/time_estimate.cpp (the reference's time-estimate.cpp against the C-ABI) compiles
+    with the host compiler alone, links to libtfhe_hip.so and runs up to its first device call
+    (no operation selected: it prints the ABI version and exits)."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "time_estimate"
+    lib_dir = os.path.join(root, "tfhe-gpu_amd", "lib")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "examples", "time_estimate.cpp"), "-L", lib_dir, "-ltfhe_hip",
+                    f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe), "1", "none"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "C-ABI version 2"

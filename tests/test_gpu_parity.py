@@ -448,6 +448,47 @@ def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     orc.close()
 
 
+@pytest.mark.parametrize("shape,path", [(s, p) for s in ("logq11", "logq11-thr1", "arb11-thr1", "STD128_AP")
+                                        for p in ("fast", "generic")])
+def test_n1024_digit_shapes_parity(capi, oracle, shape, path):
+    """The four-wavefront kernel's other digit shapes (N = 1024, Q = 2^27 - 2^11 + 1):
+    logQ = 11 without a thrown digit (six 5-bit digits, top digit eliminated), logQ = 11 with
+    one thrown digit (five transformed digits, the thrown one's carry kept; EvalFloor's context
+    in the reference's time-estimate.cpp:100) and STD128_AP (three 9-bit digits whose top
+    digit wraps, so none is eliminated).  Fast kernel (br_kernel 1) and generic v2
+    (TFHE_FORCE_GENERIC=1) equal the oracle for accumulator boundary values and both a-moduli."""
+    if shape == "STD128_AP":
+        op, cp = oracle.params_from_set(shape), capi.params_from_set(shape)
+    else:
+        arb, thr = shape.startswith("arb"), 1 if shape.endswith("thr1") else 0
+        op = oracle.params_from_logq("STD128", arb, 11, 0, 0, thr)
+        cp = capi.params_from_logq("STD128", arb, 11, 0, 0, thr)
+    rs = np.random.default_rng(17)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    bsk[: 4 * op.N] = np.array([0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1], dtype=np.uint64).repeat(op.N)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    if path == "generic":
+        os.environ["TFHE_FORCE_GENERIC"] = "1"
+    try:
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    finally:
+        os.environ.pop("TFHE_FORCE_GENERIC", None)
+    assert ctx.info().br_kernel == (1 if path == "fast" else 0)
+    B = 3
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    half = op.Q >> 1
+    acc[0, :, :8] = [0, op.Q - 1, half, half + 1, half - 1, 1, op.Q - 2, half + 2]
+    acc[1] = np.where(rs.integers(0, 2, (2, op.N)) == 1, half, half + 1).astype(np.uint64)  # extreme digits
+    for amod in (op.q, 2 * op.N):
+        a = rs.integers(0, amod, (B, op.n), dtype=np.uint64)
+        assert np.array_equal(ctx.EvalAcc(a, amod, acc), orc.eval_acc(a, amod, acc))
+    if shape == "logq11-thr1":  # EvalFloor end to end (the reference example's call)
+        ct = random_cts(rs, 4, cp.n, cp.q)
+        assert np.array_equal(ctx.EvalFloor(ct, cp.q, 1), orc.eval_floor(ct, cp.q, 1))
+    ctx.GPUClean()
+    orc.close()
+
+
 @pytest.mark.parametrize("pset", ["STD128Q", "STD128Q_OPT"])
 def test_wrap_correction_late_round(capi, oracle, pset):
     """The STD128Q fold's WRAP correction in the LAST round (vote flag of round parity

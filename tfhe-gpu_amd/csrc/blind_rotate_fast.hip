@@ -1,7 +1,9 @@
 // blind_rotate_fast.hip -- CGGI blind rotation specialised for the STD128 class
 // (N = 1024, dG2 = 8, baseG = 2^7, Q < 2^27; STD128, STD128_OPT): the key/table packing
 // shared by both specialised kernels, the two-wavefront kernel k_blind_rotate_fast2 and the
-// launcher, which runs the four-wavefront kernel of blind_rotate_fast4.hip by default.
+// launcher, which runs the four-wavefront kernel of blind_rotate_fast4.hip by default.  The
+// four-wavefront kernel and the packing also take the other N = 1024, Q < 2^27 digit shapes
+// fast4_shape_supported lists (logQ = 11 contexts, STD128_AP).
 //
 // Same math as the generic kernel and the oracle (rgsw-acc-cggi.cpp:246-307 and
 // rgsw-acc.cpp:57-111), re-organised for gfx950 (k_blind_rotate_fast2's layout below;
@@ -663,10 +665,13 @@ k_blind_rotate_fast2(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 }
 
 // generic (plain, N^-1-scaled) BSK and tables -> centred Montgomery copies: key rows with the
-// top digit folded in (hc[l] = 2^(7l-21), hc[3] = N 2^-21 mod Q; see k_blind_rotate_fast2),
-// twiddles packed per pass (table-block comment above), monomials in the rotated layout.
+// top digit folded in when M.fold (hc[l] = G^(l - top), hc[top] = N G^-top mod Q; STD128:
+// 2^(7l-21) and N 2^-21, see k_blind_rotate_fast2), else plain; twiddles packed per pass
+// (table-block comment above), monomials in the rotated layout.
 struct PackMode {
-    uint32_t hc[4];
+    uint32_t hc[8];
+    uint32_t rw;    // key rows per (key, column) = dG2
+    uint32_t fold;  // top digit eliminated
 };
 __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t words, const uint32_t* __restrict__ psi,
                             const uint32_t* __restrict__ ipsi, const uint32_t* __restrict__ mono,
@@ -677,11 +682,14 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
         return m > Q / 2 ? (int32_t)m - (int32_t)Q : (int32_t)m;
     };
     if (idx < words) {
-        // idx = (((i * 2 + k) * 8 + row) * 2 + j) * N + slot; row = 2l + p
-        const uint32_t row = (uint32_t)((idx / (2 * FN)) % FDG2), l = row >> 1, p = row & 1;
-        const size_t i6 = idx + ((size_t)(6 + p) - row) * 2 * FN;  // row 6 + p, same k, j, slot
-        const uint64_t w6 = (uint64_t)(bsk[i6] % Q) * M.hc[l] % Q;
-        const uint32_t v = l < 3 ? (uint32_t)(((uint64_t)(bsk[idx] % Q) + Q - w6) % Q) : (uint32_t)w6;
+        // idx = (((i * 2 + k) * rw + row) * 2 + j) * N + slot; row = 2l + p
+        const uint32_t row = (uint32_t)((idx / (2 * FN)) % M.rw), l = row >> 1, p = row & 1, top = M.rw / 2 - 1;
+        uint32_t v = bsk[idx] % Q;
+        if (M.fold) {
+            const size_t it = idx + ((size_t)(2 * top + p) - row) * 2 * FN;  // row 2 top + p, same k, j, slot
+            const uint64_t wt = (uint64_t)(bsk[it] % Q) * M.hc[l] % Q;
+            v = l < top ? (uint32_t)(((uint64_t)v + Q - wt) % Q) : (uint32_t)wt;
+        }
         out[TB_WORDS + idx] = mont(v);
     }
     if (idx < TW_WORDS) {
@@ -712,12 +720,28 @@ __global__ void k_pack_fast(uint32_t Q, const uint32_t* __restrict__ bsk, size_t
 
 }  // namespace
 
-bool fast_path_supported(const BRParams& P, int word_bits) {
-    return word_bits == 32 && P.N == FN && P.dG2 == FDG2 && P.digits == FDIG && P.thr == 0 && P.logG == FLOGG &&
-           P.Q < (1ull << 27) && P.n > 0;
+// The digit shape of P for the 4-wavefront kernel; fold when no digit is thrown and the top
+// digit of every centred coefficient c in [-(Q>>1)-1, Q>>1) stays in [-G/2, G/2) (no wrap), so
+// that c = sum_l d_l G^l exactly (DESIGN.md 3.1 idea 1).
+static Fast4Shape fast_shape(const BRParams& P) {
+    Fast4Shape sh{(int)P.digits, (int)P.logG, (int)P.thr, false};
+    if (P.thr == 0 && P.digits >= 2 && P.logG >= 1 && P.logG * P.digits <= 40) {
+        const int64_t G = (int64_t)1 << P.logG, Qh = (int64_t)(P.Q >> 1);
+        const uint32_t top = P.digits - 1;
+        int64_t K = 0;
+        for (uint32_t z = 0; z < top; ++z) K = K * G + G / 2;  // (G/2)(G^top - 1)/(G - 1)
+        const int64_t lo = (-Qh - 1 + K) >> (P.logG * top), hi = (Qh - 1 + K) >> (P.logG * top);
+        sh.fold = lo >= -G / 2 && hi < G / 2;
+    }
+    return sh;
 }
 
-size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * FDG2 * 2 * FN + TB_WORDS) * 4; }
+bool fast_path_supported(const BRParams& P, int word_bits) {
+    return word_bits == 32 && P.N == FN && P.dG2 == 2 * P.digits && P.Q < (1ull << 27) && P.n > 0 &&
+           fast4_shape_supported(fast_shape(P));
+}
+
+size_t bsk_fast_bytes(const BRParams& P) { return ((size_t)P.n * 2 * P.dG2 * 2 * FN + TB_WORDS) * 4; }
 
 namespace {
 // TFHE_FAST_VARIANT selects the kernel build (A/B experiments): 30-58 k_blind_rotate_fast2
@@ -767,11 +791,16 @@ int get_fast_variant() { return fast_variant(); }
 
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
                                 hipStream_t s) {
-    const size_t words = (size_t)P.n * 2 * FDG2 * 2 * FN;
+    const size_t words = (size_t)P.n * 2 * P.dG2 * 2 * FN;
+    const Fast4Shape sh = fast_shape(P);
+    if (P.dG2 > 16 || !fast4_shape_supported(sh)) return hipErrorNotSupported;
     PackMode M{};
-    const uint64_t Q = P.Q, i21 = powmod(2, Q - 1 - 21, Q);  // 2^-21 (Q prime)
-    for (int l = 0; l < 3; ++l) M.hc[l] = (uint32_t)((unsigned __int128)powmod(2, 7 * l, Q) * i21 % Q);
-    M.hc[3] = (uint32_t)((unsigned __int128)FN * i21 % Q);
+    M.rw = P.dG2;
+    M.fold = sh.fold;
+    const uint32_t top = P.digits - 1;
+    const uint64_t Q = P.Q, igt = powmod(2, Q - 1 - (uint64_t)P.logG * top, Q);  // G^-top (Q prime)
+    for (uint32_t l = 0; l < top; ++l) M.hc[l] = (uint32_t)((unsigned __int128)powmod(2, (uint64_t)P.logG * l, Q) * igt % Q);
+    M.hc[top] = (uint32_t)((unsigned __int128)FN * igt % Q);
     hipLaunchKernelGGL(k_pack_fast, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint32_t)P.Q,
                        (const uint32_t*)bsk, words, (const uint32_t*)T.psi, (const uint32_t*)T.ipsi,
                        (const uint32_t*)T.mono, (int32_t*)bsk_fast, M);
@@ -803,8 +832,10 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     const int32_t* tabs = (const int32_t*)bsk_fast;
     const int32_t* bsk = tabs + TB_WORDS;
     const int variant = fast_variant();
-    if (variant >= 59)
-        return launch_blind_rotate_fast4(variant, &K, P.n, loga, tabs + T_WORDS, bsk, a, acc, B, s);
+    const Fast4Shape sh = fast_shape(P);
+    const bool std128 = sh.dig == (int)FDIG && sh.logg == (int)FLOGG && sh.thr == 0 && sh.fold;
+    if (variant >= 59 || !std128)  // the two-wavefront builds know only the STD128 shape
+        return launch_blind_rotate_fast4(variant, sh, &K, P.n, loga, tabs + T_WORDS, bsk, a, acc, B, s);
     auto launch2 = [&](auto kern, int nb = 1) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes2(2, nb));
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(TPC * 2), lds_bytes2(2, nb), s, K, P.n, loga,

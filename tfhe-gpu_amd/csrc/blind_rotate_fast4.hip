@@ -31,7 +31,7 @@
 namespace tfhe {
 namespace f4 {
 
-constexpr uint32_t FN = 1024, FDG2 = 8, FDIG = 4, FLOGG = 7;
+constexpr uint32_t FN = 1024;
 constexpr int TPC = 256;
 
 // Global table block written by k_pack_fast (blind_rotate_fast.hip), int32 centred Montgomery:
@@ -345,7 +345,13 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 // XB: cross-exchange areas (2: alternate, no barrier before the stores; 1: one area + a barrier)
 // CTS (NCT = 1): ciphertexts per workgroup, in lockstep through the transforms' barriers, so
 // their wavefronts read each key row at about the same time (L1 reuse instead of L2 traffic).
-template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2, int CTS = 1>
+// Digit shape (any N = 1024 set with Q < 2^27 and baseG <= 2^9; tools/bounds_fast4.py): DIG digits
+// per polynomial (dG2 = 2 DIG), baseG = 2^LOGG, THR thrown digits.  FOLD: the top digit is
+// eliminated (its rows carry C = N^-1 NTT(acc), k_pack_fast folds it into the other rows), valid
+// when THR = 0 and the top digit never wraps (the host checks); otherwise every digit is
+// transformed.  Pass 0's lookup tables hold digits in [-64, 64), so they need LOGG <= 7.
+template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2, int CTS = 1, int DIG = 4, int LOGG = 7,
+          int THR = 0, bool FOLD = true>
 __global__ void __launch_bounds__(TPC * CTS, MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
@@ -353,6 +359,13 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     constexpr int P = 2 * NCT;
     extern __shared__ __align__(16) int32_t lds[];
     static_assert(CTS == 1 || NCT == 1, "CTS > 1 needs NCT = 1");
+    constexpr uint32_t RW = 2 * DIG;                  // key rows per (key, column)
+    constexpr int TOP = DIG - 1;                       // FOLD: the eliminated digit (its rows: the C products)
+    constexpr int NT = FOLD ? DIG - 1 : DIG;           // transformed digits per round
+    static_assert(!FOLD || THR == 0, "top-digit elimination needs every digit");
+    static_assert(LOGG * (THR + NT) <= 32, "digit field beyond 32 bits");
+    // XB = 2 alternates cross areas between consecutive transforms: laid out for STD128's order only
+    static_assert(XB == 1 || (DIG == 4 && FOLD), "two cross areas need the STD128 digit order");
     const uint32_t cl = __builtin_amdgcn_readfirstlane(threadIdx.x / TPC);  // ciphertext in the workgroup
     const uint32_t tid = threadIdx.x % TPC;
     const uint32_t wg_ct = blockIdx.x * CTS * NCT + cl;                     // first ciphertext of this lane
@@ -401,32 +414,34 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 
     // C = N^-1 NTT(acc) in L5
     int32_t Cp[P][4];
+    if constexpr (FOLD) {
 #pragma unroll
-    for (int q = 0; q < NCT; ++q)
+        for (int q = 0; q < NCT; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][1][r];
-    ntt_fwd<XA1, P, EXP, 0, PRE, (OPT & 8) != 0>(Cp, lds, C, K);
+            for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][1][r];
+        ntt_fwd<XA1, P, EXP, 0, PRE, (OPT & 8) != 0>(Cp, lds, C, K);
 #pragma unroll
-    for (int p = 0; p < P; ++p)
+        for (int p = 0; p < P; ++p)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Cp[p][r] = smul(Cp[p][r], K.ninv, K);
+            for (int r = 0; r < 4; ++r) Cp[p][r] = smul(Cp[p][r], K.ninv, K);
+    }
 
-    constexpr uint32_t ROWB = 2 * FDG2 * 2 * FN * 4;  // key bytes per round
+    constexpr uint32_t ROWB = 2 * RW * 2 * FN * 4;  // key bytes per round
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(bsk), 0, (int)(n * ROWB), 0x00020000);
     const uint32_t voff = tid * 16;  // 4 consecutive slots per lane
     const uint32_t et = 2 * (__builtin_bitreverse32(tid) >> 24) + 1;  // slot 4t + r: e = 512 bitrev2(r) + et
     const uint32_t amask = (1u << loga) - 1, ashift = 11 - loga;
 
-    // group gi = (key k, column j) of digit l (l = 3: the C rows): rows 2l (poly 0), 2l + 1 (poly 1)
+    // group gi = (key k, column j) of digit l (FOLD, l = TOP: the C rows): rows 2l (poly 0), 2l + 1 (poly 1)
     auto issue = [&](v4i (&pw)[2], uint32_t round_off, int l, int gi) {
         const int k = gi >> 1, j = gi & 1;
         if constexpr ((EXP & 2) != 0) {
             pw[0] = v4i{(int)round_off, l, gi, 4}, pw[1] = pw[0] + 1;
             return;
         }
-        pw[0] = ld_bsk(rsrc, voff, round_off + ((k * FDG2 + 2 * l) * 2 + j) * FN * 4);
-        pw[1] = ld_bsk(rsrc, voff, round_off + ((k * FDG2 + 2 * l + 1) * 2 + j) * FN * 4);
+        pw[0] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l) * 2 + j) * FN * 4);
+        pw[1] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l + 1) * 2 + j) * FN * 4);
     };
     auto mac = [&](int64_t (&s)[NCT][2][2][4], const int32_t (&X)[P][4], const v4i (&pw)[2], int gi) {
         const int k = gi >> 1, j = gi & 1;
@@ -442,8 +457,13 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     };
 
     v4i pw[4][2];  // key ring: the rows of the digit being consumed / about to be
+    // FOLD: the C rows of round 0.  Otherwise digit 0's rows are issued at the start of each
+    // round (not during the previous round's last products), so the ring is dead across the
+    // monomial step and the inverse transform: fewer live registers (no spills in the loop).
+    if constexpr (FOLD) {
 #pragma unroll
-    for (int gi = 0; gi < 4; ++gi) issue(pw[gi], 0, 3, gi);
+        for (int gi = 0; gi < 4; ++gi) issue(pw[gi], 0, TOP, gi);
+    }
 
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t round_off = i * ROWB;
@@ -465,35 +485,44 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
                     for (int r = 0; r < 4; ++r) s[q][k][j][r] = 0;
 
         // the C digit (no transform); its groups' registers take digit 0's rows
+        if constexpr (FOLD) {
 #pragma unroll
-        for (int gi = 0; gi < 4; ++gi) {
-            __builtin_amdgcn_sched_barrier(0);
-            mac(s, Cp, pw[gi], gi);
-            issue(pw[gi], round_off, 0, gi);
+            for (int gi = 0; gi < 4; ++gi) {
+                __builtin_amdgcn_sched_barrier(0);
+                mac(s, Cp, pw[gi], gi);
+                issue(pw[gi], round_off, 0, gi);
+            }
+        } else {
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) issue(pw[gi], round_off, 0, gi);
         }
 #pragma unroll
-        for (uint32_t l = 0; l < FDIG - 1; ++l) {
-            const int32_t kl = (int32_t)(((1u << (FLOGG * l)) - 1) / ((1u << FLOGG) - 1)) << (FLOGG - 1);
+        for (uint32_t l = 0; l < NT; ++l) {
+            // closed-form signed digit lt (thrown digits counted): sext_LOGG((c + K_lt) >> LOGG lt)
+            const uint32_t lt = l + THR;
+            const int32_t kl = (int32_t)(((1u << (LOGG * lt)) - 1) / ((1u << LOGG) - 1)) << (LOGG - 1);
             int32_t X[P][4];
 #pragma unroll
             for (int q = 0; q < NCT; ++q)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    X[2 * q][r] = __builtin_amdgcn_sbfe(acc[q][0][r] + kl, FLOGG * l, FLOGG);
-                    X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, FLOGG * l, FLOGG);
+                    X[2 * q][r] = __builtin_amdgcn_sbfe(acc[q][0][r] + kl, LOGG * lt, LOGG);
+                    X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, LOGG * lt, LOGG);
                 }
             __builtin_amdgcn_sched_barrier(0);
-            constexpr int SM = (OPT & 4) ? 2 : (OPT & 1) ? 1 : 0;
+            constexpr int SM = LOGG > 7 ? 0 : (OPT & 4) ? 2 : (OPT & 1) ? 1 : 0;
             if (l & 1) ntt_fwd<XA1, P, EXP, SM, PRE, (OPT & 8) != 0>(X, lds, C, K);
             else ntt_fwd<XA0, P, EXP, SM, PRE, (OPT & 8) != 0>(X, lds, C, K);
-            // next digit's rows (after digit 2: the next round's C rows; the last round re-fetches)
-            const uint32_t noff = l < 2 ? round_off : (i + 1 < n ? i + 1 : i) * ROWB;
-            const int nl = l < 2 ? (int)l + 1 : 3;
+            // next digit's rows (after the last, FOLD: the next round's C rows; the last round
+            // re-fetches)
+            const bool last = l + 1 == NT;
+            const uint32_t noff = !last ? round_off : (i + 1 < n ? i + 1 : i) * ROWB;
+            const int nl = !last ? (int)l + 1 : TOP;
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi) {
                 __builtin_amdgcn_sched_barrier(0);
                 mac(s, X, pw[gi], gi);
-                issue(pw[gi], noff, nl, gi);
+                if (FOLD || !last) issue(pw[gi], noff, nl, gi);
             }
         }
 
@@ -519,11 +548,13 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             }
         }
         // C <- C + S, reduced every 8 rounds
+        if constexpr (FOLD) {
 #pragma unroll
-        for (int p = 0; p < P; ++p)
+            for (int p = 0; p < P; ++p)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Cp[p][r] += S[p][r];
-        if ((i & 7) == 7) {
+                for (int r = 0; r < 4; ++r) Cp[p][r] += S[p][r];
+        }
+        if (FOLD && (i & 7) == 7) {
 #pragma unroll
             for (int p = 0; p < P; ++p)
 #pragma unroll
@@ -612,8 +643,16 @@ hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, h
     return hipGetLastError();
 }
 
-hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
-                                     const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s) {
+bool fast4_shape_supported(const Fast4Shape& sh) {
+    return (sh.dig == 4 && sh.logg == 7 && sh.thr == 0 && sh.fold) ||   // STD128, STD128_OPT
+           (sh.dig == 6 && sh.logg == 5 && sh.thr == 0 && sh.fold) ||   // logQ = 11, no thrown digit
+           (sh.dig == 5 && sh.logg == 5 && sh.thr == 1 && !sh.fold) ||  // logQ = 11, one thrown digit
+           (sh.dig == 3 && sh.logg == 9 && sh.thr == 0 && !sh.fold);    // STD128_AP (top digit wraps)
+}
+
+hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
+                                     const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
+                                     size_t B, hipStream_t s) {
     const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
     auto launch = [&](auto kern, int nct, int xb = 2, int cts = 1) {
         const size_t lb = f4::lds_bytes(2 * nct, xb, cts);
@@ -621,6 +660,20 @@ hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uin
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct * cts - 1) / (nct * cts))), dim3(f4::TPC * cts), lb, s, Kc,
                            n, loga, tabs4, bsk, a, acc, (uint32_t)B);
     };
+    // other digit shapes: the default build (variant 60's template arguments) at that shape
+    if (sh.dig == 6 && sh.logg == 5 && sh.thr == 0 && sh.fold) {
+        launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 6, 5, 0, true>, 1, 1);
+        return hipGetLastError();
+    }
+    if (sh.dig == 5 && sh.logg == 5 && sh.thr == 1 && !sh.fold) {
+        launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 5, 5, 1, false>, 1, 1);
+        return hipGetLastError();
+    }
+    if (sh.dig == 3 && sh.logg == 9 && sh.thr == 0 && !sh.fold) {
+        launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 3, 9, 0, false>, 1, 1);
+        return hipGetLastError();
+    }
+    if (!(sh.dig == 4 && sh.logg == 7 && sh.thr == 0 && sh.fold)) return hipErrorNotSupported;
     switch (variant) {
         case 59: launch(f4::k_blind_rotate_fast4<3, 1, 0, 3, 1>, 1, 1); break;
         case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;      // two ciphertexts per wavefront

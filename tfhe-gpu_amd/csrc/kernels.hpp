@@ -46,11 +46,18 @@ size_t bsk_fast_bytes(const BRParams& P);
 bool set_fast_variant(int v);
 int get_fast_variant();
 // 4-wavefront variant (blind_rotate_fast4.hip): its table block, packed behind the fast tables,
-// and its launch (K: the fast kernel's FastConst).
+// and its launch (K: the fast kernel's FastConst).  Digit shape: dig digits per polynomial
+// (dG2 = 2 dig), baseG = 2^logg, thr thrown digits, fold = top digit eliminated.
+struct Fast4Shape {
+    int dig, logg, thr;
+    bool fold;
+};
+bool fast4_shape_supported(const Fast4Shape& sh);
 size_t fast4_table_words();
 hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, hipStream_t s);
-hipError_t launch_blind_rotate_fast4(int variant, const void* K, uint32_t n, uint32_t loga, const int32_t* tabs4,
-                                     const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s);
+hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
+                                     const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
+                                     size_t B, hipStream_t s);
 
 // Exact-FP64 blind rotation for 2^32 <= Q < 2^40 (STD192 class): keys/tables as centred
 // doubles derived on device from the generic (u64) arena.

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Throughput of the other SURVEY.md 8(d) configurations on one MI355X (C3, C4, C5a, C5b).
+"""Throughput of the other SURVEY.md 8(d) configurations on one MI355X (C3, C4, C5a, C5b; F11 /
+F11t0: EvalFloor in the reference example's logQ = 11 context, with / without the thrown digit).
 
 bench.py measures the headline C2 (STD128 NAND, inputs resident in HBM).  This script
 times the host-array entry points (EvalFunc / EvalBinGate / EvalSign: PCIe transfers
@@ -40,6 +41,9 @@ def main():
         elif name == "C5a":   # STD128Q EvalSign, ciphertext modulus 2^23, B=1024
             p = capi.params_from_set("STD128Q")
             B, op = 1024, "EvalSign(Qin=2^23)"
+        elif name in ("F11", "F11t0"):  # EvalFloor in the logQ = 11 context (time-estimate.cpp:100), B=4096
+            p = capi.params_from_logq("STD128", False, 11, 0, 0, 1 if name == "F11" else 0)
+            B, op = 4096, "EvalFloor(roundbits=1)"
         elif name == "C5b":   # STD128 logQ=23 throw=1 EvalSign, ciphertext modulus 2^23, B=1024
             p = capi.params_from_logq("STD128", False, 23, 0, 0, 1)
             B, op = 1024, "EvalSign(Qin=2^23)"
@@ -57,6 +61,9 @@ def main():
             ct = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
             lut = np.array([(x ** 3) % 8 for x in range(8)] * (p.q // 8), dtype=np.uint64)
             call = lambda: ctx.EvalFunc(ct, lut)
+        elif name in ("F11", "F11t0"):
+            ct = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
+            call = lambda: ctx.EvalFloor(ct, p.q, 1)
         elif name in ("C4", "C2host"):
             c1 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
             c2 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)

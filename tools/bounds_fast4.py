@@ -3,7 +3,8 @@
 (forward, Cooley-Tukey) and the reverse (inverse, Gentleman-Sande), signed Montgomery
 products (|smul(y, w)| <= |y| (Q/2) / 2^32 + Q/2).  RED lists, per inverse pass, which stage's
 sum outputs are reduced (smul by R mod Q).  Asserts every 32-bit value < 2^31, the external
-product row sums < 2^63, and the accumulator update window.  Run: python3 tools/bounds_fast4.py [Q]"""
+product row sums < 2^63, and the accumulator update window, for every digit shape the kernel is
+built for.  Run: python3 tools/bounds_fast4.py [Q]"""
 import sys
 
 Q = int(sys.argv[1]) if len(sys.argv) > 1 else 134215681
@@ -53,16 +54,32 @@ def inv(b_in):
     return b
 
 
-F = max(max(fwd([64] * 1024)), max(fwd([64] * 1024, small=True)))  # digit transforms (both pass-0 forms)
-C0 = smul_b(max(fwd([Qh + 1] * 1024)))    # C = N^-1 NTT(acc)
-rowsum = 6 * F * Qh + 2 * F * Qh          # 3 digits + C (kept <= F) over 2 polynomials
-assert rowsum < 2 ** 63
-A = rowsum / 2 ** 32 + Qh                 # sredc of the row sum
-S = (2 * A * Qh) / 2 ** 32 + Qh           # monomial combination
-Cmax = C0 + 8 * S
-Cred = smul_b(Cmax)
-assert max(C0, Cred) + 7 * S <= F
-out = max(inv([S] * 1024))
-assert out < 3 * Q, f"inverse output {out / Q:.2f}Q"
-print(f"Q={Q}: fwd {F / Q:.3f}Q, C {(max(C0, Cred) + 7 * S) / Q:.3f}Q, S {S / Q:.3f}Q, "
-      f"inverse out {out / Q:.3f}Q (reductions {RED})  OK")
+
+
+def check(dig, logg, fold):
+    """DIG digits of base 2^logg per polynomial; fold = top digit eliminated (C rows)"""
+    dmax = 1 << (logg - 1)
+    F = max(fwd([dmax] * 1024))
+    if logg <= 7:  # pass 0 from the lookup tables (digits in [-64, 64))
+        F = max(F, max(fwd([dmax] * 1024, small=True)))
+    nt = dig - 1 if fold else dig          # transformed digits
+    rowsum = 2 * nt * F * Qh + (2 * F * Qh if fold else 0)  # C rows kept <= F
+    assert rowsum < 2 ** 63
+    A = rowsum / 2 ** 32 + Qh                 # sredc of the row sum
+    S = (2 * A * Qh) / 2 ** 32 + Qh           # monomial combination
+    msg = ""
+    if fold:
+        C0 = smul_b(max(fwd([Qh + 1] * 1024)))    # C = N^-1 NTT(acc)
+        Cred = smul_b(C0 + 8 * S)
+        assert max(C0, Cred) + 7 * S <= F
+        msg = f", C {(max(C0, Cred) + 7 * S) / Q:.3f}Q"
+    out = max(inv([S] * 1024))
+    assert out < 3 * Q, f"inverse output {out / Q:.3f}Q"
+    print(f"Q={Q} dig={dig} logG={logg} fold={fold}: fwd {F / Q:.3f}Q{msg}, S {S / Q:.3f}Q, "
+          f"row sums 2^{rowsum.bit_length() if isinstance(rowsum, int) else __import__('math').log2(rowsum):.1f}, "
+          f"inverse out {out / Q:.3f}Q (reductions {RED})  OK")
+
+
+# the shapes blind_rotate_fast4.hip instantiates (fast4_shape_supported)
+for shape in ((4, 7, True), (6, 5, True), (5, 5, False), (3, 9, False)):
+    check(*shape)
