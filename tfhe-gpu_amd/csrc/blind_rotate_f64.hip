@@ -25,11 +25,13 @@ namespace tfhe {
 namespace {
 
 
+typedef double v2d __attribute__((ext_vector_type(2)));  // one 16-byte buffer load: two doubles
 struct F64Const {
     double Q, Qinv;
     int64_t Qi;
     double Ninv;  // N^-1 mod Q, centred (FOLD)
     double wfac;  // 2^(gL) N^-1 mod Q, centred (WRAP)
+    uint32_t kround_mask;  // timing experiments only (results invalid): key rows of round i & mask
 };
 
 // Top-digit elimination (FOLD), as in the specialised STD128 kernel (blind_rotate_fast4.hip):
@@ -727,9 +729,9 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
     const size_t round_words = (size_t)4 * P.dG2 * N;
-    uint32_t ex[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) ex[s] = 2 * (__builtin_bitreverse32(u4 + s) >> 21) + 1;
+    const uint64_t amask = amod - 1;  // amod divides 2N (dev_blind_rotate): a power of two
+    // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
 
     int64_t acc[2][CN];  // canonical [0, Q), pass A's layout
 #pragma unroll
@@ -761,9 +763,9 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const uint32_t shiftL = P.digits * logG;
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint64_t ar = ap[i] & amask;  // a_i mod amod, rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-        const double* ek = bsk + (size_t)i * round_words + u4;
+        const uint32_t round_off = (i & K.kround_mask) * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
         auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4], bool sync) {
@@ -823,13 +825,16 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         constexpr int RW = 2 * LD + 2, NG = 4 * RW;
         auto kload = [&](int gi, double (&kv)[4]) {
             const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
-            const double* kp = ek + ((size_t)(kk * P.dG2 + r) * 2 + j) * N;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) kv[q] = kp[q];
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
+            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
+            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
         };
-        uint32_t ip[4];
+        uint32_t ip[4];  // slot x evaluates at psi^(2 bitrev(x) + 1) (recomputed each round, the
+        uint32_t uo = u4;  // opaque copy keeps the compiler from hoisting four live values)
+        asm volatile("" : "+v"(uo));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ip[q] = (ex[q] * ai) & (twoN - 1);
+        for (int q = 0; q < 4; ++q) ip[q] = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
         double S[2][4], A[2][4];
         double kv[2][4];
         kload(0, kv[0]);
@@ -996,6 +1001,13 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     K.Ninv = -(double)((P.Q - 1) / P.N);
     const uint64_t wf = (uint64_t)((unsigned __int128)pow_mod(2, (uint64_t)P.logG * P.digits, P.Q) * ninv % P.Q);
     K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
+    K.kround_mask = ~0u;
+    {  // TFHE_F64_KEYROUNDS=m (timing only, needs TFHE_TIMING_EXPERIMENTS=1): rounds read the key
+       // rows of round i & (m - 1), an L2-resident set (results invalid)
+        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+        const char* e = std::getenv("TFHE_F64_KEYROUNDS");
+        if (x && x[0] == '1' && e && e[0]) K.kround_mask = (uint32_t)std::atoi(e) - 1;
+    }
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const bool wrap = fold && !fold_exact(P);
     const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double);  // psi, ipsi, two polynomials, monomial tables
@@ -1015,7 +1027,9 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         const char* e = std::getenv("TFHE_F64W_MT");
         return e && e[0] ? e[0] - '0' : 2;
     }();
-    if (!no_w && P.N == 2048 && fold && (P.digits == 2 || P.digits == 3)) {
+    // f64w addresses the keys with 32-bit byte offsets (buffer resource)
+    const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
+    if (!no_w && fits32 && P.N == 2048 && fold && (P.digits == 2 || P.digits == 3)) {
         const bool m = mtw != 0;  // tables: STD192 474 -> 385 ms, STD128Q 319 -> 288 ms (profiles/r02ae)
         const int ld = (int)P.digits - 1;
 #define F64W_GO(R, W, L)                                                                     \

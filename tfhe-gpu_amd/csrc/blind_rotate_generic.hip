@@ -694,6 +694,21 @@ struct SfTw {
     const uint64_t* __restrict__ w0;
     const uint64_t* __restrict__ w1;
 };
+// the same table pair in memory through buffer resources: a lane's twiddle address is a 32-bit
+// offset from a uniform base, so no 64-bit per-lane addresses stay live across the round loop
+// (sf2's two-digit build kept six of them in scratch)
+struct SfTwB {
+    __amdgpu_buffer_rsrc_t r0, r1;
+};
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t tw0(const SfTw& T, uint32_t i) { return T.w0[i]; }
+__device__ __forceinline__ uint64_t tw1(const SfTw& T, uint32_t i) { return T.w1[i]; }
+__device__ __forceinline__ uint64_t tw0(const SfTwB& T, uint32_t i) {
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(T.r0, (int)(i * 8), 0, 0));
+}
+__device__ __forceinline__ uint64_t tw1(const SfTwB& T, uint32_t i) {
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(T.r1, (int)(i * 8), 0, 0));
+}
 
 // Monomial factors from two 64-entry LDS tables instead of gathers from the 2N-entry table in
 // memory (those missed the cache and stalled every round, profiles/r02z): T[j] = psi^(64 j),
@@ -715,19 +730,21 @@ __device__ __forceinline__ uint64_t sf_mono_mul(uint64_t A, uint32_t e, const ui
     return sf_mul(sf_mul(A, th[0], th[1], K.c), tl[0], tl[1], K.c) + (K.Q9 - A);
 }
 
-__device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const SfTw& T, uint32_t i, const SfC& K) {
-    const uint64_t v = sf_mul(y, T.w0[i], T.w1[i], K.c);
+template <class TW>
+__device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const TW& T, uint32_t i, const SfC& K) {
+    const uint64_t v = sf_mul(y, tw0(T, i), tw1(T, i), K.c);
     y = x + (K.Q2 - v);
     x = x + v;
 }
-template <bool FOLD = false>
-__device__ __forceinline__ void sf_gs(uint64_t& x, uint64_t& y, const SfTw& T, uint32_t i, const SfC& K) {
+template <bool FOLD = false, class TW>
+__device__ __forceinline__ void sf_gs(uint64_t& x, uint64_t& y, const TW& T, uint32_t i, const SfC& K) {
     const uint64_t d = x + (K.Q9 - y), s = x + y;
     x = FOLD ? sf_fold(s, K.c) : s;
-    y = sf_mul(d, T.w0[i], T.w1[i], K.c);
+    y = sf_mul(d, tw0(T, i), tw1(T, i), K.c);
 }
 
-__device__ __forceinline__ void sf_fwd_core(uint64_t (&v)[8], uint32_t m0, uint32_t g, const SfTw& T, const SfC& K) {
+template <class TW>
+__device__ __forceinline__ void sf_fwd_core(uint64_t (&v)[8], uint32_t m0, uint32_t g, const TW& T, const SfC& K) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) sf_ct(v[k], v[k + 4], T, m0 + g, K);
     sf_ct(v[0], v[2], T, 2 * m0 + 2 * g, K), sf_ct(v[1], v[3], T, 2 * m0 + 2 * g, K);
@@ -736,8 +753,8 @@ __device__ __forceinline__ void sf_fwd_core(uint64_t (&v)[8], uint32_t m0, uint3
     for (int j = 0; j < 4; ++j) sf_ct(v[2 * j], v[2 * j + 1], T, 4 * m0 + 4 * g + j, K);
 }
 // FOLD: fold the last stage's sums (inverse passes C and B; bounds_sf.py INV_FOLD_PASS)
-template <bool FOLD>
-__device__ __forceinline__ void sf_inv_core(uint64_t (&v)[8], uint32_t m, uint32_t g, const SfTw& T, const SfC& K) {
+template <bool FOLD, class TW>
+__device__ __forceinline__ void sf_inv_core(uint64_t (&v)[8], uint32_t m, uint32_t g, const TW& T, const SfC& K) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) sf_gs(v[2 * j], v[2 * j + 1], T, m + 4 * g + j, K);
     sf_gs(v[0], v[2], T, (m >> 1) + 2 * g, K), sf_gs(v[1], v[3], T, (m >> 1) + 2 * g, K);
@@ -1017,18 +1034,28 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
 
 // inverse: units of slots 4u .. 4u+3 from registers (second stage's sums folded), C and B
 // wave-local (last stage's sums folded), barrier, pass A into v (polynomial t >> 8, < 8.2 Q)
-__device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], uint64_t (&v)[8], const SfTw& T,
-                                            const SfC& K) {
+// the units of polynomial q (this lane's own slots of the buffer)
+template <class TW>
+__device__ __forceinline__ void sf2_inv_unit(uint64_t* buf, int q, const uint64_t (&sq)[4], const TW& T,
+                                             const SfC& K) {
     constexpr uint32_t N = G3_N;
     const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
     const uint32_t u = (w << 6) | l, u0 = g3_swz(4 * u);
+    uint64_t* pq = buf + q * N;
+    uint64_t v0 = sq[0], v1 = sq[1], v2 = sq[2], v3 = sq[3];
+    sf_gs(v0, v1, T, N / 2 + 2 * u, K), sf_gs(v2, v3, T, N / 2 + 2 * u + 1, K);
+    sf_gs<true>(v0, v2, T, N / 4 + u, K), sf_gs<true>(v1, v3, T, N / 4 + u, K);
+    pq[u0] = v0, pq[u0 ^ 1] = v1, pq[u0 ^ 2] = v2, pq[u0 ^ 3] = v3;
+}
+// UNITS = false: the caller has already run both polynomials' units (sf2_inv_unit)
+template <bool UNITS = true, class TW>
+__device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], uint64_t (&v)[8], const TW& T,
+                                            const SfC& K) {
+    constexpr uint32_t N = G3_N;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    if constexpr (UNITS) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        uint64_t* pq = buf + q * N;
-        uint64_t v0 = s[q][0], v1 = s[q][1], v2 = s[q][2], v3 = s[q][3];
-        sf_gs(v0, v1, T, N / 2 + 2 * u, K), sf_gs(v2, v3, T, N / 2 + 2 * u + 1, K);
-        sf_gs<true>(v0, v2, T, N / 4 + u, K), sf_gs<true>(v1, v3, T, N / 4 + u, K);
-        pq[u0] = v0, pq[u0 ^ 1] = v1, pq[u0 ^ 2] = v2, pq[u0 ^ 3] = v3;
+        for (int q = 0; q < 2; ++q) sf2_inv_unit(buf, q, s[q], T, K);
     }
     wl_sync();
     uint32_t tw = (w << 5) | (l & 31);
@@ -1076,15 +1103,14 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
     uint64_t* mt = psi1_l + N;  // monomial tables
     sf_mono_tables(mt, mono, mono1, Q);
-    const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
+    const SfTw TF{psi_l, psi1_l};
+    const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
     const size_t round_words = (size_t)4 * P.dG2 * N;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
-    uint32_t ex[4];  // slot x evaluates at psi^(2 bitrev(x) + 1)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ex[j] = 2 * (__builtin_bitreverse32(u4 + j) >> 21) + 1;
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
 
     uint64_t acc[2][CN];  // canonical [0, Q), pass A's layout
@@ -1097,11 +1123,13 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         }
     __syncthreads();  // forward twiddles in LDS
 
+    const uint64_t amask = amod - 1;  // amod divides 2N (dev_blind_rotate): a power of two
+    const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
+        const uint64_t ar = ap[i] & amask;  // a_i mod amod, rgsw-acc-cggi.cpp:153
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-        const uint64_t* ek = bsk + (size_t)i * round_words + u4;
-        const uint64_t* ek1 = bsk1 + (size_t)i * round_words + u4;
+        const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
         uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
@@ -1130,15 +1158,24 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         // words each, the next group's loaded before this group's arithmetic; A_kj of slots u4 + s
         // (< 2.1 Q per digit); once both keys of column j are summed, its monomial factors
         constexpr int RW = 2 * DIG, NG = 4 * RW;
+        // key words through buffer resources: uniform round + row offset, 32-bit lane offset
         auto kload = [&](int g, uint64_t (&kw)[8]) {
             const uint32_t j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
-            const size_t o = ((size_t)(kk * P.dG2 + r) * 2 + j) * N;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) kw[s] = ek[o + s], kw[4 + s] = ek1[o + s];
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
+            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
+            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
+            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
+            kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
+            kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
+            kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
+            kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
         };
-        uint32_t ip[4];
+        uint32_t ip[4];  // slot x evaluates at psi^(2 bitrev(x) + 1) (recomputed each round, the
+        uint32_t uo = u4;  // opaque copy keeps the compiler from hoisting four live values)
+        asm volatile("" : "+v"(uo));
 #pragma unroll
-        for (int s = 0; s < 4; ++s) ip[s] = (ex[s] * ai) & (twoN - 1);
+        for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
         uint64_t S[2][4], A[2][4];
         uint64_t kw[2][8];
         kload(0, kw[0]);
@@ -1160,11 +1197,16 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                     const uint32_t in = (twoN - ip[s]) & (twoN - 1);
                     S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip[s], mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
                 }
+                // two digits: the buffer is dead after the last forward units (its outputs are in
+                // registers), so column j's inverse units run now and S[j] dies here (fewer live
+                // registers through column 1's products).  One digit: the buffer still holds that
+                // digit's outputs for column 1.
+                if constexpr (DIG > 1) sf2_inv_unit(buf, j, S[j], TI, K);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
         uint64_t v[8];
-        sf2_ntt_inv(buf, S, v, TI, K);  // outputs < 8.2 Q
+        sf2_ntt_inv<DIG == 1>(buf, S, v, TI, K);  // outputs < 8.2 Q
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -1300,7 +1342,9 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
         const char* e = std::getenv("TFHE_SF2");
         return e && e[0] == '0';
     }();
-    if (!no_sf2 && (P.digits == 1 || P.digits == 2)) {
+    // sf2 addresses the keys with 32-bit byte offsets (buffer resources)
+    const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
+    if (!no_sf2 && fits32 && (P.digits == 1 || P.digits == 2)) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
