@@ -729,7 +729,6 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const uint64_t scale = (uint64_t)twoN / amod;
     const size_t round_words = (size_t)4 * P.dG2 * N;
-    const uint64_t amask = amod - 1;  // amod divides 2N (dev_blind_rotate): a power of two
     // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
 
@@ -763,7 +762,10 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const uint32_t shiftL = P.digits * logG;
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] & amask;  // a_i mod amod, rgsw-acc-cggi.cpp:153
+        // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
+        // consumer of this round's scalar load moved past the forward transform and results came
+        // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
+        const uint64_t ar = ap[i] % amod;
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
         const uint32_t round_off = (i & K.kround_mask) * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS

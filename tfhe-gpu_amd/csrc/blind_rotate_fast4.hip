@@ -135,6 +135,13 @@ __device__ __forceinline__ int32_t sredc(int64_t T, const FastConst& K) {
 }
 __device__ __forceinline__ int32_t smul(int32_t a, int32_t wM, const FastConst& K) { return sredc((int64_t)a * wM, K); }
 __device__ __forceinline__ uint32_t csub32(uint32_t a, uint32_t m) { return min(a, a - m); }
+// s + a b as one v_mad_i64_i32: s passes through an empty asm so the compiler cannot
+// re-associate a row sum's terms into (a b + c d) + s, which costs a separate 64-bit add per pair
+// (24 per wave-round)
+__device__ __forceinline__ int64_t mac64(int32_t a, int32_t b, int64_t s) {
+    asm("" : "+v"(s));  // opaque: the sum is formed in this order
+    return (int64_t)a * b + s;
+}
 
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v4i ld_bsk(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -443,7 +450,8 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         pw[0] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l) * 2 + j) * FN * 4);
         pw[1] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l + 1) * 2 + j) * FN * 4);
     };
-    auto mac = [&](int64_t (&s)[NCT][2][2][4], const int32_t (&X)[P][4], const v4i (&pw)[2], int gi) {
+    // first: the round's first terms (s = 0 until now)
+    auto mac = [&](int64_t (&s)[NCT][2][2][4], const int32_t (&X)[P][4], const v4i (&pw)[2], int gi, bool first) {
         const int k = gi >> 1, j = gi & 1;
         const int32_t w0[4] = {pw[0].x, pw[0].y, pw[0].z, pw[0].w};
         const int32_t w1[4] = {pw[1].x, pw[1].y, pw[1].z, pw[1].w};
@@ -451,8 +459,8 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         for (int q = 0; q < NCT; ++q)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                s[q][k][j][r] = (int64_t)X[2 * q][r] * w0[r] + s[q][k][j][r];
-                s[q][k][j][r] = (int64_t)X[2 * q + 1][r] * w1[r] + s[q][k][j][r];
+                s[q][k][j][r] = first ? (int64_t)X[2 * q][r] * w0[r] : mac64(X[2 * q][r], w0[r], s[q][k][j][r]);
+                s[q][k][j][r] = mac64(X[2 * q + 1][r], w1[r], s[q][k][j][r]);
             }
     };
 
@@ -489,7 +497,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi) {
                 __builtin_amdgcn_sched_barrier(0);
-                mac(s, Cp, pw[gi], gi);
+                mac(s, Cp, pw[gi], gi, true);
                 issue(pw[gi], round_off, 0, gi);
             }
         } else {
@@ -521,7 +529,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 #pragma unroll
             for (int gi = 0; gi < 4; ++gi) {
                 __builtin_amdgcn_sched_barrier(0);
-                mac(s, X, pw[gi], gi);
+                mac(s, X, pw[gi], gi, !FOLD && l == 0);
                 if (FOLD || !last) issue(pw[gi], noff, nl, gi);
             }
         }

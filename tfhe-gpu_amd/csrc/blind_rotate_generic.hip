@@ -1123,11 +1123,13 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         }
     __syncthreads();  // forward twiddles in LDS
 
-    const uint64_t amask = amod - 1;  // amod divides 2N (dev_blind_rotate): a power of two
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] & amask;  // a_i mod amod, rgsw-acc-cggi.cpp:153
+        // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
+        // consumer of this round's scalar load moved past the forward transform and results came
+        // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
+        const uint64_t ar = ap[i] % amod;
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
         uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)

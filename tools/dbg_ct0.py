@@ -1,6 +1,6 @@
 """Debug: repeated EvalAcc parity (new random inputs each time) on STD192 (f64w) and the logQ = 12
 arbFunc context (sf2, one digit); prints the ciphertexts that differ from the oracle.
-Usage: python3 tools/dbg_ct0.py [reps]"""
+Usage: python3 tools/dbg_ct0.py [reps] [STD192 arb12 logq23 STD128Q ...]"""
 import os
 import sys
 
@@ -14,9 +14,12 @@ import pyoracle  # noqa: E402
 from tfhe_amd import capi  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-for name in ("STD192", "arb12"):
+names = sys.argv[2:] or ["STD192", "arb12"]
+for name in names:
     if name == "arb12":
         op, cp = pyoracle.params_from_logq("STD128", True, 12, 0, 0, 1), capi.params_from_logq("STD128", True, 12, 0, 0, 1)
+    elif name == "logq23":  # C5b: sf2 with two digits
+        op, cp = pyoracle.params_from_logq("STD128", False, 23, 0, 0, 1), capi.params_from_logq("STD128", False, 23, 0, 0, 1)
     else:
         op, cp = pyoracle.params_from_set(name), capi.params_from_set(name)
     rs = np.random.default_rng(5)

@@ -1,0 +1,24 @@
+# Re-entry validation of the committed tree (after the N = 2048 register-pressure changes):
+# full GPU suite, smoke, headline bench + rocprofv3 kernel stats of the same command, and the
+# other SURVEY 8(d) configurations through the host-array API.
+set -u
+export TMPDIR=/tmp
+D=gpurun_out/r02at
+mkdir -p $D
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $D/pytest_gpu.log 2>&1 || { tail -30 $D/pytest_gpu.log; exit 1; }
+tail -1 $D/pytest_gpu.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { cat $D/smoke.log; exit 1; }
+tail -1 $D/smoke.log
+timeout -k 10 400 python3 bench.py > $D/bench.log 2>&1 || { cat $D/bench.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python3 bench.py > $D/prof.log 2>&1 || { tail -20 $D/prof.log; exit 1; }
+timeout -k 10 600 python3 tools/bench_configs.py C2host C3 C4 C5a C5b --reps 2 > $D/configs.log 2>&1 || { cat $D/configs.log; exit 1; }
+grep -h '^{' $D/bench.log | cut -c1-400
+grep -h '^{' $D/configs.log | python3 -c "
+import sys,json
+for l in sys.stdin: d=json.loads(l); print(d['config'], d['kernel'], d['bootstraps_per_s'])"
+python3 - <<'PY'
+import csv, glob
+for f in glob.glob("gpurun_out/r02at/prof/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print(r["Name"][:70], r["Calls"], f'{float(r["AverageNs"])/1e6:.3f} ms', r["Percentage"])
+PY
