@@ -514,6 +514,29 @@ def test_wrap_correction_late_round(capi, oracle, pset):
     ctx.GPUClean()
     orc.close()
 
+@pytest.mark.parametrize("pset", ["STD128Q_OPT", "STD192"])
+def test_repeated_calls_stable(capi, oracle, pset):
+    """The same EvalAcc six times on one context, every result equal to the oracle: the
+    N = 2048 kernels once went wrong in some calls only (a uniform value scalar-loaded at the
+    top of a round and consumed after the transforms, profiles/r02ay/summary.txt); one call per
+    test did not show it reliably."""
+    op = oracle.params_from_set(pset)
+    cp = capi.params_from_set(pset)
+    rs = np.random.default_rng(12)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    B = 3
+    a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    acc[:2, :, 10:20] = ((op.Q >> 1) - 1 - rs.integers(0, 1 << 23, (2, 2, 10))).astype(np.uint64)
+    want = orc.eval_acc(a, op.q, acc)
+    bad = [r for r in range(6) if not np.array_equal(ctx.EvalAcc(a, op.q, acc), want)]
+    assert bad == [], f"calls {bad} differ from the oracle"
+    ctx.GPUClean()
+    orc.close()
+
+
 def _prime_1_mod(m, bits):
     """Largest prime p < 2^bits with p = 1 (mod m) (deterministic Miller-Rabin for 64-bit)."""
     def is_prime(n):

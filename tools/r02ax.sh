@@ -1,5 +1,4 @@
 # Bisect of the f64w nondeterminism (r02av, r02aw): D = a mod amod by %, E = no key-round mask, F = both
-# exponents without the opaque per-round copy; the rest of the 51071bb changes kept in each.
 set -u
 export TMPDIR=/tmp
 D=gpurun_out/r02ax
