@@ -1,0 +1,21 @@
+#!/bin/bash
+# f64w under other LLVM scheduling strategies (altlib/libtfhe_hip_f64_<strategy>.so: only
+# blind_rotate_f64.hip rebuilt with -mllvm -amdgpu-sched-strategy=...): parity, then STD192 /
+# STD128Q device-resident bench, alternating with the default build on one box.
+set -u
+export TMPDIR=/tmp
+D=gpurun_out/r02be
+mkdir -p $D
+for st in max-ilp iterative-ilp; do
+  TFHE_LIB=$PWD/altlib/libtfhe_hip_f64_$st.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "n2048 or wrap" > $D/pytest_$st.log 2>&1 || { echo "$st parity FAILED"; tail -20 $D/pytest_$st.log; exit 1; }
+  echo "$st $(tail -1 $D/pytest_$st.log)"
+done
+for rep in 1 2; do
+  for st in default max-ilp iterative-ilp; do
+    L=""; [ $st != default ] && L="TFHE_LIB=$PWD/altlib/libtfhe_hip_f64_$st.so"
+    for ps in STD192 STD128Q; do
+      env $L timeout -k 10 300 python3 bench.py --params $ps --no-cpu-baseline --steps 3 --warmup 1 > $D/${ps}_${st}_$rep.log 2>&1 || { tail -5 $D/${ps}_${st}_$rep.log; exit 1; }
+      echo "$ps $st rep=$rep $(tail -1 $D/${ps}_${st}_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["kernel_ms"])')"
+    done
+  done
+done
