@@ -606,6 +606,7 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     }
 }
 
+#ifndef TFHE_FAST4_KERNEL_ONLY  // blind_rotate_fast4_d6.hip includes the kernel template only
 // generic psi / ipsi / mono tables (plain u32) -> the table block above (centred Montgomery)
 __global__ void k_pack_tables4(uint32_t Q, const uint32_t* __restrict__ psi, const uint32_t* __restrict__ ipsi,
                                const uint32_t* __restrict__ mono, int32_t* __restrict__ out) {
@@ -641,7 +642,9 @@ __global__ void k_pack_tables4(uint32_t Q, const uint32_t* __restrict__ psi, con
     }
 }
 
+#endif  // TFHE_FAST4_KERNEL_ONLY
 }  // namespace f4
+#ifndef TFHE_FAST4_KERNEL_ONLY
 
 size_t fast4_table_words() { return f4::T4_WORDS; }
 
@@ -658,6 +661,11 @@ bool fast4_shape_supported(const Fast4Shape& sh) {
            (sh.dig == 3 && sh.logg == 9 && sh.thr == 0 && !sh.fold);    // STD128_AP (top digit wraps)
 }
 
+// blind_rotate_fast4_d6.hip: the logQ = 11 folded shape (6 digits of 5 bits), built with the default
+// LLVM scheduler (29 % slower under iterative-ilp, profiles/r02bh)
+hipError_t launch_blind_rotate_fast4_d6(const f4::FastConst& K, uint32_t n, uint32_t loga, const int32_t* tabs4,
+                                        const int32_t* bsk, const uint64_t* a, uint64_t* acc, size_t B, hipStream_t s);
+
 hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
                                      size_t B, hipStream_t s) {
@@ -669,10 +677,8 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
                            n, loga, tabs4, bsk, a, acc, (uint32_t)B);
     };
     // other digit shapes: the default build (variant 60's template arguments) at that shape
-    if (sh.dig == 6 && sh.logg == 5 && sh.thr == 0 && sh.fold) {
-        launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 6, 5, 0, true>, 1, 1);
-        return hipGetLastError();
-    }
+    if (sh.dig == 6 && sh.logg == 5 && sh.thr == 0 && sh.fold)  // own translation unit (Makefile)
+        return launch_blind_rotate_fast4_d6(Kc, n, loga, tabs4, bsk, a, acc, B, s);
     if (sh.dig == 5 && sh.logg == 5 && sh.thr == 1 && !sh.fold) {
         launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 5, 5, 1, false>, 1, 1);
         return hipGetLastError();
@@ -704,4 +710,5 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
     return hipGetLastError();
 }
 
+#endif  // TFHE_FAST4_KERNEL_ONLY
 }  // namespace tfhe
