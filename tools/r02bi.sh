@@ -1,7 +1,8 @@
 #!/bin/bash
 # iterative-ilp for the special-form / generic kernels (altlib/libtfhe_hip_gen_ilp.so: C3, C5b)
 # and for the tiled key switch (altlib/libtfhe_hip_ks_ilp.so: headline step), against the tree
-# build, alternating on one box; parity first.
+# build, alternating on one box; parity first.  (Not yet run: rebuild the two altlib/ files from
+# the tree objects with the one translation unit recompiled under -mllvm -amdgpu-sched-strategy=iterative-ilp.)
 set -u
 export TMPDIR=/tmp
 D=gpurun_out/r02bi
