@@ -13,16 +13,27 @@ RCCL/xGMI (torch.distributed, backend "nccl" = RCCL), then every rank bootstraps
 its own 8192-ciphertext shard with no data-path collective (weak scaling).
 
 Extra JSON fields:
-  roofline      the blind-rotation kernel, timed alone with HIP events on its
-                stream; algorithmic bytes per SURVEY.md 8(d) (B_alg = BSK key
-                stream per bootstrap + KS gather + LWE I/O, no cross-ciphertext
-                reuse); traffic from rocprofv3 PMC if --pmc-json is given.
-  valu          the real bound (integer VALU issue): modular
-                multiplies/s, and the VALU issue fraction = PMC-measured VALU
-                instructions x 4 cycles (wave64 integer multiply/add issue,
-                profiles/r01_valu_rates.txt) / (SIMDs x clock x kernel time).
-  cpu_baseline  the C oracle (oracle/tfhe_oracle.c, OpenMP) on a bounded sample
-                of the same workload on this host's cores (rank 0, N=1 only).
+  roofline      the blind-rotation kernel (the dominant one), timed alone with HIP
+                events on its stream.  Its bound is integer VALU issue:
+                bound "valu-int", achieved = the algorithmic modular multiplies of
+                SURVEY 8(d) (n[(dG2+2)(N/2)log2 N + 4 dG2 N + 4N] per bootstrap) per
+                second, peak = the microbenchmarked signed-Montgomery modmul rate of
+                gfx950 (tools/microbench/valu_rates.hip, --valu-peak-json), frac = their
+                ratio.  traffic = PMC HBM bytes per launch (rocprofv3 FETCH_SIZE x2 +
+                WRITE_SIZE, MI355X_MICROARCH.md corrections; --pmc-json), hbm_frac =
+                traffic / kernel time / 8 TB/s, effective_keystream_tbs = SURVEY B_alg
+                (BSK + KS gather + LWE I/O per bootstrap, no cross-ciphertext reuse) x
+                batch / kernel time.
+  valu          PMC view of the same kernel: VALU instructions, issue and busy
+                fractions, the clock the part held under it.
+  host_array    the same gates through the host-array entry point (tfhe_eval_bin_gate:
+                PCIe copies, pinned staging and the host thread included), same inputs.
+  cpu_baseline  the REFERENCE's own OpenFHE CPU path (oracle/_ref/ref_kat: the
+                unchanged vector EvalBinGate with the reference's CPU accumulator and
+                key switch behind the GPU symbols, OpenMP over ciphertexts) on a bounded
+                sample of the same workload with the same keys on this host's cores
+                (rank 0, N = 1 only), which also checks the benchmarked GPU outputs bit
+                for bit; the C restatement (oracle/) when ref_kat is not built.
 """
 from __future__ import annotations
 
@@ -59,14 +70,37 @@ def parse():
                     help="torch.distributed backend ('nccl' = RCCL; 'gloo' only to rehearse N ranks on fewer GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_blind_rotate.json"))
+    ap.add_argument("--valu-peak-json", default=os.path.join(ROOT, "profiles", "r03_valu_peak.json"))
+    ap.add_argument("--no-host-array", action="store_true")
     return ap.parse_args()
 
 
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix_stream(seed, start, count, mod, out):
+    """out[k] = splitmix64 value number start+k+1 of seed, mod `mod` (SURVEY.md Appendix B
+    generator; the stream or_kat_keys and the reference driver draw from), vectorised."""
+    M1, M2 = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+    step = 1 << 24
+    with np.errstate(over="ignore"):
+        for o in range(0, count, step):
+            k = np.arange(start + o + 1, start + min(count, o + step) + 1, dtype=np.uint64)
+            z = np.uint64(seed) + k * GAMMA
+            z = (z ^ (z >> np.uint64(30))) * M1
+            z = (z ^ (z >> np.uint64(27))) * M2
+            z ^= z >> np.uint64(31)
+            out[o:o + len(k)] = z % np.uint64(mod)
+    return out
+
+
 def synthetic_keys(p, seed=1):
-    """Uniform random BSK/KSK of the right shapes (throughput does not depend on key validity)."""
-    rs = np.random.default_rng(seed)
-    bsk = rs.integers(0, p.Q, p.bsk_words(), dtype=np.uint64)
-    ksk = rs.integers(0, p.qKS, p.ksk_words(), dtype=np.uint64)
+    """The Appendix B synthetic keys ("synth:<seed>": BSK coefficients then KSK words from one
+    splitmix64 stream), so the reference CPU run (cpu_baseline) uses exactly the same keys;
+    throughput does not depend on key validity."""
+    nb, nk = p.bsk_words(), p.ksk_words()
+    bsk = splitmix_stream(seed, 0, nb, p.Q, np.empty(nb, dtype=np.uint64))
+    ksk = splitmix_stream(seed, nb, nk, p.qKS, np.empty(nk, dtype=np.uint64))
     return bsk, ksk
 
 
@@ -86,12 +120,70 @@ def b_alg_per_bootstrap(p):
     return bsk + ks + io, bsk
 
 
+def host_threads():
+    """Threads for the CPU baseline: every core this process may run on, unless the pool caps
+    OpenMP (OMP_NUM_THREADS is set to the box's CPU share on the GPU pool)."""
+    visible = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(visible, cap) if cap else visible), visible
+
+
+REF_KAT = os.path.join(ROOT, "oracle", "_ref", "ref_kat")
+
+
+def cpu_baseline_reference(p, seconds, gpu_sample):
+    """The reference's own OpenFHE code (oracle/_ref/ref_kat, vector EvalBinGate, CPU functions
+    behind the seven GPU symbols, OpenMP over ciphertexts) on K pairs; the first ones are the
+    GPU's benchmarked inputs, whose outputs are compared bit for bit."""
+    import subprocess
+    import tempfile
+
+    threads, visible = host_threads()
+    g1, g2, gout = gpu_sample
+    per_gate_s = 0.3  # single-thread OpenFHE STD128 gate, measured here (SURVEY 6: 0.144-0.27 s)
+    K = max(len(g1), int(seconds * threads / per_gate_s))
+    rs = np.random.default_rng(5)
+    c1 = np.concatenate([g1, rs.integers(0, p.q, (K - len(g1), p.n + 1), dtype=np.uint64)])
+    c2 = np.concatenate([g2, rs.integers(0, p.q, (K - len(g2), p.n + 1), dtype=np.uint64)])
+
+    def run(a1, a2, nthreads):
+        with tempfile.TemporaryDirectory() as tmp:
+            f1, f2, fo = (os.path.join(tmp, x) for x in ("c1", "c2", "out"))
+            a1.tofile(f1)
+            a2.tofile(f2)
+            env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
+            r = subprocess.run([REF_KAT, "ctx=set:STD128", "keys=synth:1", "op=NAND", "api=vector", f"in={f1}",
+                                f"in2={f2}", f"out={fo}"], capture_output=True, text=True, env=env, timeout=900)
+            if r.returncode:
+                raise RuntimeError(r.stderr[-2000:])
+            js = json.loads(r.stdout.strip().splitlines()[-1])
+            return js, np.fromfile(fo, dtype=np.uint64).reshape(len(a1), p.n + 1)
+
+    js, out = run(c1, c2, threads)
+    B1 = max(2, int(seconds / 4 / per_gate_s))
+    js1, _ = run(c1[:B1], c2[:B1], 1)
+    parity = {"ciphertexts": int(len(gout)), "bit_exact": bool(np.array_equal(out[:len(gout)], gout)),
+              "vs": "the reference's OpenFHE CPU path (oracle/_ref/ref_kat), same keys and inputs"}
+    return {"value": round(K / js["best_s"], 3), "unit": "bootstraps/s", "cores": threads, "kind": "reference",
+            "host_cores_visible": visible, "single_thread_value": round(B1 / js1["best_s"], 3),
+            "sample": f"STD128 EvalBinGate(NAND), vector API of the reference's OpenFHE (compiled from its sources, "
+                      f"oracle/Makefile.ref) with its CPU accumulator / key switch behind the GPU symbols, OpenMP "
+                      f"over ciphertexts, {threads} threads: {K} pairs in {js['best_s']:.1f} s (key load "
+                      f"{js['key_load_s']:.1f} s not counted); single thread: {B1} pairs in {js1['best_s']:.1f} s",
+            "gpu_parity": parity}
+
+
 def cpu_baseline(p, bsk, ksk, seconds, gpu_sample=None):
+    if os.path.exists(REF_KAT) and gpu_sample is not None:
+        try:
+            return cpu_baseline_reference(p, seconds, gpu_sample)
+        except Exception as e:  # fall back to the restatement
+            print(f"[bench] reference CPU baseline failed ({e}); using the C restatement", file=sys.stderr)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
     pyoracle.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, visible = host_threads()
     orc = pyoracle.Oracle(p_oracle(pyoracle, p), bsk, ksk, threads=threads)
     rs = np.random.default_rng(5)
     # calibrate on one gate per thread, then size the sample to ~`seconds`
@@ -124,7 +216,7 @@ def cpu_baseline(p, bsk, ksk, seconds, gpu_sample=None):
                   "vs": "oracle/tfhe_oracle.c on the same synthetic keys and inputs"}
     orc.close()
     return {"value": round(B / dt, 3), "unit": "bootstraps/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(B1 / dt1, 3),
+            "host_cores_visible": visible, "single_thread_value": round(B1 / dt1, 3),
             "sample": f"STD128 EvalBinGate(NAND) on {B} random ciphertext pairs, same synthetic keys; "
                       f"oracle/tfhe_oracle.c (exact u128 CPU restatement, OpenMP one ciphertext per thread); "
                       f"{dt:.1f} s; single thread: {B1} pairs in {dt1:.1f} s",
@@ -241,7 +333,6 @@ def main():
     torch.cuda.synchronize(dev)
     br_ms = e0.elapsed_time(e1) / args.kernel_reps
     balg, bsk_bytes = b_alg_per_bootstrap(p)
-    achieved = balg * B / (br_ms * 1e-3) / 1e9
     traffic, valu_insts, pmc = None, None, {}
     if os.path.exists(args.pmc_json):
         try:
@@ -254,13 +345,24 @@ def main():
         except Exception:
             traffic, valu_insts, pmc = None, None, {}
     mm = modmuls_per_bootstrap(p)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 3), "traffic": traffic,
+    achieved_mm = mm * B / (br_ms * 1e-3)
+    peak_mm, peak_src = None, None
+    if os.path.exists(args.valu_peak_json):
+        vp = json.load(open(args.valu_peak_json))
+        peak_mm, peak_src = vp["modmul_per_s"], vp
+    roofline = {"bound": "valu-int", "achieved": round(achieved_mm / 1e12, 3),
+                "peak": None if peak_mm is None else round(peak_mm / 1e12, 3), "unit": "Tmodmul/s",
+                "frac": None if peak_mm is None else round(achieved_mm / peak_mm, 3), "traffic": traffic,
                 "kernel": "blind_rotate (tfhe_eval_acc_device)", "kernel_ms": round(br_ms, 3),
-                "units_per_launch": B, "alg_bytes_per_unit": balg,
-                "note": "B_alg per SURVEY.md 8(d): key-stream bytes with no cross-ciphertext reuse; frac > 1 means "
-                        "the 64 MiB BSK is re-served from L2/MALL across the batch. The kernel is VALU-bound: "
-                        "see 'valu'."}
+                "units_per_launch": B, "alg_modmul_per_unit": mm,
+                "hbm_frac": None if traffic is None else round(traffic / (br_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4),
+                "effective_keystream_tbs": round(balg * B / (br_ms * 1e-3) / 1e12, 2), "alg_bytes_per_unit": balg,
+                "note": "achieved = SURVEY 8(d) algorithmic modmuls per bootstrap x batch / event-timed kernel; peak = "
+                        "signed-Montgomery modmul rate of the VALU microbenchmark "
+                        + ("(" + os.path.relpath(args.valu_peak_json, ROOT) + ", " + str(peak_src.get("clock", "")) + ")"
+                           if peak_src else "(not found)")
+                        + "; hbm_frac = PMC HBM bytes / kernel time / 8 TB/s; effective_keystream_tbs = B_alg "
+                          "(no cross-ciphertext reuse) x batch / kernel time, served from L2/MALL"}
     simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
     valu = {"bound": "valu-int", "modmul_per_bootstrap": mm,
             "achieved_modmul_per_s": round(mm * B / (br_ms * 1e-3), 1),
@@ -279,6 +381,21 @@ def main():
         valu["note"] += ("; busy_frac = SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8); held_clock_ghz = "
                          "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass, MI355X_MICROARCH.md 'DVFS give-back')")
 
+    # ---- the same gates through the host-array entry point (PCIe + host staging included) ----
+    host_array = None
+    if rank == 0 and world == 1 and not args.no_host_array:
+        h1 = ct1.cpu().numpy().astype(np.uint64)
+        h2 = ct2.cpu().numpy().astype(np.uint64)
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            hout = ctx.EvalBinGate("NAND", h1, h2)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        host_array = {"value": round(B / best, 1), "unit": "bootstraps/s", "ms": round(best * 1e3, 3),
+                      "equal_to_device_resident": bool(np.array_equal(hout, out.cpu().numpy().astype(np.uint64))),
+                      "note": "tfhe_eval_bin_gate on host arrays: H2D + kernels + D2H through pinned staging, best of 2"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if bsk is None:
@@ -287,7 +404,7 @@ def main():
         sample = tuple(x[:K].cpu().numpy().astype(np.uint64) for x in (ct1, ct2, out))
         cpu = cpu_baseline(p, bsk, ksk, args.cpu_seconds, sample)
         if cpu["gpu_parity"] and not cpu["gpu_parity"]["bit_exact"]:
-            print("[bench] ERROR: GPU outputs differ from the oracle", file=sys.stderr)
+            print("[bench] ERROR: GPU outputs differ from the CPU reference", file=sys.stderr)
 
     if rank == 0:
         line = {
@@ -300,7 +417,7 @@ def main():
             "config": {"workload": f"{args.params} GINX EvalBinGate(NAND), inputs resident in HBM",
                        "global_batch": B * world, "batch_per_gpu": B, "n": p.n, "N": p.N, "Q": p.Q,
                        "dG2": p.dG2, "parallelism": f"shard{world}"},
-            "roofline": roofline, "valu": valu, "cpu_baseline": cpu,
+            "roofline": roofline, "valu": valu, "host_array": host_array, "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2), "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2),
             "key_image_bytes": int(ctx.info().key_image_bytes),
         }

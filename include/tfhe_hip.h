@@ -117,7 +117,9 @@ tfhe_status tfhe_params_from_logq(int paramset, int arb_func, uint32_t logQ, int
                                   uint32_t num_digits_to_throw, tfhe_params* out);
 tfhe_status tfhe_params_finish(tfhe_params* p);
 
-/* ---- reference boundary ---- */
+/* ---- reference boundary ----
+ * num_gpus as GPUSetup(numGPUs) (bootstrapping.cu:736-739): <= 0 or more than visible = every visible
+ * device; batches are cut into one contiguous shard per device. */
 tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
                        int num_gpus);
 /* Same, with the BSK exactly as OpenFHE holds it after KeyGen / BTKeyLoad: EVALUATION
@@ -133,6 +135,13 @@ tfhe_status tfhe_clean(tfhe_ctx* ctx);
 /* a[B][n] mod a_mod; acc[B][2][N] coefficient in/out; acc0 returned transposed
  * (the callers rely on it: binfhe-base-scheme.cpp:665-671, 1203-1204). */
 tfhe_status tfhe_eval_acc(tfhe_ctx* ctx, size_t B, const uint64_t* a, uint64_t a_mod, uint64_t* acc);
+/* EvalAcc_CUDA for the accumulators the vector callers build (BootstrapGateCore / BootstrapFuncCore,
+ * binfhe-base-scheme.cpp:1110-1138, 1163-1185): acc0 = 0 and acc1 zero except at multiples of
+ * N / tv_len, whose values are tv[B][tv_len] (tv_len = a_mod / 2 there).  Same output as tfhe_eval_acc
+ * on the expanded accumulators, with tv_len instead of 2N words per ciphertext sent to the device
+ * (the drop-in shim detects the shape, tfhe-gpu_amd/shim/bootstrapping_hip.cpp). */
+tfhe_status tfhe_eval_acc_tv(tfhe_ctx* ctx, size_t B, const uint64_t* a, uint64_t a_mod, const uint64_t* tv,
+                             uint32_t tv_len, uint64_t* acc);
 /* ct_ext[B][N+1] mod Q -> out[B][n+1] mod fmod: ModSwitch(qKS), KeySwitch, ModSwitch(fmod) */
 tfhe_status tfhe_mkm_switch(tfhe_ctx* ctx, size_t B, const uint64_t* ct_ext, uint64_t fmod, uint64_t* out);
 /* out[c] = sum_k matrix[k][c] * ct[k] mod modulus, c < cols: ct[K][n+1], matrix[K][cols], out[cols][n+1] */

@@ -69,6 +69,9 @@ def lib():
         L.or_set_threads.argtypes = [C.c_int]
         L.or_splitmix64.argtypes = [C.POINTER(Rng)]
         L.or_splitmix64.restype = C.c_uint64
+        L.or_splitmix_fill.argtypes = [C.POINTER(Rng), C.c_size_t, C.c_uint64, u64p]
+        L.or_fnv1a64.argtypes = [u64p, C.c_size_t]
+        L.or_fnv1a64.restype = C.c_uint64
         L.or_kat_keys.argtypes = [P, C.POINTER(Rng), u64p, u64p]
         L.or_root_of_unity.argtypes = [C.c_uint64, C.c_uint32]
         L.or_root_of_unity.restype = C.c_uint64
@@ -144,8 +147,9 @@ def openfhe_ntt(Q: int, N: int, polys, inverse: bool = False) -> np.ndarray:
 
 
 def splitmix(rng: Rng, count: int, mod: int) -> np.ndarray:
-    L = lib()
-    return np.array([L.or_splitmix64(C.byref(rng)) % mod for _ in range(count)], dtype=np.uint64)
+    out = np.empty(count, dtype=np.uint64)
+    lib().or_splitmix_fill(C.byref(rng), count, mod, out)
+    return out
 
 
 def encrypt(p: Params, rng: Rng, sk, m: int, ptxt_mod: int, mod: int) -> np.ndarray:
@@ -159,6 +163,8 @@ def decrypt(p: Params, sk, ct, ptxt_mod: int, mod: int) -> int:
 
 
 def fnv1a64(values) -> int:
+    if isinstance(values, np.ndarray) and values.dtype == np.uint64:
+        return int(lib().or_fnv1a64(np.ascontiguousarray(values).ravel(), values.size))
     h = 0xCBF29CE484222325
     for v in values:
         v = int(v)

@@ -514,6 +514,20 @@ uint64_t or_splitmix64(or_rng* r) {
     return z ^ (z >> 31);
 }
 
+void or_splitmix_fill(or_rng* r, size_t count, uint64_t mod, uint64_t* out) {
+    for (size_t i = 0; i < count; ++i) out[i] = or_splitmix64(r) % mod;
+}
+
+uint64_t or_fnv1a64(const uint64_t* w, size_t count) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < count; ++i)
+        for (int b = 0; b < 8; ++b) {
+            h ^= (w[i] >> (8 * b)) & 0xff;
+            h *= 0x100000001b3ull;
+        }
+    return h;
+}
+
 void or_kat_keys(const or_params* p, or_rng* r, uint64_t* bsk, uint64_t* ksk) {
     const size_t nb = (size_t)p->n * 2 * p->dG2 * 2 * p->N;
     for (size_t i = 0; i < nb; ++i) bsk[i] = or_splitmix64(r) % p->Q;

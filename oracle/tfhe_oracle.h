@@ -90,6 +90,10 @@ void or_set_threads(int nthreads);
 /* KAT synthetic keys (SURVEY.md Appendix B recipe; splitmix64 stream) */
 typedef struct { uint64_t s; } or_rng;
 uint64_t or_splitmix64(or_rng* r);
+/* out[i] = splitmix64() % mod, i < count (the same stream as count calls of or_splitmix64) */
+void or_splitmix_fill(or_rng* r, size_t count, uint64_t mod, uint64_t* out);
+/* FNV-1a-64 over the little-endian bytes of w[0..count-1] (the golden-vector digest) */
+uint64_t or_fnv1a64(const uint64_t* w, size_t count);
 void or_kat_keys(const or_params* p, or_rng* r, uint64_t* bsk_coeff, uint64_t* ksk);
 
 /* Valid keys (for decrypt-correctness): ternary LWE key sk[n] (mod qKS, as the

@@ -21,6 +21,9 @@
 #include "device_math.hpp"
 #include "kernels.hpp"
 
+#ifndef TFHE_AI_PROBE  // a_i load form in f64w (tools/ai_probe.sh); 0 = the tree's
+#define TFHE_AI_PROBE 0
+#endif
 namespace tfhe {
 namespace {
 
@@ -711,6 +714,9 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     double* buf = lds_d + 2 * N;  // [2][N]
     double* mt = lds_d + 4 * N;   // monomial tables (k_blind_rotate_f64)
     __shared__ int wflag[2];
+#if TFHE_AI_PROBE == 7
+    __shared__ int wvote[2][8];
+#endif
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
@@ -761,12 +767,44 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
     const uint32_t shiftL = P.digits * logG;
 
+#if TFHE_AI_PROBE == 4
+    uint32_t* exps = reinterpret_cast<uint32_t*>(mt + 128);  // [n] rotation exponents, staged once
+    for (uint32_t k = t; k < P.n; k += TH) {
+        const uint64_t ar = ap[k] & (amod - 1);
+        exps[k] = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+    }
+    __syncthreads();
+#endif
     for (uint32_t i = 0; i < P.n; ++i) {
+#if TFHE_AI_PROBE == 0
         // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
         // consumer of this round's scalar load moved past the forward transform and results came
         // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
         const uint64_t ar = ap[i] % amod;
+#elif TFHE_AI_PROBE == 1  // 51071bb: mask, scalar load consumed after the forward transform
+        const uint64_t ar = ap[i] & (amod - 1);
+#elif TFHE_AI_PROBE == 2  // mask, scalar load consumed at once
+        uint64_t araw = ap[i];
+        asm volatile("" : "+s"(araw));
+        const uint64_t ar = araw & (amod - 1);
+#elif TFHE_AI_PROBE == 5  // mask, scalar load waited for at once (no data dependence)
+        const uint64_t araw = ap[i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t ar = araw & (amod - 1);
+#elif TFHE_AI_PROBE == 7  // as 1, the WRAP vote by an unmasked LDS atomic instead of a masked store
+        const uint64_t ar = ap[i] & (amod - 1);
+#elif TFHE_AI_PROBE == 3  // mask, vector load (not through the scalar cache), then readfirstlane
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        const uint64_t av = ap[i + z];
+        const uint64_t ar = (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(av >> 32)) << 32) |
+                             __builtin_amdgcn_readfirstlane((uint32_t)av)) & (amod - 1);
+#endif
+#if TFHE_AI_PROBE == 4
+        const uint32_t ai = exps[i];
+#else
         const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+#endif
         const uint32_t round_off = (i & K.kround_mask) * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
@@ -793,8 +831,13 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             if (WRAP && !CORR && l == 0) {
                 // round i - 1 read wflag[(i + 1) & 1] before its inverse barrier; round i + 1
                 // writes it after this round's barriers; the forward barrier publishes the vote
+#if TFHE_AI_PROBE == 7
+                // per-wave vote slots, written by every lane (no exec-masked store, no reset)
+                wvote[i & 1][t >> 6] = __builtin_amdgcn_ballot_w64(wv) != 0;
+#else
                 if (t == 0) wflag[(i + 1) & 1] = 0;
                 if (wv) wflag[i & 1] = 1;
+#endif
             }
             if (sync) __syncthreads();  // other waves may still read their blocks
             if (!CORR && l + 1 == LD) f64w_ntt_fwd<RED, true>(buf, v, d, psi, K);
@@ -810,7 +853,13 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 #pragma unroll
             for (int s = 0; s < 4; ++s) Cx[p][s] = Cn[p][s];
         if constexpr (WRAP) {
-            if (wflag[i & 1]) {
+#if TFHE_AI_PROBE == 7
+            const int* wvs = wvote[i & 1];
+            const bool wset = (wvs[0] | wvs[1] | wvs[2] | wvs[3] | wvs[4] | wvs[5] | wvs[6] | wvs[7]) != 0;
+#else
+            const bool wset = wflag[i & 1] != 0;
+#endif
+            if (wset) {
                 // the correction's transform overwrites the buffer that holds the last digit's
                 // outputs: transform the last digit again afterwards (rare rounds only)
                 double dc[2][4];
@@ -1012,7 +1061,8 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     }
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const bool wrap = fold && !fold_exact(P);
-    const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double);  // psi, ipsi, two polynomials, monomial tables
+    const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double)  // psi, ipsi, two polynomials, monomial tables
+                       + (TFHE_AI_PROBE == 4 ? (size_t)P.n * 4 : 0);
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,

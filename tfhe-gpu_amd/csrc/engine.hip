@@ -753,11 +753,17 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, xs);
             if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, xs);
             if (st != TFHE_OK) break;
-            HCHECK(hipEventRecord(d.h2d_ev[set], xs));
-            HCHECK(hipStreamWaitEvent(cs, d.h2d_ev[set], 0));
+            // no early return below this point: both streams are synchronised before returning
+            if (hipEventRecord(d.h2d_ev[set], xs) != hipSuccess || hipStreamWaitEvent(cs, d.h2d_ev[set], 0) != hipSuccess) {
+                st = fail(TFHE_ERR_DEVICE, "host batch: event ordering failed");
+                break;
+            }
             st = op(d, din1, din2, dout, b, off);
             if (st != TFHE_OK) break;
-            HCHECK(hipEventRecord(d.k_ev[set], cs));
+            if (hipEventRecord(d.k_ev[set], cs) != hipSuccess) {
+                st = fail(TFHE_ERR_DEVICE, "host batch: event record failed");
+                break;
+            }
             if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu queued at %.2f ms\n", k, now() - t0);
             if (k > 0) st = d2h(k - 1);
         }
@@ -784,10 +790,10 @@ tfhe_status create_ctx(const tfhe_params* p, int num_gpus, std::unique_ptr<tfhe_
     SCHECK(init_derived(c.get()));
     int count = 0;
     HCHECK(hipGetDeviceCount(&count));
-    if (num_gpus < 1) num_gpus = 1;
-    if (num_gpus > count)
-        return fail(TFHE_ERR_INVALID_ARGUMENT,
-                    "requested " + std::to_string(num_gpus) + " GPUs, " + std::to_string(count) + " visible");
+    if (count < 1) return fail(TFHE_ERR_DEVICE, "no HIP device visible");
+    // GPUSetup(numGPUs): numGPUs <= 0 or more than visible uses every visible device
+    // (bootstrapping.cu:736-739)
+    if (num_gpus < 1 || num_gpus > count) num_gpus = count;
     c->devs.resize(num_gpus);
     for (int g = 0; g < num_gpus; ++g) c->devs[g].id = g;
     out = std::move(c);
@@ -1059,20 +1065,31 @@ tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_m
         if (B == 0) return TFHE_OK;
         if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
         const tfhe_params& p = c->p;
-        return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-            const size_t chunk = std::min(cnt, c->max_chunk);
-            SCHECK(ensure_scratch(c, d, chunk));
-            SCHECK(sc_acquire(d, d.stream));
-            for (size_t off = lo; off < lo + cnt; off += chunk) {
-                const size_t b = std::min(chunk, lo + cnt - off);
-                HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
-                HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * 2 * p.N, b * 2 * p.N * 8, hipMemcpyHostToDevice, d.stream));
-                SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
-                HCHECK(hipMemcpyAsync(acc + off * 2 * p.N, d.sc.acc, b * 2 * p.N * 8, hipMemcpyDeviceToHost, d.stream));
-                HCHECK(hipStreamSynchronize(d.stream));
-            }
-            return TFHE_OK;
-        });
+        const size_t wacc = 2 * (size_t)p.N;
+        // pinned, staged copies (run_lwe_batch); the blind rotation runs in place on the input
+        // set's accumulators, which then move to the output set (one device copy)
+        return run_lwe_batch(c, B, a, p.n, acc, wacc, acc, wacc,
+                             [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
+                                 HCHECK(hipMemcpyAsync(o, i2, b * wacc * 8, hipMemcpyDeviceToDevice, d.stream));
+                                 return dev_blind_rotate(c, d, i1, a_mod, o, b);
+                             });
+    });
+}
+
+tfhe_status tfhe_eval_acc_tv(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_mod, const uint64_t* tv,
+                             uint32_t tv_len, uint64_t* acc) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!a || !tv || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const tfhe_params& p = c->p;
+        if (tv_len == 0 || tv_len > p.N || p.N % tv_len != 0)
+            return fail(TFHE_ERR_INVALID_ARGUMENT, "test-vector length must divide N");
+        return run_lwe_batch(c, B, a, p.n, tv, tv_len, acc, 2 * (size_t)p.N,
+                             [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
+                                 HCHECK(launch_expand_tv(p.N, tv_len, i2, o, b, d.stream));
+                                 return dev_blind_rotate(c, d, i1, a_mod, o, b);
+                             });
     });
 }
 

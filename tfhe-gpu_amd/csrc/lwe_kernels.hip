@@ -223,6 +223,26 @@ hipError_t launch_extract(uint32_t N, uint64_t Q, uint64_t b_add, const uint64_t
     return hipGetLastError();
 }
 
+// Sparse test vectors of the drop-in path (tfhe_eval_acc_tv): tv[B][tvlen] -> acc[B][2][N] with
+// acc0 = 0 and acc1[j * factor] = tv[j] (the accumulators BootstrapGateCore / BootstrapFuncCore
+// build, binfhe-base-scheme.cpp:1110-1138, 1163-1185), every other coefficient 0.
+__global__ void k_expand_tv(uint32_t N, uint32_t tvlen, uint32_t factor, const uint64_t* __restrict__ tv,
+                            uint64_t* __restrict__ acc) {
+    const uint64_t* t = tv + (size_t)blockIdx.x * tvlen;
+    uint64_t* g = acc + (size_t)blockIdx.x * 2 * N;
+    for (uint32_t x = threadIdx.x; x < N; x += blockDim.x) {
+        g[x] = 0;
+        g[N + x] = x % factor == 0 ? t[x / factor] : 0;
+    }
+}
+
+hipError_t launch_expand_tv(uint32_t N, uint32_t tvlen, const uint64_t* tv, uint64_t* acc, size_t B, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (tvlen == 0 || N % tvlen != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_expand_tv, dim3((unsigned)B), dim3(256), 0, s, N, tvlen, N / tvlen, tv, acc);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // LWE glue, element-wise over [B][n+1]
 // ---------------------------------------------------------------------------

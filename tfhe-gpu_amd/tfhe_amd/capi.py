@@ -68,6 +68,7 @@ _SIGS = {
     "tfhe_setup_eval": ([C.POINTER(VP), P, u64p, u64p, C.c_int], C.c_int),
     "tfhe_clean": ([VP], C.c_int),
     "tfhe_eval_acc": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_eval_acc_tv": ([VP, SZ, u64p, U64, u64p, C.c_uint32, u64p], C.c_int),
     "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),
     "tfhe_ciphertext_mul_matrix": ([VP, SZ, u64p, SZ, i64p, U64, u64p], C.c_int),
     "tfhe_lwe_gpu_setup": ([C.c_int], C.c_int),
