@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 2  /* 2: tfhe_info.br_kernel */
+#define TFHE_HIP_ABI_VERSION 3  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -99,14 +99,21 @@ typedef struct tfhe_info {
     uint64_t bootstraps;       /* blind rotations executed since setup */
     uint64_t key_image_bytes;  /* size of the exportable device key image */
     int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
+    int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
+    double replicate_ms;       /* wall time of that replication (0 for one device) */
 } tfhe_info;
+
+/* tfhe_info.replicate_method */
+#define TFHE_REPLICATE_NONE 0  /* one device */
+#define TFHE_REPLICATE_RCCL 1  /* one RCCL broadcast from device 0 over xGMI (librccl, loaded at setup) */
+#define TFHE_REPLICATE_PEER 2  /* concurrent peer copies from device 0 (no RCCL, or TFHE_REPLICATE=peer) */
 
 /* tfhe_info.br_kernel */
 #define TFHE_BR_GENERIC 0      /* generic v2 (or v1) Shoup kernel, blind_rotate_generic.hip */
 #define TFHE_BR_FAST 1         /* specialised STD128 kernel, blind_rotate_fast4.hip */
 #define TFHE_BR_F64 2          /* exact-FP64 kernel, blind_rotate_f64.hip */
 #define TFHE_BR_F64_FOLD 3     /* exact-FP64 kernel, top digit's transforms eliminated */
-#define TFHE_BR_RNS 4          /* four-prime RNS kernel (2^53 < Q < 2^58), blind_rotate_rns.hip */
+#define TFHE_BR_RNS 4          /* (retired in round 3: the four-prime RNS kernel; never returned) */
 #define TFHE_BR_SF 5           /* special-form u64 kernel (Q = 2^54 - c), blind_rotate_generic.hip sf2 / gen3sf */
 
 typedef struct tfhe_ctx tfhe_ctx;
@@ -194,6 +201,16 @@ const char* tfhe_last_error(void);
 int tfhe_abi_version(void);
 /* host-only self test of the NTT tables and packing (no GPU needed); 0 = pass */
 tfhe_status tfhe_host_selftest(const tfhe_params* p);
+
+/* ---- sharding (no reference counterpart; the reference deals SM_count-sized chunks round-robin,
+ * bootstrapping.cu:1617): contiguous shard `rank` of `world` over `total` units, sizes differing by at
+ * most one -- the split tfhe_setup(num_gpus) contexts use across their devices and bench.py uses across
+ * ranks.  tfhe_host_shard_selftest runs the multi-device runner (one host thread per device) on
+ * `devices` fake devices with no GPU: spans[2g], spans[2g+1] = the (lo, count) device g was given;
+ * fail_device >= 0 makes that device's body fail, and the call returns its status with
+ * tfhe_last_error() = "device <g>: ...". ---- */
+tfhe_status tfhe_shard_range(size_t total, int world, int rank, size_t* lo, size_t* hi);
+tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, size_t* spans);
 
 /* ---- extension (no reference counterpart): build of the specialised STD128-class blind
  * rotation used by later calls, for A/B runs and tests; 0 restores the default.  Process-wide;

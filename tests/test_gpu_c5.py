@@ -1,0 +1,69 @@
+"""GPU: BASELINE config C5 on its own workload -- large-precision EvalSign with Qin = 2^23
+(time-estimate.cpp:158-189; binfhe-base-scheme.cpp:989-1037), batch 1024, on
+both contexts SURVEY 8(d) names:
+  C5a STD128Q (GenerateBinFHEContext(STD128Q, GINX)): 7 EvalFloor iterations (2 bootstraps each)
+      + 1 = 15 bootstraps per sign, exact-FP64 f64w kernel with the WRAP correction;
+  C5b STD128 logQ = 23, throw = 1: 3 iterations + 1 = 7 bootstraps, special-form u64 sf2 kernel.
+Valid keys from the oracle's keygen, p = GetMaxPlaintextSpace * Qin / q = 2^15.  Checks: every
+output decrypts to [m >= p/2] except within MARGIN of a sign boundary (p/2, or 0 = p), every such
+failure is the algorithm's own -- the oracle returns the same ciphertext bit for bit (on C5a,
+seed 5: m = p/2 - 4, p - 1 and p - 28 decrypt wrongly on the CPU oracle too) -- and a sample of the
+batch equals the oracle bit for bit; the reference's own outputs on these contexts are pinned by
+tests/test_gpu_ref_vectors.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+QIN = 1 << 23
+B = 1024
+# sign failures of the algorithm itself stay within this distance of a boundary (p/2 or 0)
+MARGIN = {"C5a_STD128Q": 64, "C5b_logQ23": 8}
+
+
+@pytest.fixture(scope="module", params=["C5a_STD128Q", "C5b_logQ23"])
+def c5(request, oracle):
+    import tfhe_amd
+
+    if request.param == "C5a_STD128Q":
+        op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
+    else:
+        op = oracle.params_from_logq("STD128", False, 23, 0, 0, 1)
+        cp = tfhe_amd.params_from_logq("STD128", False, 23, 0, 0, 1)
+    rng = oracle.Rng(31)
+    sk, bsk, ksk = oracle.keygen(op, rng)
+    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    yield dict(name=request.param, op=op, sk=sk, ctx=ctx, orc=orc, rng=rng)
+    ctx.GPUClean()
+    orc.close()
+
+
+def test_c5_evalsign_batch_decrypts_and_matches_oracle(c5, oracle):
+    op, sk, ctx, orc, rng = c5["op"], c5["sk"], c5["ctx"], c5["orc"], c5["rng"]
+    p = (op.q // 128 // 2) * (QIN // op.q)  # GetMaxPlaintextSpace() * factor (time-estimate.cpp:171-173)
+    assert p == 1 << 15
+    rs = np.random.default_rng(5)
+    ms = rs.integers(0, p, B)
+    ms[:8] = [0, 1, p // 2 - 4, p // 2 + 3, p // 2 + 4, p - 1, p // 4, 3 * p // 4]
+    ct = np.stack([oracle.encrypt(op, rng, sk, int(m), p, QIN) for m in ms])
+    out = ctx.EvalSign(ct, QIN)
+    dec = np.array([oracle.decrypt(op, sk, r, 2, op.q) for r in out])
+    want = (ms >= p // 2).astype(dec.dtype)
+    margin = MARGIN[c5["name"]]
+    dist = np.minimum(np.abs(ms - p // 2), np.minimum(ms, p - ms))  # to the nearest sign boundary
+    bad = np.flatnonzero(dec != want)
+    assert bad.size <= 8 and np.all(dist[bad] < margin), (c5["name"], bad[:10], ms[bad[:10]])
+    idx = sorted(set([0, 4, 511, 1023] + bad.tolist()))
+    assert np.array_equal(out[idx], orc.eval_sign(ct[idx], QIN)), c5["name"]
+
+
+def test_c5_bootstrap_count(c5, oracle):
+    """2 bootstraps per EvalFloor iteration + 1 (binfhe-base-scheme.cpp:1011-1032): 15 (C5a), 7 (C5b)."""
+    op, ctx = c5["op"], c5["ctx"]
+    before = ctx.info().bootstraps
+    ct = np.zeros((4, op.n + 1), dtype=np.uint64)
+    ctx.EvalSign(ct, QIN)
+    per = (ctx.info().bootstraps - before) // 4
+    assert per == (15 if c5["name"] == "C5a_STD128Q" else 7), per

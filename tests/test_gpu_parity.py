@@ -411,15 +411,13 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
 
 
 @pytest.mark.parametrize("arb,logq,path,kernel", [(True, 12, "sf", 5), (False, 23, "sf", 5), (True, 12, "gen3sf", 5),
-                                                   (False, 23, "gen3sf", 5), (True, 12, "rns", 4),
-                                                   (False, 23, "rns", 4), (True, 12, "generic", 0),
+                                                   (False, 23, "gen3sf", 5), (True, 12, "generic", 0),
                                                    (False, 23, "generic", 0)])
 def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     """The logQ contexts (Q = 2^54 - 77823, N = 2048, throw = 1: C3 logQ=12 with one 27-bit digit
     per polynomial, C5b logQ=23 with two 18-bit digits) run on the special-form u64 kernel by
-    default (constants as (w, w 2^31 mod Q), five multiplies per product), on the four-prime RNS
-    kernel with TFHE_RNS=1 (exact integer ring product, Garner CRT) and on the Shoup gen3 kernel
-    with TFHE_SF=0; all equal the oracle, for accumulator and key boundary values (0, Q-1, the
+    default (constants as (w, w 2^31 mod Q), five multiplies per product) and on the Shoup gen3
+    kernel with TFHE_SF=0; all equal the oracle, for accumulator and key boundary values (0, Q-1, the
     centring threshold, the largest top digits) and several a-moduli."""
     op = oracle.params_from_logq("STD128", arb, logq, 0, 0, 1)
     cp = capi.params_from_logq("STD128", arb, logq, 0, 0, 1)
@@ -427,10 +425,10 @@ def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
     bsk[: 4 * op.N] = np.array([0, op.Q - 1, op.Q >> 1, (op.Q >> 1) + 1], dtype=np.uint64).repeat(op.N)
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
-    env = {"rns": ("TFHE_RNS", "1"), "generic": ("TFHE_SF", "0"), "gen3sf": ("TFHE_SF2", "0")}.get(path)
+    env = {"generic": ("TFHE_SF", "0"), "gen3sf": ("TFHE_SF2", "0")}.get(path)
     if env:
         os.environ[env[0]] = env[1]
-    try:  # TFHE_RNS / TFHE_SF are read at setup, TFHE_SF2 at every launch
+    try:  # TFHE_SF is read at setup, TFHE_SF2 at every launch
         ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
         assert ctx.info().br_kernel == kernel
         B = 3

@@ -21,9 +21,6 @@
 #include "device_math.hpp"
 #include "kernels.hpp"
 
-#ifndef TFHE_AI_PROBE  // a_i load form in f64w (tools/ai_probe.sh); 0 = the tree's
-#define TFHE_AI_PROBE 0
-#endif
 namespace tfhe {
 namespace {
 
@@ -389,7 +386,8 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     const uint32_t sh = 64 - logG;
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n] (synchronised below)
+    stage_rot_exponents<F64_THREADS>(ex, ap, P.n, amod, twoN);
     const size_t round_words = (size_t)4 * P.dG2 * N;
 
     int64_t acc[2][CN];  // canonical [0, Q)
@@ -434,8 +432,7 @@ k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, cons
     const uint32_t shiftL = P.digits * logG;
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         double A[2][2][CN];  // |A| <= dG2 Q/2 (+)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -609,7 +606,8 @@ __device__ __forceinline__ void f64w_sync() {
 
 // TO_LDS: the units' outputs stay in the buffer (slots 4u .. 4u+3 of the wave's block, read back
 // by the products of this wave) instead of registers
-template <bool RED, bool TO_LDS = false>
+// DELAY (fault probe, see k_blind_rotate_f64w): waves 1.. sleep between passes B and C
+template <bool RED, bool TO_LDS = false, bool DELAY = false>
 __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double (&d)[2][4], const double* psi,
                                              const F64Const& K) {
     constexpr uint32_t N = 2048;
@@ -633,6 +631,10 @@ __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double
         f64_r8_fwd<RED>(p, ad, 8, tw >> 5, psi, K);
     }
     f64w_sync();
+    if constexpr (DELAY) {
+        if (w != 0)
+            for (int z = 0; z < 32; ++z) __builtin_amdgcn_s_sleep(127);
+    }
     {
         uint32_t ad[8];
         ad_C(tw, ad);
@@ -702,8 +704,10 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 }
 
 // FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64, MT:
-// monomial tables in LDS
-template <bool RED, bool WRAP, int LD, bool MT>
+// monomial tables in LDS.  PROBE (fault probe, TFHE_F64W_PROBE; tests/test_gpu_f64w_race.py):
+// bit 1 delays waves 1.. inside the prologue's C' transform (between passes B and C), bit 0
+// omits the barrier after it -- together they reproduce the round-0 race of the round-2 kernel
+template <bool RED, bool WRAP, int LD, bool MT, int PROBE = 0>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
                     const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -714,9 +718,6 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     double* buf = lds_d + 2 * N;  // [2][N]
     double* mt = lds_d + 4 * N;   // monomial tables (k_blind_rotate_f64)
     __shared__ int wflag[2];
-#if TFHE_AI_PROBE == 7
-    __shared__ int wvote[2][8];
-#endif
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
@@ -733,7 +734,6 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const uint32_t sh = 64 - logG;
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
     const size_t round_words = (size_t)4 * P.dG2 * N;
     // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
@@ -747,6 +747,8 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
         }
     if (WRAP && t < 2) wflag[t] = 0;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n]
+    stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
     __syncthreads();
     double Cn[2][4];  // N^-1 NTT(acc) at slots u4 + s, |Cn| <~ Q/2
     {
@@ -757,54 +759,24 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             for (int k = 0; k < CN; ++k)
                 v[p * CN + k] = (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
         double d[2][4];
-        f64w_ntt_fwd<RED>(buf, v, d, psi, K);
+        f64w_ntt_fwd<RED, false, (PROBE & 2) != 0>(buf, v, d, psi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int s = 0; s < 4; ++s) Cn[p][s] = fmodmul(d[p][s], K.Ninv, K);
     }
+    // passes C and the units of that transform read the wave's own block of the buffer, and
+    // round 0's first pass A (no barrier of its own) writes every block: without this barrier a
+    // wave that gets here first overwrites blocks other waves are still reading (the wrong
+    // STD128Q / STD192 ciphertexts of round 2)
+    if constexpr (!(PROBE & 1)) __syncthreads();
     int64_t KdL = 0;  // WRAP: residual after all digits = (c + KdL) >> (L g)
     for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
     const uint32_t shiftL = P.digits * logG;
 
-#if TFHE_AI_PROBE == 4
-    uint32_t* exps = reinterpret_cast<uint32_t*>(mt + 128);  // [n] rotation exponents, staged once
-    for (uint32_t k = t; k < P.n; k += TH) {
-        const uint64_t ar = ap[k] & (amod - 1);
-        exps[k] = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-    }
-    __syncthreads();
-#endif
     for (uint32_t i = 0; i < P.n; ++i) {
-#if TFHE_AI_PROBE == 0
-        // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
-        // consumer of this round's scalar load moved past the forward transform and results came
-        // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
-        const uint64_t ar = ap[i] % amod;
-#elif TFHE_AI_PROBE == 1  // 51071bb: mask, scalar load consumed after the forward transform
-        const uint64_t ar = ap[i] & (amod - 1);
-#elif TFHE_AI_PROBE == 2  // mask, scalar load consumed at once
-        uint64_t araw = ap[i];
-        asm volatile("" : "+s"(araw));
-        const uint64_t ar = araw & (amod - 1);
-#elif TFHE_AI_PROBE == 5  // mask, scalar load waited for at once (no data dependence)
-        const uint64_t araw = ap[i];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t ar = araw & (amod - 1);
-#elif TFHE_AI_PROBE == 7  // as 1, the WRAP vote by an unmasked LDS atomic instead of a masked store
-        const uint64_t ar = ap[i] & (amod - 1);
-#elif TFHE_AI_PROBE == 3  // mask, vector load (not through the scalar cache), then readfirstlane
-        uint32_t z;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-        const uint64_t av = ap[i + z];
-        const uint64_t ar = (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(av >> 32)) << 32) |
-                             __builtin_amdgcn_readfirstlane((uint32_t)av)) & (amod - 1);
-#endif
-#if TFHE_AI_PROBE == 4
-        const uint32_t ai = exps[i];
-#else
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
-#endif
+        // rotation exponent staged in LDS (no 64-bit remainder in the round loop)
+        const uint32_t ai = ex[i];
         const uint32_t round_off = (i & K.kround_mask) * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
@@ -831,13 +803,8 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             if (WRAP && !CORR && l == 0) {
                 // round i - 1 read wflag[(i + 1) & 1] before its inverse barrier; round i + 1
                 // writes it after this round's barriers; the forward barrier publishes the vote
-#if TFHE_AI_PROBE == 7
-                // per-wave vote slots, written by every lane (no exec-masked store, no reset)
-                wvote[i & 1][t >> 6] = __builtin_amdgcn_ballot_w64(wv) != 0;
-#else
                 if (t == 0) wflag[(i + 1) & 1] = 0;
                 if (wv) wflag[i & 1] = 1;
-#endif
             }
             if (sync) __syncthreads();  // other waves may still read their blocks
             if (!CORR && l + 1 == LD) f64w_ntt_fwd<RED, true>(buf, v, d, psi, K);
@@ -853,13 +820,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 #pragma unroll
             for (int s = 0; s < 4; ++s) Cx[p][s] = Cn[p][s];
         if constexpr (WRAP) {
-#if TFHE_AI_PROBE == 7
-            const int* wvs = wvote[i & 1];
-            const bool wset = (wvs[0] | wvs[1] | wvs[2] | wvs[3] | wvs[4] | wvs[5] | wvs[6] | wvs[7]) != 0;
-#else
-            const bool wset = wflag[i & 1] != 0;
-#endif
-            if (wset) {
+            if (wflag[i & 1]) {
                 // the correction's transform overwrites the buffer that holds the last digit's
                 // outputs: transform the last digit again afterwards (rare rounds only)
                 double dc[2][4];
@@ -1061,8 +1022,8 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     }
     if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const bool wrap = fold && !fold_exact(P);
-    const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double)  // psi, ipsi, two polynomials, monomial tables
-                       + (TFHE_AI_PROBE == 4 ? (size_t)P.n * 4 : 0);
+    // psi, ipsi, two polynomials, monomial tables, rotation exponents
+    const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
     auto go = [&](auto kern) {
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
@@ -1086,6 +1047,17 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         const int ld = (int)P.digits - 1;
 #define F64W_GO(R, W, L)                                                                     \
     (m ? go(k_blind_rotate_f64w<R, W, L, true>) : go(k_blind_rotate_f64w<R, W, L, false>))
+        const int probe = [] {  // fault probe, read per launch (tests/test_gpu_f64w_race.py)
+            const char* e = std::getenv("TFHE_F64W_PROBE");
+            return e && e[0] ? e[0] - '0' : 0;
+        }();
+        if (probe != 0) {  // STD128Q's instance only
+            if (!(red && wrap && ld == 1 && m)) return hipErrorInvalidValue;
+            if (probe == 2) go(k_blind_rotate_f64w<true, true, 1, true, 2>);
+            else if (probe == 3) go(k_blind_rotate_f64w<true, true, 1, true, 3>);
+            else return hipErrorInvalidValue;
+            return hipGetLastError();
+        }
         if (red) {
             if (wrap) ld == 1 ? F64W_GO(true, true, 1) : F64W_GO(true, true, 2);
             else ld == 1 ? F64W_GO(true, false, 1) : F64W_GO(true, false, 2);

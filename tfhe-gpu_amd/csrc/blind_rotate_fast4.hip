@@ -688,24 +688,10 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
         return hipGetLastError();
     }
     if (!(sh.dig == 4 && sh.logg == 7 && sh.thr == 0 && sh.fold)) return hipErrorNotSupported;
-    switch (variant) {
-        case 59: launch(f4::k_blind_rotate_fast4<3, 1, 0, 3, 1>, 1, 1); break;
-        case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;      // two ciphertexts per wavefront
-        case 81: launch(f4::k_blind_rotate_fast4<4, 1, 0, 3, 1>, 1, 1); break;   // pass-0 first stage only
-        case 83: launch(f4::k_blind_rotate_fast4<4, 1, 0, 11, 1>, 1, 1); break;  // + pass-4 twiddles in LDS
-        case 84: launch(f4::k_blind_rotate_fast4<4, 1, 0, 15, 1>, 1, 1); break;  // both
-        case 85: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 2>, 1, 1, 2); break;  // 2 ciphertexts per workgroup
-        case 86: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 4>, 1, 1, 4); break;  // 4 ciphertexts per workgroup
-        case 87: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 2, 2>, 1, 2, 2); break;  // 2 per workgroup, 2 cross areas
-        case 88: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 2, 4>, 1, 2, 4); break;  // 4 per workgroup, 2 cross areas
-        case 76: launch(f4::k_blind_rotate_fast4<4, 1, 0, 0, 1>, 1, 1); break;  // without the OPT changes
-        case 61: launch(f4::k_blind_rotate_fast4<4, 1, 1, 3, 1>, 1, 1); break;  // timing only: no barriers
-        case 62: launch(f4::k_blind_rotate_fast4<4, 1, 2, 3, 1>, 1, 1); break;  // timing only: no key loads
-        case 65: launch(f4::k_blind_rotate_fast4<4, 1, 8, 3, 1>, 1, 1); break;  // timing only: no transforms
-        case 71: launch(f4::k_blind_rotate_fast4<2, 2, 1>, 2); break;   // timing only: no barriers
-        case 72: launch(f4::k_blind_rotate_fast4<2, 2, 2>, 2); break;   // timing only: no key loads
-        case 75: launch(f4::k_blind_rotate_fast4<2, 2, 8>, 2); break;   // timing only: no transforms
-        default: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1>, 1, 1); break;  // = 60 (82)
+    switch (variant) {  // cross-check builds (blind_rotate_fast.hip known_variant)
+        case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;                    // two ciphertexts per wavefront
+        case 86: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 4>, 1, 1, 4); break;  // four per workgroup
+        default: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1>, 1, 1); break;  // = 60
     }
     return hipGetLastError();
 }

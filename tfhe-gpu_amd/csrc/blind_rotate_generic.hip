@@ -82,16 +82,16 @@ k_blind_rotate_generic(BRParams P, const W* __restrict__ psi, const W* __restric
     const uint32_t sh = 64 - P.logG;
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + (size_t)(2 + P.dG2) * N * sizeof(W));  // rotation exponents [n]
+    stage_rot_exponents<GEN_THREADS>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
 
     for (uint32_t k = tid; k < twoN; k += T) acc[k] = (W)g[k];
     __syncthreads();
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        // a'_i = ((amod - a_i) mod amod) * (2N / amod)   (rgsw-acc-cggi.cpp:153, bootstrapping.cu:1623)
-        const uint64_t ar = ap[i] % amod;
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i = ((amod - a_i) mod amod) * (2N / amod), staged (rgsw-acc-cggi.cpp:153)
 
         // signed digit decomposition, row = poly + 2*digit (rgsw-acc.cpp:80-110)
         for (uint32_t k = tid; k < twoN; k += T) {
@@ -277,7 +277,9 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
     const uint32_t sh = 64 - logG;
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + (size_t)2 * N * sizeof(W));  // rotation exponents [n]
+    stage_rot_exponents<GEN_THREADS>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
 
     W acc[2][CN];
@@ -287,8 +289,7 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
         for (int k = 0; k < CN; ++k) acc[p][k] = (W)g[p * N + t + GEN_THREADS * k];
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         W A[2][2][CN];  // A_kj per owned slot, lazily reduced (< 2 dG2 Q)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -552,7 +553,9 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
     const G3Tw<W> TF{psi_l, psis_l}, TI{ipsi, ipsi_sh};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + (size_t)4 * G3_N * sizeof(W));  // rotation exponents [n]
+    stage_rot_exponents<G3_TH>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
     // accumulator entry [p][k]: polynomial t >> 8, coefficient (t & 255) + 256 (p CN + k)
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
@@ -565,8 +568,7 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
     __syncthreads();  // forward twiddles in LDS
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         W A[2][2][CN];  // A_kj per owned slot, lazily reduced (< 2 dG2 Q)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -857,7 +859,9 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     const SfTw TF{psi_l, psi1_l}, TI{ipsi, ipsi1};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * G3_N + SF_MT) * 8);  // rotation exponents [n]
+    stage_rot_exponents<G3_TH>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
 
@@ -872,8 +876,7 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     __syncthreads();  // forward twiddles in LDS
 
     for (uint32_t i = 0; i < P.n; ++i) {
-        const uint64_t ar = ap[i] % amod;  // rgsw-acc-cggi.cpp:153
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         uint64_t A[2][2][CN];  // A_kj per owned slot (< 2.1 Q per digit)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
@@ -1108,7 +1111,9 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    const uint64_t scale = (uint64_t)twoN / amod;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * G3_N + SF_MT) * 8);  // rotation exponents [n]
+    stage_rot_exponents<G3_TH>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
@@ -1129,8 +1134,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
         // consumer of this round's scalar load moved past the forward transform and results came
         // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
-        const uint64_t ar = ap[i] % amod;
-        const uint32_t ai = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
         uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
 #pragma unroll
@@ -1256,7 +1260,7 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
         return e && e[0] == '0';
     }();
     if (!v1 && !no_gen3 && P.N == G3_N) {
-        const size_t lds = (size_t)4 * G3_N * wb;  // two polynomials + forward twiddles
+        const size_t lds = (size_t)4 * G3_N * wb + rot_exponent_bytes(P.n);  // two polynomials, forward twiddles, a'_i
         auto go3 = [&](auto tag) {
             using W = decltype(tag);
             auto kern = k_blind_rotate_gen3<W>;
@@ -1270,7 +1274,7 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
         return hipGetLastError();
     }
     if (!v1 && (P.N == 1024 || P.N == 2048)) {
-        const size_t lds2 = (size_t)2 * P.N * wb;
+        const size_t lds2 = (size_t)2 * P.N * wb + rot_exponent_bytes(P.n);
         dim3 grid((unsigned)B), block(GEN_THREADS);
         auto go = [&](auto kern, auto tag) {
             using W = decltype(tag);
@@ -1285,7 +1289,7 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
             P.N == 1024 ? go(k_blind_rotate_gen2<uint64_t, 4>, uint64_t{}) : go(k_blind_rotate_gen2<uint64_t, 8>, uint64_t{});
         return hipGetLastError();
     }
-    const size_t lds = (size_t)(2 + P.dG2) * P.N * wb;
+    const size_t lds = (size_t)(2 + P.dG2) * P.N * wb + rot_exponent_bytes(P.n);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     dim3 grid((unsigned)B), block(GEN_THREADS);
     if (word_bits == 32) {
@@ -1339,7 +1343,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     K.Q = P.Q, K.Q2 = 2 * P.Q, K.Q9 = 9 * P.Q;
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     const uint64_t* w1 = (const uint64_t*)sf;
-    const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8;  // two polynomials, forward twiddles, monomial tables
+    const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8 + rot_exponent_bytes(P.n);  // two polynomials, forward twiddles, monomial tables, a'_i
     const bool no_sf2 = [] {  // read per launch (tests and A/B runs switch it)
         const char* e = std::getenv("TFHE_SF2");
         return e && e[0] == '0';

@@ -63,4 +63,19 @@ __device__ __forceinline__ uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q)
     return (uint64_t)floor(__dadd_rn(0.5, u)) % q;
 }
 
+// Rotation exponents a'_i = ((amod - a_i) mod amod) * (2N / amod) of one ciphertext
+// (rgsw-acc-cggi.cpp:153, bootstrapping.cu:1623), written to LDS once at kernel start by the whole
+// workgroup, so the round loops carry no 64-bit remainder.  The caller synchronises the workgroup
+// before the first read.
+template <int TH>
+__device__ __forceinline__ void stage_rot_exponents(uint32_t* ex, const uint64_t* ap, uint32_t n, uint64_t amod,
+                                                    uint32_t twoN) {
+    const uint64_t scale = (uint64_t)twoN / amod;
+    for (uint32_t k = threadIdx.x; k < n; k += TH) {
+        const uint64_t ar = ap[k] % amod;
+        ex[k] = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+    }
+}
+__host__ __device__ constexpr size_t rot_exponent_bytes(uint32_t n) { return ((size_t)n * 4 + 15) & ~(size_t)15; }
+
 }  // namespace tfhe

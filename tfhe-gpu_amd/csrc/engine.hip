@@ -10,7 +10,9 @@
 //    MKM -> LWE glue, one stream per device, host sees only LWE ciphertexts;
 //  * a batch is split into contiguous shards, one host thread + stream per
 //    device (the reference interleaves SM_count-sized chunks, bootstrapping.cu:1617).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -114,7 +116,6 @@ struct Device {
     unsigned char* arena = nullptr;
     void* bsk_fast = nullptr;
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
-    void* keys_rns = nullptr;  // RNS path: prime tables + residue BSK
     void* keys_sf = nullptr;   // special-form path: W1 = w 2^31 mod Q of the arena's tables and BSK
     Scratch sc;
     DevTables tables{};
@@ -162,13 +163,14 @@ struct tfhe_ctx {
     bool use_fast = false;
     bool use_f64 = false;
     bool f64_fold = false;  // exact-FP64 kernel with the top digit's transforms eliminated
-    bool use_rns = false;   // four-prime RNS kernel (logQ / arbFunc contexts, opt-in)
     bool use_sf = false;    // special-form u64 kernel (logQ / arbFunc contexts, default)
     BRParams br{};
     KSParams ks{};
     ArenaLayout layout{};
     std::vector<Device> devs;
     std::atomic<uint64_t> bootstraps{0};
+    int replicate_method = TFHE_REPLICATE_NONE;
+    double replicate_ms = 0;
     size_t max_chunk = 65536;  // the reference's max_bootstapping_num, bootstrapping.cuh:140
     ~tfhe_ctx();  // frees every device's arena, scratch, streams (error paths included)
 };
@@ -203,14 +205,9 @@ tfhe_status init_derived(tfhe_ctx* c) {
     c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     c->use_f64 = f64_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     c->f64_fold = c->use_f64 && f64_fold_enabled(c->br);
-    // TFHE_RNS=1: the four-prime RNS kernel for the logQ contexts (opt-in: measured slower than
-    // the u64 kernel)
-    const char* rns = std::getenv("TFHE_RNS");
-    c->use_rns = !c->use_fast && !c->use_f64 && c->word_bits == 64 && rns_path_supported(c->br) &&
-                 !(force && force[0] == '1') && rns && rns[0] == '1';
     // Q = 2^54 - c: the special-form kernel (TFHE_SF=0 keeps the Shoup gen3 kernel)
     const char* sfe = std::getenv("TFHE_SF");
-    c->use_sf = !c->use_fast && !c->use_f64 && !c->use_rns && sf_path_supported(c->br, c->word_bits) &&
+    c->use_sf = !c->use_fast && !c->use_f64 && sf_path_supported(c->br, c->word_bits) &&
                 !(force && force[0] == '1') && !(sfe && sfe[0] == '0');
     if (p.Q >= (1ull << 58) || (c->word_bits == 64 && (u128)2 * p.dG2 * p.Q >= ((u128)1 << 64)))
         return fail(TFHE_ERR_UNSUPPORTED, "modulus too large for lazy accumulation");
@@ -328,11 +325,6 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
         HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
         HCHECK(hipStreamSynchronize(d.stream));
     }
-    if (c->use_rns) {
-        HCHECK(hipMalloc(&d.keys_rns, rns_keys_bytes(c->br)));
-        HCHECK(launch_pack_bsk_rns(c->br, d.tables, d.arena + c->layout.bsk, d.keys_rns, d.stream));
-        HCHECK(hipStreamSynchronize(d.stream));
-    }
     return TFHE_OK;
 }
 
@@ -344,7 +336,6 @@ void free_device(Device& d) {
     hipFree(d.arena);
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
-    hipFree(d.keys_rns);
     hipFree(d.keys_sf);
     if (d.stream2) hipStreamSynchronize(d.stream2);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
@@ -417,8 +408,6 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
     } else if (c->use_f64) {
         HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream));
-    } else if (c->use_rns) {
-        HCHECK(launch_blind_rotate_rns(c->br, d.tables, d.keys_rns, a, amod, acc, B, d.stream));
     } else if (c->use_sf) {
         HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream));
     } else {
@@ -615,33 +604,43 @@ tfhe_status dev_sign(tfhe_ctx* c, Device& d, const uint64_t* ct, uint64_t mod, u
 // ---------------------------------------------------------------------------
 // host-array front ends: shard over devices, chunk to scratch, H2D/D2H
 // ---------------------------------------------------------------------------
-template <typename F>
-tfhe_status for_each_shard(tfhe_ctx* c, size_t B, F&& body) {
-    const size_t D = c->devs.size();
+// One host thread per device, each on a contiguous shard (shard_span).  select(g) makes device g
+// current on the calling thread (hipSetDevice; a no-op in tfhe_host_shard_selftest); body(g, lo, cnt)
+// queues and waits for that shard.  Every thread's status and thread-local error message is
+// collected; the first failing device's is returned as "device g: ...".
+template <typename Select, typename Body>
+tfhe_status run_shards(size_t D, size_t B, Select&& select, Body&& body) {
     if (D == 1 || B < 2 * D) {
-        HCHECK(hipSetDevice(c->devs[0].id));
-        return body(c->devs[0], (size_t)0, B);
+        SCHECK(select(0));
+        return body((size_t)0, (size_t)0, B);
     }
     std::vector<tfhe_status> st(D, TFHE_OK);
     std::vector<std::string> msg(D);
     std::vector<std::thread> th;
-    const size_t per = (B + D - 1) / D;
     for (size_t g = 0; g < D; ++g) {
-        const size_t lo = std::min(B, g * per), hi = std::min(B, lo + per);
-        th.emplace_back([&, g, lo, hi] {
-            if (hipSetDevice(c->devs[g].id) != hipSuccess) {
-                st[g] = TFHE_ERR_DEVICE;
-                msg[g] = "hipSetDevice failed";
-                return;
-            }
-            if (hi > lo) st[g] = body(c->devs[g], lo, hi - lo);
-            if (st[g] != TFHE_OK) msg[g] = g_last_error;
+        size_t lo, cnt;
+        shard_span(B, D, g, &lo, &cnt);
+        th.emplace_back([&, g, lo, cnt] {
+            st[g] = select(g);
+            if (st[g] == TFHE_OK && cnt > 0) st[g] = body(g, lo, cnt);
+            if (st[g] != TFHE_OK) msg[g] = g_last_error;  // thread_local: this thread's message
         });
     }
     for (auto& t : th) t.join();
     for (size_t g = 0; g < D; ++g)
         if (st[g] != TFHE_OK) return fail(st[g], "device " + std::to_string(g) + ": " + msg[g]);
     return TFHE_OK;
+}
+
+template <typename F>
+tfhe_status for_each_shard(tfhe_ctx* c, size_t B, F&& body) {
+    return run_shards(
+        c->devs.size(), B,
+        [&](size_t g) -> tfhe_status {
+            HCHECK(hipSetDevice(c->devs[g].id));
+            return TFHE_OK;
+        },
+        [&](size_t g, size_t lo, size_t cnt) { return body(c->devs[g], lo, cnt); });
 }
 
 // Host <-> device copies through two pinned 8 MiB blocks: the host copy pool fills (or
@@ -718,9 +717,11 @@ tfhe_status ensure_io_set(Scratch& sc, size_t words) {
     return TFHE_OK;
 }
 
+// out_in: the output rows' initial contents (uploaded into the output set before the kernels of
+// their sub-batch, for ops that work in place on the output, e.g. the blind rotation)
 template <typename Op>
 tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
-                          uint64_t* out, size_t wo, Op&& op) {
+                          uint64_t* out, size_t wo, Op&& op, const uint64_t* out_in = nullptr) {
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
         const size_t parts = host_parts(cnt);
         const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
@@ -752,6 +753,7 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             uint64_t *din1 = io[set], *din2 = in2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
             st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, xs);
             if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, xs);
+            if (st == TFHE_OK && out_in) st = h2d_staged(d, dout, out_in + off * wo, b * wo * 8, xs);
             if (st != TFHE_OK) break;
             // no early return below this point: both streams are synchronised before returning
             if (hipEventRecord(d.h2d_ev[set], xs) != hipSuccess || hipStreamWaitEvent(cs, d.h2d_ev[set], 0) != hipSuccess) {
@@ -878,6 +880,84 @@ tfhe_status tfhe_params_finish(tfhe_params* p) {
 }
 
 namespace {
+// RCCL, loaded when a context spans several devices (no link-time dependency for one-GPU use)
+struct RcclApi {
+    bool ok = false;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclBroadcast) bcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+};
+const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return a;
+        a.init_all = (decltype(a.init_all))dlsym(h, "ncclCommInitAll");
+        a.bcast = (decltype(a.bcast))dlsym(h, "ncclBroadcast");
+        a.group_start = (decltype(a.group_start))dlsym(h, "ncclGroupStart");
+        a.group_end = (decltype(a.group_end))dlsym(h, "ncclGroupEnd");
+        a.destroy = (decltype(a.destroy))dlsym(h, "ncclCommDestroy");
+        a.err = (decltype(a.err))dlsym(h, "ncclGetErrorString");
+        a.ok = a.init_all && a.bcast && a.group_start && a.group_end && a.destroy && a.err;
+        return a;
+    }();
+    return api;
+}
+
+// Device 0's image -> devices 1..D-1.  GPUSetup(numGPUs) in the reference copies every key from the
+// host to each GPU in turn (bootstrapping.cu:1005-1069); here the image crosses PCIe once and is
+// broadcast by RCCL over xGMI (one communicator over the context's devices, one ncclBroadcast per
+// device in a group), or -- without librccl, or with TFHE_REPLICATE=peer -- copied from device 0 by
+// concurrent peer DMAs.  Every device's copy is complete when this returns.
+tfhe_status replicate_arena(tfhe_ctx* c, size_t bytes) {
+    const size_t D = c->devs.size();
+    if (D < 2) return TFHE_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const char* env = std::getenv("TFHE_REPLICATE");
+    const bool want_rccl = !(env && std::strcmp(env, "peer") == 0);
+    bool done = false;
+    if (want_rccl && rccl().ok) {
+        const RcclApi& R = rccl();
+        std::vector<ncclComm_t> comms(D);
+        std::vector<int> ids(D);
+        for (size_t g = 0; g < D; ++g) ids[g] = c->devs[g].id;
+        if (R.init_all(comms.data(), (int)D, ids.data()) == ncclSuccess) {
+            ncclResult_t r = R.group_start();
+            for (size_t g = 0; g < D && r == ncclSuccess; ++g) {
+                Device& d = c->devs[g];
+                HCHECK(hipSetDevice(d.id));
+                r = R.bcast(c->devs[0].arena, d.arena, bytes, ncclUint8, 0, comms[g], d.stream);
+            }
+            const ncclResult_t r2 = R.group_end();
+            bool synced = r == ncclSuccess && r2 == ncclSuccess;
+            for (size_t g = 0; g < D; ++g) {
+                hipSetDevice(c->devs[g].id);
+                synced = hipStreamSynchronize(c->devs[g].stream) == hipSuccess && synced;
+            }
+            for (auto& cm : comms) R.destroy(cm);
+            done = synced;
+        }
+    }
+    if (!done) {
+        for (size_t g = 1; g < D; ++g) {
+            Device& d = c->devs[g];
+            HCHECK(hipSetDevice(d.id));
+            HCHECK(hipMemcpyPeerAsync(d.arena, d.id, c->devs[0].arena, c->devs[0].id, bytes, d.stream));
+        }
+        for (size_t g = 1; g < D; ++g) {
+            HCHECK(hipSetDevice(c->devs[g].id));
+            HCHECK(hipStreamSynchronize(c->devs[g].stream));
+        }
+    }
+    c->replicate_method = done ? TFHE_REPLICATE_RCCL : TFHE_REPLICATE_PEER;
+    c->replicate_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return TFHE_OK;
+}
+
 tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, bool bsk_eval,
                          const uint64_t* ksk, int num_gpus) {
     if (!out || !bsk_coeff || !ksk) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
@@ -892,14 +972,19 @@ tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* b
         HCHECK(hipSetDevice(d.id));
         SCHECK(create_streams(d));
         HCHECK(hipMalloc(&d.arena, bytes));
-        if (g == 0) {
-            HCHECK(hipMemcpy(d.arena, img.data(), bytes, hipMemcpyHostToDevice));
-        } else {
-            // replicate device 0's image over xGMI (peer DMA; staged by the runtime if P2P is off)
-            HCHECK(hipMemcpyPeer(d.arena, d.id, c->devs[0].arena, c->devs[0].id, bytes));
-        }
-        SCHECK(finish_device(c.get(), d));
     }
+    HCHECK(hipSetDevice(c->devs[0].id));
+    HCHECK(hipMemcpy(c->devs[0].arena, img.data(), bytes, hipMemcpyHostToDevice));
+    img = std::vector<unsigned char>();
+    SCHECK(replicate_arena(c.get(), bytes));
+    // derived key forms, every device at once (each derives its own from its arena)
+    SCHECK(run_shards(
+        c->devs.size(), 2 * c->devs.size(),
+        [&](size_t g) -> tfhe_status {
+            HCHECK(hipSetDevice(c->devs[g].id));
+            return TFHE_OK;
+        },
+        [&](size_t g, size_t, size_t) { return finish_device(c.get(), c->devs[g]); }));
     *out = c.release();
     return TFHE_OK;
 }
@@ -1045,17 +1130,41 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
         out->num_devices = (int)c->devs.size();
         out->word_bits = c->word_bits;
         out->bsk_device_bytes = c->layout.ksk - c->layout.bsk + (c->use_fast ? bsk_fast_bytes(c->br) : 0) +
-                                (c->use_f64 ? bsk_f64_bytes(c->br) : 0) + (c->use_rns ? rns_keys_bytes(c->br) : 0) +
+                                (c->use_f64 ? bsk_f64_bytes(c->br) : 0) +
                                 (c->use_sf ? sf_bytes(c->br) : 0);
         out->ksk_device_bytes = c->layout.total - c->layout.ksk;
         out->bootstraps = c->bootstraps.load();
         out->key_image_bytes = c->layout.total;
         out->br_kernel = c->use_fast  ? TFHE_BR_FAST
                          : c->use_f64 ? (c->f64_fold ? TFHE_BR_F64_FOLD : TFHE_BR_F64)
-                         : c->use_rns ? TFHE_BR_RNS
                          : c->use_sf  ? TFHE_BR_SF
                                       : TFHE_BR_GENERIC;
+        out->replicate_method = c->replicate_method;
+        out->replicate_ms = c->replicate_ms;
         return TFHE_OK;
+    });
+}
+
+tfhe_status tfhe_shard_range(size_t total, int world, int rank, size_t* lo, size_t* hi) {
+    if (world < 1 || rank < 0 || rank >= world || !lo || !hi) return fail(TFHE_ERR_INVALID_ARGUMENT, "bad world/rank");
+    size_t l, cnt;
+    shard_span(total, (size_t)world, (size_t)rank, &l, &cnt);
+    *lo = l, *hi = l + cnt;
+    return TFHE_OK;
+}
+
+tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, size_t* spans) {
+    return guarded([&]() -> tfhe_status {
+        if (devices < 1 || !spans) return fail(TFHE_ERR_INVALID_ARGUMENT, "bad arguments");
+        for (int g = 0; g < devices; ++g) spans[2 * g] = spans[2 * g + 1] = 0;
+        return run_shards(
+            (size_t)devices, B, [](size_t) { return TFHE_OK; },
+            [&](size_t g, size_t lo, size_t cnt) -> tfhe_status {
+                spans[2 * g] = lo, spans[2 * g + 1] = cnt;
+                if ((int)g == fail_device) return fail(TFHE_ERR_DEVICE, "injected fault on shard [" + std::to_string(lo) +
+                                                                            ", " + std::to_string(lo + cnt) + ")");
+                return TFHE_OK;
+            });
     });
 }
 
@@ -1066,13 +1175,39 @@ tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_m
         if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
         const tfhe_params& p = c->p;
         const size_t wacc = 2 * (size_t)p.N;
-        // pinned, staged copies (run_lwe_batch); the blind rotation runs in place on the input
-        // set's accumulators, which then move to the output set (one device copy)
-        return run_lwe_batch(c, B, a, p.n, acc, wacc, acc, wacc,
-                             [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
-                                 HCHECK(hipMemcpyAsync(o, i2, b * wacc * 8, hipMemcpyDeviceToDevice, d.stream));
-                                 return dev_blind_rotate(c, d, i1, a_mod, o, b);
-                             });
+        // TFHE_EVAL_ACC_PATH (read per call): "legacy" = pageable copies on the compute stream;
+        // "d2d" = the pinned runner with a device copy into the output set; default "inplace" = the
+        // pinned runner, accumulators uploaded straight into the output set and rotated there
+        const char* e = std::getenv("TFHE_EVAL_ACC_PATH");
+        const std::string path = e && e[0] ? e : "inplace";
+        if (path == "legacy") {
+            return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
+                const size_t chunk = std::min(cnt, c->max_chunk);
+                SCHECK(ensure_scratch(c, d, chunk));
+                SCHECK(sc_acquire(d, d.stream));
+                for (size_t off = lo; off < lo + cnt; off += chunk) {
+                    const size_t b = std::min(chunk, lo + cnt - off);
+                    HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
+                    HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * wacc, b * wacc * 8, hipMemcpyHostToDevice, d.stream));
+                    SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
+                    HCHECK(hipMemcpyAsync(acc + off * wacc, d.sc.acc, b * wacc * 8, hipMemcpyDeviceToHost, d.stream));
+                    HCHECK(hipStreamSynchronize(d.stream));
+                }
+                return TFHE_OK;
+            });
+        }
+        if (path == "d2d")
+            return run_lwe_batch(c, B, a, p.n, acc, wacc, acc, wacc,
+                                 [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
+                                     HCHECK(hipMemcpyAsync(o, i2, b * wacc * 8, hipMemcpyDeviceToDevice, d.stream));
+                                     return dev_blind_rotate(c, d, i1, a_mod, o, b);
+                                 });
+        return run_lwe_batch(
+            c, B, a, p.n, nullptr, 0, acc, wacc,
+            [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
+                return dev_blind_rotate(c, d, i1, a_mod, o, b);
+            },
+            acc);
     });
 }
 

@@ -57,6 +57,16 @@ inline uint64_t addmod(uint64_t a, uint64_t b, uint64_t m) {
     return r >= m ? r - m : r;
 }
 inline uint64_t submod(uint64_t a, uint64_t b, uint64_t m) { return a >= b ? a - b : a + (m - b); }
+// Contiguous shard g of D over B units: [lo, lo + cnt), sizes differing by at most one (the first
+// B mod D shards one larger).  The engine's multi-device split (for_each_shard) and the one-process-
+// per-GPU split of tfhe_amd.dist.shard_range are this function (tfhe_shard_range).  The reference
+// deals SM_count-sized chunks round-robin instead (bootstrapping.cu:1617).
+inline void shard_span(size_t B, size_t D, size_t g, size_t* lo, size_t* cnt) {
+    const size_t base = B / D, extra = B % D;
+    *lo = g * base + (g < extra ? g : extra);
+    *cnt = base + (g < extra ? 1 : 0);
+}
+
 uint64_t powmod(uint64_t b, uint64_t e, uint64_t m);
 bool is_prime(uint64_t x);
 uint32_t ilog2(uint64_t x);

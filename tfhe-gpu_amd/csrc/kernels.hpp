@@ -81,15 +81,6 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
 
-// RNS blind rotation (blind_rotate_rns.hip) for N = 2048, 2^53 < Q < 2^58 of the form 2^k - c (the
-// logQ / arbFunc contexts): four 26-bit NTT primes, signed 32-bit Montgomery arithmetic, exact
-// integer ring product, Garner CRT back to Q.  Keys derived on device from the generic u64 arena.
-bool rns_path_supported(const BRParams& P);
-size_t rns_keys_bytes(const BRParams& P);
-hipError_t launch_pack_bsk_rns(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
-hipError_t launch_blind_rotate_rns(const BRParams& P, const DevTables& T, const void* keys, const uint64_t* a,
-                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
-
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
 //   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.
 //   kska: [N][baseKS][dKS][n_pad] (A part, rows padded to 16 bytes), kskb: [N][baseKS][dKS] (B),

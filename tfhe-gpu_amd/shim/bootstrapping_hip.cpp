@@ -178,8 +178,30 @@ void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> pa
     tm.lap("device", Bn);
     const auto polyParams = params->GetPolyParams();
     const NativeInteger Q = params->GetQ();
+    // Results go into the accumulators' own coefficient vectors when this vector holds the only
+    // reference and they have the shape of the result (the callers' fresh test vectors): no
+    // allocation.  Otherwise new objects, as the reference does (bootstrapping.cu:1655-1664); the
+    // replaced ones are released on this thread afterwards (freeing another thread's blocks from
+    // the OpenMP workers serialises on the allocator).
+    std::vector<RLWECiphertext> old(Bn);
 #pragma omp parallel for
-    for (size_t s = 0; s < Bn; ++s) {  // replaced in place, acc0 already transposed (bootstrapping.cu:675-686)
+    for (size_t s = 0; s < Bn; ++s) {  // acc0 already transposed (bootstrapping.cu:675-686)
+        RLWECiphertext& ct = (*acc)[s];
+        bool reuse = ct.use_count() == 1;
+        if (reuse) {
+            const auto& e = ct->GetElements();
+            for (uint32_t j = 0; j < 2 && reuse; ++j)
+                reuse = e[j].GetFormat() == Format::COEFFICIENT && e[j].GetLength() == N && e[j].GetModulus() == Q;
+        }
+        if (reuse) {
+            auto& e = ct->GetElements();
+            for (uint32_t j = 0; j < 2; ++j) {
+                NativeVector& v = const_cast<NativeVector&>(e[j].GetValues());
+                const uint64_t* src = fac + (s * 2 + j) * N;
+                for (uint32_t x = 0; x < N; ++x) v[x] = src[x];
+            }
+            continue;
+        }
         std::vector<NativePoly> res(2);
         for (uint32_t j = 0; j < 2; ++j) {
             NativeVector v(N, Q);
@@ -188,8 +210,10 @@ void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> pa
             res[j] = NativePoly(polyParams, Format::COEFFICIENT, false);
             res[j].SetValues(std::move(v), Format::COEFFICIENT);
         }
-        (*acc)[s] = std::make_shared<RLWECiphertextImpl>(std::move(res));
+        old[s] = std::move(ct);
+        ct = std::make_shared<RLWECiphertextImpl>(std::move(res));
     }
+    old.clear();
     tm.lap("marshal out", Bn);
 }
 
@@ -211,12 +235,15 @@ void GPUFFTBootstrap::MKMSwitch_CUDA(const std::shared_ptr<LWECryptoParams> para
     tm.lap("marshal in", Bn);
     check(tfhe_mkm_switch(g_ctx, Bn, in, fmod.ConvertToInt(), out), "tfhe_mkm_switch");
     tm.lap("device", Bn);
+    std::vector<LWECiphertext> old(Bn);  // released on this thread (see EvalAcc_CUDA)
 #pragma omp parallel for
     for (size_t s = 0; s < Bn; ++s) {
         NativeVector av(n, fmod);  // output modulus fmod (bootstrapping.cu:1898,1926)
         for (uint32_t k = 0; k < n; ++k) av[k] = out[s * (n + 1) + k];
+        old[s] = std::move((*ctExt)[s]);
         (*ctExt)[s] = std::make_shared<LWECiphertextImpl>(std::move(av), NativeInteger(out[s * (n + 1) + n]));
     }
+    old.clear();
     tm.lap("marshal out", Bn);
 }
 

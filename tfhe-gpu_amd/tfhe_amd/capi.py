@@ -12,7 +12,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
-ABI_VERSION = 2  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (2: tfhe_info.br_kernel)
+ABI_VERSION = 3  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -45,7 +45,7 @@ class Params(C.Structure):
 class Info(C.Structure):
     _fields_ = [("num_devices", C.c_int), ("word_bits", C.c_int), ("bsk_device_bytes", C.c_uint64),
                 ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64),
-                ("br_kernel", C.c_int)]
+                ("br_kernel", C.c_int), ("replicate_method", C.c_int), ("replicate_ms", C.c_double)]
 
 
 u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
@@ -68,6 +68,8 @@ _SIGS = {
     "tfhe_setup_eval": ([C.POINTER(VP), P, u64p, u64p, C.c_int], C.c_int),
     "tfhe_clean": ([VP], C.c_int),
     "tfhe_eval_acc": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_shard_range": ([SZ, C.c_int, C.c_int, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)], C.c_int),
+    "tfhe_host_shard_selftest": ([SZ, C.c_int, C.c_int, C.POINTER(C.c_size_t)], C.c_int),
     "tfhe_eval_acc_tv": ([VP, SZ, u64p, U64, u64p, C.c_uint32, u64p], C.c_int),
     "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),
     "tfhe_ciphertext_mul_matrix": ([VP, SZ, u64p, SZ, i64p, U64, u64p], C.c_int),
@@ -124,7 +126,9 @@ def lib():
             pass
         L = C.CDLL(_LIB)
         for name, (args, res) in _SIGS.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)  # an older build (TFHE_LIB A/B runs) may lack a newer entry point
+            if fn is None:
+                continue
             fn.argtypes = args
             fn.restype = res
         if L.tfhe_abi_version() != ABI_VERSION:  # the structs above mirror this ABI version

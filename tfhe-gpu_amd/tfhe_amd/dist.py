@@ -21,12 +21,18 @@ import torch.distributed as dist
 
 
 def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
-    """Contiguous [lo, hi) of `total` units for `rank` of `world` (sizes differ by <= 1)."""
+    """Contiguous [lo, hi) of `total` units for `rank` of `world` (sizes differ by <= 1): the engine's
+    own split (tfhe_shard_range, the one tfhe_setup(num_gpus) contexts use across devices)."""
+    import ctypes as C
+
+    from .capi import lib
+
     if world < 1 or not (0 <= rank < world):
         raise ValueError("bad world/rank")
-    base, extra = divmod(total, world)
-    lo = rank * base + min(rank, extra)
-    return lo, lo + base + (1 if rank < extra else 0)
+    lo, hi = C.c_size_t(), C.c_size_t()
+    if lib().tfhe_shard_range(total, world, rank, C.byref(lo), C.byref(hi)) != 0:
+        raise ValueError("bad world/rank")
+    return lo.value, hi.value
 
 
 def broadcast_key_image(image: torch.Tensor | None, nbytes: int | None, device, src: int = 0) -> torch.Tensor:
