@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend ('nccl' = RCCL; 'gloo' only to rehearse N ranks on fewer GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_pmc_blind_rotate.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_blind_rotate.json"))
     ap.add_argument("--valu-peak-json", default=os.path.join(ROOT, "profiles", "r03_valu_peak.json"))
     ap.add_argument("--no-host-array", action="store_true")
     return ap.parse_args()

@@ -23,8 +23,9 @@
  *
  * Conventions
  *  - All integers are u64, little-endian, flat row-major arrays in HOST memory
- *    unless the name ends in _device (then device pointers on the context's
- *    first device, ordered on the given hipStream_t, passed as void*).
+ *    unless the name ends in _device (then device pointers, ordered on the given
+ *    hipStream_t passed as void*; the call runs on the context's device that
+ *    holds the output buffer, found with hipPointerGetAttributes).
  *  - LWE ciphertext: [n+1] words, a[0..n-1] then b.
  *  - RLWE accumulator: [2][N] words, coefficient form.
  *  - BSK (coefficient form): [n][2][dG2][2][N]: LWE index i, ternary key
@@ -171,7 +172,10 @@ tfhe_status tfhe_eval_sign(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t
 tfhe_status tfhe_eval_decomp(tfhe_ctx* ctx, size_t B, const uint64_t* ct, uint64_t mod, uint32_t max_digits,
                              uint64_t* out, uint64_t* moduli, uint32_t* num_digits);
 
-/* ---- device-resident variants (inputs/outputs already in HBM of device 0) ---- */
+/* ---- device-resident variants (inputs/outputs already in HBM) ----
+ * The device is the one holding d_out / d_acc (a multi-device context runs the
+ * call on that device's key arena; the stream must belong to it).  A buffer on
+ * a device the context does not use is TFHE_ERR_INVALID_ARGUMENT. */
 tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* ctx, int gate, size_t B, const uint64_t* d_ct1,
                                       const uint64_t* d_ct2, uint64_t q, uint64_t* d_out, void* stream);
 tfhe_status tfhe_eval_acc_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_a, uint64_t a_mod, uint64_t* d_acc,

@@ -1,7 +1,10 @@
 """World-size-2 torch.distributed (gloo, CPU) tests of the multi-rank path:
 contiguous sharding, the key-image broadcast, max-over-ranks timing, and an
 end-to-end sharded batch (each rank bootstraps its shard with the CPU oracle,
-standing in for its GPU) that must equal the unsharded result."""
+standing in for its GPU) that must equal the unsharded result.  The split itself is
+the engine's own code: tfhe_shard_range across ranks, and inside each rank the
+host-thread runner of a multi-device context (tfhe_host_shard_selftest: the same
+run_shards the device calls use, with no GPU work), including its error path."""
 import os
 import socket
 import sys
@@ -48,6 +51,12 @@ def _worker(rank, world, port, outdir):
     c1 = np.stack([pyoracle.encrypt(p, rng, sk, i % 2, 4, p.q) for i in range(B)])
     c2 = np.stack([pyoracle.encrypt(p, rng, sk, (i // 2) % 2, 4, p.q) for i in range(B)])
     lo, hi = tdist.shard_range(B, world, rank)
+    # the engine's in-process split of this rank's shard over 2 devices (global spans)
+    BIG = 8191
+    blo, bhi = tdist.shard_range(BIG, world, rank)
+    dev_spans = [(blo + l, n) for l, n in tdist.device_shards(bhi - blo, 2)]
+    all_dev = [None] * world
+    dist.all_gather_object(all_dev, dev_spans)
     orc = pyoracle.Oracle(p, bsk, ksk, threads=1)
     part = orc.eval_bin_gate("NAND", c1[lo:hi], c2[lo:hi]) if hi > lo else np.zeros((0, p.n + 1), np.uint64)
     parts = [None] * world
@@ -60,6 +69,9 @@ def _worker(rank, world, port, outdir):
         np.save(os.path.join(outdir, "ref.npy"), ref)
         with open(os.path.join(outdir, "meta.txt"), "w") as f:
             f.write(f"{m} {total}\n")
+        spans = sorted(x for r in all_dev for x in r)
+        with open(os.path.join(outdir, "dev_spans.txt"), "w") as f:
+            f.write(" ".join(f"{l}:{n}" for l, n in spans) + f" total={BIG}\n")
     orc.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -88,3 +100,33 @@ def test_gloo_world2_broadcast_and_sharded_batch(tmp_path, oracle):
     m, total = open(tmp_path / "meta.txt").read().split()
     assert float(m) == 2.5 and int(total) == 5
     assert np.array_equal(np.load(tmp_path / "sharded.npy"), np.load(tmp_path / "ref.npy"))
+    # 4 device spans (2 ranks x 2 devices) partition the batch in order, sizes within 1
+    *parts, tot = open(tmp_path / "dev_spans.txt").read().split()
+    spans = [tuple(map(int, x.split(":"))) for x in parts]
+    assert int(tot.split("=")[1]) == sum(n for _, n in spans) == 8191
+    assert spans[0][0] == 0 and all(l + n == l2 for (l, n), (l2, _) in zip(spans, spans[1:]))
+    assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+
+
+def test_engine_device_split_and_error_propagation():
+    """The multi-device runner of a tfhe_setup(num_gpus) context (run_shards, one host thread
+    per device): contiguous balanced spans, a batch below 2 per device stays on device 0, and a
+    failing device's error comes back with its shard."""
+    sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+    from tfhe_amd.capi import TfheError
+    from tfhe_amd.dist import device_shards
+
+    for total in (0, 1, 5, 16, 8192, 65537):
+        for devices in (1, 2, 3, 8):
+            spans = device_shards(total, devices)
+            if devices == 1 or total < 2 * devices:
+                assert spans[0] == (0, total) and all(n == 0 for _, n in spans[1:])
+                continue
+            assert spans[0][0] == 0 and sum(n for _, n in spans) == total
+            assert all(l + n == l2 for (l, n), (l2, _) in zip(spans, spans[1:]))
+            assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+    with pytest.raises(TfheError, match=r"device 1: injected fault on shard \[10, 20\)"):
+        device_shards(30, 3, fail_device=1)
+    with pytest.raises(TfheError, match=r"device 7: injected fault on shard \[7168, 8192\)"):
+        device_shards(8192, 8, fail_device=7)
+    assert device_shards(30, 3, fail_device=5)[2] == (20, 10)  # no such device: no failure

@@ -100,7 +100,8 @@ struct Scratch {
     uint64_t* a = nullptr;    // [cap][n]
     uint64_t* ext = nullptr;  // [cap][N+1]
     uint64_t* lwe[6] = {};    // [cap][n+1] each
-    void* ks = nullptr;       // tiled key switch: digit planes (ks_tiled_scratch_bytes)
+    void* ks = nullptr;       // tiled key switch: digit planes (ks_tiled_scratch_bytes) for ks_cap
+    size_t ks_cap = 0;
     size_t cap = 0;
     uint64_t* io = nullptr;   // host-array staging: in1 | in2 | out
     size_t io_words = 0;
@@ -375,6 +376,25 @@ tfhe_status sc_release(Device& d, hipStream_t s) {
     return TFHE_OK;
 }
 
+// The context device holding device buffer p (the _device entry points' device index).
+tfhe_status device_for(tfhe_ctx* c, const void* p, Device*& out) {
+    if (c->devs.size() == 1) {  // nothing to choose: skip the query
+        out = &c->devs[0];
+        return TFHE_OK;
+    }
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(TFHE_ERR_INVALID_ARGUMENT, "not a device buffer");
+    }
+    for (Device& d : c->devs)
+        if (d.id == at.device) {
+            out = &d;
+            return TFHE_OK;
+        }
+    return fail(TFHE_ERR_INVALID_ARGUMENT, "buffer is on a device this context does not use");
+}
+
 tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     if (B <= d.sc.cap) return TFHE_OK;
     const tfhe_params& p = c->p;
@@ -393,8 +413,26 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     HCHECK(hipMalloc(&d.sc.a, cap * p.n * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.ext, cap * (p.N + 1) * sizeof(uint64_t)));
     for (auto*& q : d.sc.lwe) HCHECK(hipMalloc(&q, cap * (p.n + 1) * sizeof(uint64_t)));
-    if (ks_tiled_supported(c->ks)) HCHECK(hipMalloc(&d.sc.ks, ks_tiled_scratch_bytes(c->ks, cap)));
+    if (ks_tiled_supported(c->ks)) {
+        HCHECK(hipMalloc(&d.sc.ks, ks_tiled_scratch_bytes(c->ks, cap)));
+        d.sc.ks_cap = cap;
+    }
     d.sc.cap = cap;
+    return TFHE_OK;
+}
+
+size_t ks_tiled_min(int ksk_bits);
+
+// The tiled key switch's digit planes alone, for the device-resident key switch (which needs
+// none of the bootstrap scratch): grown to B only when the tiled form will run.
+tfhe_status ensure_ks_scratch(tfhe_ctx* c, Device& d, size_t B) {
+    const size_t tmin = ks_tiled_min(c->ksk_bits);
+    if (!ks_tiled_supported(c->ks) || tmin == 0 || B < tmin || B <= d.sc.ks_cap) return TFHE_OK;
+    if (d.sc_fence) HCHECK(hipEventSynchronize(d.sc_fence));
+    hipFree(d.sc.ks);
+    d.sc.ks = nullptr, d.sc.ks_cap = 0;
+    HCHECK(hipMalloc(&d.sc.ks, ks_tiled_scratch_bytes(c->ks, B)));
+    d.sc.ks_cap = B;
     return TFHE_OK;
 }
 
@@ -429,11 +467,11 @@ size_t ks_tiled_min(int ksk_bits) {
     return ksk_bits == 16 ? 4096 : 256;
 }
 
-// d.sc.ks must be sized for B (ensure_scratch) when the tiled form can run
+// the tiled form runs when d.sc.ks holds B ciphertexts (ensure_scratch / ensure_ks_scratch)
 tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
     if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
     const size_t tmin = ks_tiled_min(c->ksk_bits);
-    if (tmin && B >= tmin && d.sc.ks && B <= d.sc.cap) {
+    if (tmin && B >= tmin && d.sc.ks && B <= d.sc.ks_cap) {
         const hipError_t e = launch_ks_tiled(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb,
                                              ext, fmod, out, B, d.sc.ks, d.stream);
         if (e != hipErrorNotSupported) {
@@ -1232,7 +1270,11 @@ tfhe_status tfhe_eval_acc_device(tfhe_ctx* c, size_t B, const uint64_t* d_a, uin
                                  void* stream) {
     return guarded([&]() -> tfhe_status {
         SCHECK(check_ctx(c));
-        Device& d = c->devs[0];
+        if (B == 0) return TFHE_OK;
+        if (!d_a || !d_acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        Device* dp = nullptr;
+        SCHECK(device_for(c, d_acc, dp));
+        Device& d = *dp;
         HCHECK(hipSetDevice(d.id));
         hipStream_t saved = d.stream;
         if (stream) d.stream = (hipStream_t)stream;
@@ -1261,9 +1303,11 @@ tfhe_status tfhe_mkm_switch_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct_e
         SCHECK(check_ctx(c));
         if (B == 0) return TFHE_OK;
         if (!d_ct_ext || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-        Device& d = c->devs[0];
+        Device* dp = nullptr;
+        SCHECK(device_for(c, d_out, dp));
+        Device& d = *dp;
         HCHECK(hipSetDevice(d.id));
-        SCHECK(ensure_scratch(c, d, B));  // the tiled key switch's digit planes
+        SCHECK(ensure_ks_scratch(c, d, B));
         hipStream_t saved = d.stream;
         if (stream) d.stream = (hipStream_t)stream;
         tfhe_status st = sc_acquire(d, d.stream);
@@ -1297,7 +1341,9 @@ tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* c, int gate, size_t B, const uin
         if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
         if (B == 0) return TFHE_OK;
         if (!d_ct1 || !d_ct2 || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-        Device& d = c->devs[0];
+        Device* dp = nullptr;
+        SCHECK(device_for(c, d_out, dp));
+        Device& d = *dp;
         HCHECK(hipSetDevice(d.id));
         SCHECK(ensure_scratch(c, d, B));
         hipStream_t saved = d.stream;

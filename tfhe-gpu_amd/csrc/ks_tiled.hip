@@ -269,6 +269,10 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
                            uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s) {
     if (B == 0) return hipSuccess;
     if (!ks_tiled_supported(P)) return hipErrorNotSupported;
+    const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
+    // u16 keys sum in 32 bits: exact below 2^32, and wrapping mod 2^32 is harmless when qKS divides
+    // it; otherwise the gather form (k_mkm, 64-bit sums) serves the call
+    if (ksk_bits == 16 && !acc32 && (P.qKS & (P.qKS - 1)) != 0) return hipErrorNotSupported;
     const size_t Bp = ks_tiled_bp(B);
     uint32_t* dig = static_cast<uint32_t*>(scratch);
     uint64_t* bq = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)P.N * P.dKS * Bp);
@@ -278,7 +282,6 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     // every ciphertext tile of Bp gets digits (zeros past B), so k_ks_tiled reads no garbage
     const dim3 g1((unsigned)(Bp / DIG_TILE), (P.N + 1 + DIG_TILE - 1) / DIG_TILE);
     hipLaunchKernelGGL(k_ks_digits, g1, dim3(256), lds_dig, s, P, ext, dig, bq, B, Bp);
-    const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
     const char* ev = std::getenv("TFHE_KS_CTS");  // ciphertexts per thread (A/B runs)
     const int cts = ev ? std::atoi(ev) : 1;
     switch (ksk_bits) {

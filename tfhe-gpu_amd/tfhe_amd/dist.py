@@ -9,6 +9,8 @@ SURVEY.md 8(e)), so the only collectives are at setup and for timing:
   instead replicates keys host-to-device per GPU (bootstrapping.cu:1005-1069).
 * ``shard_range``: contiguous shards [g*B/G, (g+1)*B/G) (the reference deals
   SM_count-sized chunks round-robin, bootstrapping.cu:1617).
+* ``device_shards``: the engine's in-process split over the devices of one
+  tfhe_setup(num_gpus) context (one host thread per device).
 * ``max_over_ranks``: the bench's whole-job time is the slowest rank's.
 
 Everything here is backend-agnostic and is exercised on CPU with gloo
@@ -33,6 +35,20 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
     if lib().tfhe_shard_range(total, world, rank, C.byref(lo), C.byref(hi)) != 0:
         raise ValueError("bad world/rank")
     return lo.value, hi.value
+
+
+def device_shards(total: int, devices: int, fail_device: int = -1) -> list[tuple[int, int]]:
+    """(lo, count) per device of the engine's in-process split of `total` ciphertexts over
+    `devices` devices -- the host-thread runner a tfhe_setup(num_gpus) context uses
+    (tfhe_host_shard_selftest runs it with no GPU work).  fail_device >= 0 injects a failure on
+    that device's shard; the engine's error is raised as TfheError."""
+    import ctypes as C
+
+    from .capi import check, lib
+
+    spans = (C.c_size_t * (2 * devices))()
+    check(lib().tfhe_host_shard_selftest(total, devices, fail_device, spans), "tfhe_host_shard_selftest")
+    return [(spans[2 * g], spans[2 * g + 1]) for g in range(devices)]
 
 
 def broadcast_key_image(image: torch.Tensor | None, nbytes: int | None, device, src: int = 0) -> torch.Tensor:
