@@ -46,3 +46,14 @@ def test_wave_local_transform_schedule():
     out = run_tool("lds_layouts_wl.py")
     assert "wave-locality: passes B, C and the units stay in the wave's block" in out
     assert out.strip().endswith("OK"), out
+
+
+def test_fp64_kernel_bounds():
+    """f64w for Q near 2^50 (STD128Q): every sum and fmodmul operand of the forward transform
+    (one reduction), products, monomial factors, inverse (passes C and B reduce every output) and
+    accumulator update stays below 2^53 in the worst case; the round-2 inverse schedule did not."""
+    out = run_tool("bounds_f64.py")
+    assert out.strip().endswith("OK"), out
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bounds_f64.py"), "--round2"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "OVER 2^53" in r.stdout, r.stdout

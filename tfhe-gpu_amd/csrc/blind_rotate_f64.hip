@@ -204,7 +204,10 @@ __device__ __forceinline__ void f64_r8_fwd(double* p, const uint32_t (&ad)[8], u
     for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
 }
 
-// inverse GS stages h0, 2h0, 4h0 on the 8 elements at ad[]; g = block (8 h0 elements), m = N/(2h0)
+// inverse GS stages h0, 2h0, 4h0 on the 8 elements at ad[]; g = block (8 h0 elements), m = N/(2h0).
+// f64_r8_inv (RED) reduces all 8 outputs: with only the sums (k < 4) reduced, a later pass could
+// take 8 unreduced products (up to ~1.5 Q each for Q near 2^50) and sum past 2^53
+// (tools/bounds_f64.py walks the schedule element by element)
 __device__ __forceinline__ void f64_r8_inv_core(double (&v)[8], uint32_t m, uint32_t g, const double* ipsi,
                                                 const F64Const& K) {
     const double2 w0 = *(const double2*)(ipsi + m + 4 * g);
@@ -226,7 +229,7 @@ __device__ __forceinline__ void f64_r8_inv(double* p, const uint32_t (&ad)[8], u
     for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
     f64_r8_inv_core(v, m, g, ipsi, K);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) p[ad[k]] = (RED && k < 4) ? fred(v[k], K) : v[k];
+    for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
 }
 
 __device__ __forceinline__ void ad_A(uint32_t tau, uint32_t (&ad)[8]) {
@@ -607,6 +610,9 @@ __device__ __forceinline__ void f64w_sync() {
 // TO_LDS: the units' outputs stay in the buffer (slots 4u .. 4u+3 of the wave's block, read back
 // by the products of this wave) instead of registers
 // DELAY (fault probe, see k_blind_rotate_f64w): waves 1.. sleep between passes B and C
+// RED: one reduction, after pass B (stage 5): inputs |x| <= Q/2 (digits, C', the WRAP digit) stay
+// below 6.7 Q < 2^53 for every Q < 2^50 and leave at most 5.1 Q, which the products take as
+// fmodmul operands (tools/bounds_f64.py walks the worst case; round 2 reduced after every pass)
 template <bool RED, bool TO_LDS = false, bool DELAY = false>
 __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double (&d)[2][4], const double* psi,
                                              const F64Const& K) {
@@ -619,7 +625,7 @@ __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double
         ad_A(tau, ad);
         f64_r8_fwd_core(v, 1, 0, psi, K);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
+        for (int k = 0; k < 8; ++k) p[ad[k]] = v[k];
     }
     __syncthreads();
     uint32_t tw = (w << 5) | (l & 31);
@@ -638,7 +644,7 @@ __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double
     {
         uint32_t ad[8];
         ad_C(tw, ad);
-        f64_r8_fwd<RED>(p, ad, 64, tw >> 2, psi, K);
+        f64_r8_fwd<false>(p, ad, 64, tw >> 2, psi, K);
     }
     f64w_sync();
     const uint32_t u = (w << 6) | l, u0 = swz(4 * u);
@@ -650,7 +656,6 @@ __device__ __forceinline__ void f64w_ntt_fwd(double* buf, double (&v)[8], double
         double v0 = pq[u0], v1 = pq[u0 ^ 1], v2 = pq[u0 ^ 2], v3 = pq[u0 ^ 3];
         ct_bf(v0, v2, wa, K), ct_bf(v1, v3, wa, K);
         ct_bf(v0, v1, wb.x, K), ct_bf(v2, v3, wb.y, K);
-        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
         if constexpr (TO_LDS) {
             double* pw = buf + q * N;
             pw[u0] = v0, pw[u0 ^ 1] = v1, pw[u0 ^ 2] = v2, pw[u0 ^ 3] = v3;
@@ -703,11 +708,13 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
     f64_r8_inv_core(v, 4, 0, ipsi, K);
 }
 
-// FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64, MT:
-// monomial tables in LDS.  PROBE (fault probe, TFHE_F64W_PROBE; tests/test_gpu_f64w_race.py):
+// FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64.
+// MT (monomial factors psi^(+-e) - 1 of the lane's 4 slots): 0 gathers from the 2N-entry memory
+// table at each use, 1 two LDS table products at each use, 2 the 8 gathers issued once per round
+// before the products, 3 the LDS table products once per round (then one product per use).  PROBE (fault probe, TFHE_F64W_PROBE; tests/test_gpu_f64w_race.py):
 // bit 1 delays waves 1.. inside the prologue's C' transform (between passes B and C), bit 0
 // omits the barrier after it -- together they reproduce the round-0 race of the round-2 kernel
-template <bool RED, bool WRAP, int LD, bool MT, int PROBE = 0>
+template <bool RED, bool WRAP, int LD, int MT, int PROBE = 0>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
                     const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -731,20 +738,24 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const double* bsk = tabs + 2 * twoN;
     const uint64_t Qhalf = P.Q >> 1;
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
-    const uint32_t sh = 64 - logG;
+    // the accumulator is held centred in doubles, c in [Qhalf - Q, Qhalf) (rgsw-acc.cpp:80-110's
+    // signed representative), exact below 2^53; its digits are floors of exact power-of-two scalings
+    const double Qlo = (double)(int64_t)(Qhalf - P.Q), Qhi = (double)Qhalf;
+    const double Bg = (double)(1ull << logG), Bginv = 1.0 / Bg;
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     const size_t round_words = (size_t)4 * P.dG2 * N;
     // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
 
-    int64_t acc[2][CN];  // canonical [0, Q), pass A's layout
+    double acc[2][CN];  // centred [Qhalf - Q, Qhalf), pass A's layout
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
-            const uint64_t v = g[lpos(p, k)];
-            acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
+            uint64_t v = g[lpos(p, k)];
+            v = v >= P.Q ? v % P.Q : v;
+            acc[p][k] = (double)(v < Qhalf ? (int64_t)v : (int64_t)v - Qs);
         }
     if (WRAP && t < 2) wflag[t] = 0;
     uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n]
@@ -756,8 +767,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int k = 0; k < CN; ++k)
-                v[p * CN + k] = (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
+            for (int k = 0; k < CN; ++k) v[p * CN + k] = acc[p][k];
         double d[2][4];
         f64w_ntt_fwd<RED, false, (PROBE & 2) != 0>(buf, v, d, psi, K);
 #pragma unroll
@@ -770,9 +780,21 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     // wave that gets here first overwrites blocks other waves are still reading (the wrong
     // STD128Q / STD192 ciphertexts of round 2)
     if constexpr (!(PROBE & 1)) __syncthreads();
-    int64_t KdL = 0;  // WRAP: residual after all digits = (c + KdL) >> (L g)
-    for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
-    const uint32_t shiftL = P.digits * logG;
+    // digit l of c: low logG bits (signed) of (c + Kd_l) >> (l logG), Kd_l = sum_{z<l} Bh 2^(z logG)
+    // (the closed form of the reference's carries); WRAP: residual (c + KdL) >> (L logG)
+    double sl[LD + 1], kl[LD + 1];  // 2^-(l logG), Kd_l 2^-(l logG): exact
+    {
+        int64_t Kd = 0;
+        for (uint32_t l = 0; l <= (uint32_t)LD; ++l) {
+            const uint32_t shift = (l == (uint32_t)LD ? P.digits : l) * logG;
+            int64_t Kx = Kd;
+            if (l == (uint32_t)LD)
+                for (uint32_t z = l; z < P.digits; ++z) Kx = (Kx << logG) + Bh;
+            sl[l] = __builtin_ldexp(1.0, -(int)shift);
+            kl[l] = __dmul_rn((double)Kx, sl[l]);
+            Kd = (Kd << logG) + Bh;
+        }
+    }
 
     for (uint32_t i = 0; i < P.n; ++i) {
         // rotation exponent staged in LDS (no 64-bit remainder in the round loop)
@@ -782,23 +804,23 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
         auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4], bool sync) {
             constexpr bool CORR = decltype(corr_c)::value;
-            const uint32_t shift = l * logG;
-            int64_t Kd = 0;
-            for (uint32_t z = 0; z < l; ++z) Kd = (Kd << logG) + Bh;
             double v[8];
             bool wv = false;
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) {
-                    const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
+                    const double c = acc[p][k];
+                    // residual after all digits (WRAP): floor((c + KdL) 2^-(L logG))
+                    const double res = WRAP ? __builtin_floor(__fma_rn(c, sl[LD], kl[LD])) : 0.0;
                     if constexpr (CORR) {
-                        v[p * CN + k] = __dmul_rn((double)((c + KdL) >> shiftL), -K.wfac);
+                        v[p * CN + k] = __dmul_rn(res, -K.wfac);
                     } else {
-                        const int64_t dd = (c + Kd) >> shift;
-                        v[p * CN + k] = (double)(int32_t)((int64_t)((uint64_t)dd << sh) >> sh);  // |r| <= B/2
+                        const double f = l == 0 ? c : __builtin_floor(__fma_rn(c, sl[l], kl[l]));
+                        // signed low logG bits: f - B floor(f / B + 1/2), in [-B/2, B/2)
+                        v[p * CN + k] = __fma_rn(-Bg, __builtin_floor(__fma_rn(f, Bginv, 0.5)), f);
                     }
-                    if (WRAP && !CORR) wv |= ((c + KdL) >> shiftL) != 0;
+                    if (WRAP && !CORR) wv |= res != 0.0;
                 }
             if (WRAP && !CORR && l == 0) {
                 // round i - 1 read wflag[(i + 1) & 1] before its inverse barrier; round i + 1
@@ -849,6 +871,11 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         for (int q = 0; q < 4; ++q) ip[q] = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
         double S[2][4], A[2][4];
         double kv[2][4];
+        double Wp[4], Wm[4];  // MT 2/3: psi^e - 1, psi^-e - 1 at the 4 slots
+        if constexpr (MT == 2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Wp[q] = mono[ip[q]], Wm[q] = mono[(twoN - ip[q]) & (twoN - 1)];
+        }
         kload(0, kv[0]);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
@@ -868,7 +895,15 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t in = (twoN - ip[q]) & (twoN - 1);
                     double sv;
-                    if constexpr (MT) {
+                    if constexpr (MT >= 2) {
+                        if constexpr (MT == 3) {
+                            if (j == 0) {
+                                Wp[q] = __dsub_rn(fmodmul(mt[ip[q] >> 6], mt[64 + (ip[q] & 63)], K), 1.0);
+                                Wm[q] = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
+                            }
+                        }
+                        sv = fred(__dadd_rn(fmodmul(A[0][q], Wp[q], K), fmodmul(A[1][q], Wm[q], K)), K);
+                    } else if constexpr (MT == 1) {
                         auto mm = [&](double x, uint32_t e) {
                             return __dsub_rn(fmodmul(fmodmul(x, mt[e >> 6], K), mt[64 + (e & 63)], K), x);
                         };
@@ -888,18 +923,21 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
-                const double r = v[p * CN + k];  // |r| < 2^52
-                const double q = __builtin_rint(__dmul_rn(r, K.Qinv));
-                int64_t uu = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
-                uu = uu < 0 ? uu + Qs : uu;
-                acc[p][k] = uu >= Qs ? uu - Qs : uu;
+                // |r| < 2^52: c + r is exact; the reduction lands within 1 of [-Q/2, Q/2], and
+                // the two selects make it the centred representative exactly
+                double x = fred(__dadd_rn(acc[p][k], v[p * CN + k]), K);
+                x = x >= Qhi ? __dsub_rn(x, K.Q) : x;
+                acc[p][k] = x < Qlo ? __dadd_rn(x, K.Q) : x;
             }
     }
     __syncthreads();  // every last inverse pass has read its entries
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = __builtin_bit_cast(double, acc[p][k]);
+        for (int k = 0; k < CN; ++k) {
+            const int64_t c = (int64_t)acc[p][k];
+            buf[lpos(p, k)] = __builtin_bit_cast(double, (uint64_t)(c < 0 ? c + Qs : c));
+        }
     __syncthreads();
     for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
         const uint64_t v = __builtin_bit_cast(uint64_t, buf[k == 0 ? 0 : N - k]);
@@ -1036,25 +1074,29 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         const char* e = std::getenv("TFHE_F64W");
         return e && e[0] == '0';
     }();
-    const int mtw = [] {  // TFHE_F64W_MT=0: gathers from the memory table (read per launch)
+    const int mtw = [] {  // TFHE_F64W_MT=0..3 (k_blind_rotate_f64w's MT; read per launch)
         const char* e = std::getenv("TFHE_F64W_MT");
-        return e && e[0] ? e[0] - '0' : 2;
+        return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
     }();
     // f64w addresses the keys with 32-bit byte offsets (buffer resource)
     const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
     if (!no_w && fits32 && P.N == 2048 && fold && (P.digits == 2 || P.digits == 3)) {
-        const bool m = mtw != 0;  // tables: STD192 474 -> 385 ms, STD128Q 319 -> 288 ms (profiles/r02ae)
+        // MT 1 (tables) against 0 (gathers): STD192 474 -> 385 ms, STD128Q 319 -> 288 ms (profiles/r02ae);
+        // 3 against 1: 323 -> 315 ms, 254 -> 245 ms; 2 (gathers once per round): 357 / 292 ms (profiles/r03i)
         const int ld = (int)P.digits - 1;
 #define F64W_GO(R, W, L)                                                                     \
-    (m ? go(k_blind_rotate_f64w<R, W, L, true>) : go(k_blind_rotate_f64w<R, W, L, false>))
+    (mtw == 0   ? go(k_blind_rotate_f64w<R, W, L, 0>)                                         \
+     : mtw == 1 ? go(k_blind_rotate_f64w<R, W, L, 1>)                                         \
+     : mtw == 2 ? go(k_blind_rotate_f64w<R, W, L, 2>)                                         \
+                : go(k_blind_rotate_f64w<R, W, L, 3>))
         const int probe = [] {  // fault probe, read per launch (tests/test_gpu_f64w_race.py)
             const char* e = std::getenv("TFHE_F64W_PROBE");
             return e && e[0] ? e[0] - '0' : 0;
         }();
         if (probe != 0) {  // STD128Q's instance only
-            if (!(red && wrap && ld == 1 && m)) return hipErrorInvalidValue;
-            if (probe == 2) go(k_blind_rotate_f64w<true, true, 1, true, 2>);
-            else if (probe == 3) go(k_blind_rotate_f64w<true, true, 1, true, 3>);
+            if (!(red && wrap && ld == 1 && mtw == 3)) return hipErrorInvalidValue;
+            if (probe == 2) go(k_blind_rotate_f64w<true, true, 1, 3, 2>);
+            else if (probe == 3) go(k_blind_rotate_f64w<true, true, 1, 3, 3>);
             else return hipErrorInvalidValue;
             return hipGetLastError();
         }
