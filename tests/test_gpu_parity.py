@@ -593,3 +593,27 @@ def test_custom_modulus_n1024_f64_parity(capi, oracle, bits, baseG_log):
     assert np.array_equal(ctx.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
     ctx.GPUClean()
     orc.close()
+
+
+def test_host_array_unreduced_inputs_take_the_wide_wire(capi, oracle):
+    """The host-array runner sends arrays in u16 / u32 words when their modulus allows (engine.hip
+    h2d_staged); an unreduced input (a >= a_mod, acc >= Q -- the kernels reduce both) must fall
+    back to u64 and give the same result as the reduced one."""
+    op = oracle.params_from_set("STD128")
+    cp = capi.params_from_set("STD128")
+    rs = np.random.default_rng(41)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+    B, amod = 6, op.q
+    a = rs.integers(0, amod, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    want = orc.eval_acc(a, amod, acc)
+    assert np.array_equal(ctx.EvalAcc(a, amod, acc), want)
+    a_big = a + np.uint64(amod) * rs.integers(1, 1 << 40, (B, op.n), dtype=np.uint64)
+    acc_big = acc + np.uint64(op.Q) * rs.integers(0, 1 << 30, (B, 2, op.N), dtype=np.uint64)
+    assert np.array_equal(ctx.EvalAcc(a_big, amod, acc_big), want)
+    ext = rs.integers(0, op.Q, (B, op.N + 1), dtype=np.uint64)
+    assert np.array_equal(ctx.MKMSwitch(ext, op.q), orc.mkm_switch(ext, op.q))
+    ctx.GPUClean()
+    orc.close()

@@ -105,6 +105,8 @@ struct Scratch {
     size_t cap = 0;
     uint64_t* io = nullptr;   // host-array staging: in1 | in2 | out
     size_t io_words = 0;
+    void* pk = nullptr;       // the same arrays in the narrow wire format (u16 / u32 words)
+    size_t pk_bytes = 0;
 };
 
 // A device has a compute stream (`stream`, scratch `sc`) and a copy stream (`stream2`):
@@ -346,6 +348,7 @@ void free_device(Device& d) {
         for (auto* p : sc->lwe) hipFree(p);
         hipFree(sc->ks);
         hipFree(sc->io);
+        hipFree(sc->pk);
     }
     for (int k = 0; k < 2; ++k) {
         if (d.pin_ev[k]) hipEventSynchronize(d.pin_ev[k]), hipEventDestroy(d.pin_ev[k]);
@@ -407,8 +410,10 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     hipFree(d.sc.ks);
     uint64_t* io = d.sc.io;
     const size_t io_words = d.sc.io_words;
+    void* pk = d.sc.pk;
+    const size_t pk_bytes = d.sc.pk_bytes;
     d.sc = Scratch{};
-    d.sc.io = io, d.sc.io_words = io_words;
+    d.sc.io = io, d.sc.io_words = io_words, d.sc.pk = pk, d.sc.pk_bytes = pk_bytes;
     HCHECK(hipMalloc(&d.sc.acc, cap * 2 * p.N * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.a, cap * p.n * sizeof(uint64_t)));
     HCHECK(hipMalloc(&d.sc.ext, cap * (p.N + 1) * sizeof(uint64_t)));
@@ -691,37 +696,59 @@ tfhe_status ensure_pinned(Device& d) {
     }
     return TFHE_OK;
 }
-tfhe_status h2d_staged(Device& d, void* dst, const void* src, size_t bytes, hipStream_t s) {
+// words u64 host -> device through the pinned blocks; wb < 8: the narrow wire format -- the host
+// pool narrows each block into pinned memory, the DMA moves wb bytes per word into `pk` (device),
+// and one kernel widens pk into dst.  wb is the caller's guess from the array's modulus; a value
+// that does not fit (an unreduced input) sends the whole array again as u64.
+tfhe_status h2d_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t words, hipStream_t s, int wb = 8,
+                       void* pk = nullptr) {
     SCHECK(ensure_pinned(d));
-    for (size_t off = 0, k = 0; off < bytes; off += kStageBytes, ++k) {
+    const size_t per = kStageBytes / wb;  // words per block
+    uint64_t seen = 0;
+    for (size_t off = 0, k = 0; off < words; off += per, ++k) {
         const int slot = (int)(k & 1);
-        const size_t blk = std::min(kStageBytes, bytes - off);
+        const size_t nw = std::min(per, words - off);
         HCHECK(hipEventSynchronize(d.pin_ev[slot]));  // the DMA that last read this block is done
-        parallel_memcpy(d.pin[slot], (const char*)src + off, blk);
-        HCHECK(hipMemcpyAsync((char*)dst + off, d.pin[slot], blk, hipMemcpyHostToDevice, s));
+        if (wb == 8) {
+            parallel_memcpy(d.pin[slot], src + off, nw * 8);
+            HCHECK(hipMemcpyAsync(dst + off, d.pin[slot], nw * 8, hipMemcpyHostToDevice, s));
+        } else {
+            seen |= parallel_narrow(d.pin[slot], src + off, nw, wb);
+            HCHECK(hipMemcpyAsync((char*)pk + off * wb, d.pin[slot], nw * wb, hipMemcpyHostToDevice, s));
+        }
         HCHECK(hipEventRecord(d.pin_ev[slot], s));
     }
+    if (wb == 8) return TFHE_OK;
+    if (seen >> (8 * wb)) return h2d_staged(d, dst, src, words, s);
+    HCHECK(launch_widen(pk, wb, dst, words, s));
     return TFHE_OK;
 }
-tfhe_status d2h_staged(Device& d, void* dst, const void* src, size_t bytes, hipStream_t s) {
+// words u64 device -> host; wb < 8 (every value below 2^(8 wb)): one kernel narrows src into pk,
+// the DMA moves wb bytes per word, the host pool widens each block into dst
+tfhe_status d2h_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t words, hipStream_t s, int wb = 8,
+                       void* pk = nullptr) {
     SCHECK(ensure_pinned(d));
-    size_t prev_off = 0, prev_blk = 0;
-    for (size_t off = 0, k = 0;; off += kStageBytes, ++k) {
+    if (wb != 8) HCHECK(launch_narrow(src, wb, pk, words, s));
+    const char* from = wb == 8 ? (const char*)src : (const char*)pk;
+    const size_t per = kStageBytes / wb;
+    size_t prev_off = 0, prev_nw = 0;
+    for (size_t off = 0, k = 0;; off += per, ++k) {
         const int slot = (int)(k & 1);
-        const bool more = off < bytes;
-        const size_t blk = more ? std::min(kStageBytes, bytes - off) : 0;
+        const bool more = off < words;
+        const size_t nw = more ? std::min(per, words - off) : 0;
         if (more) {
             HCHECK(hipEventSynchronize(d.pin_ev[slot]));
-            HCHECK(hipMemcpyAsync(d.pin[slot], (const char*)src + off, blk, hipMemcpyDeviceToHost, s));
+            HCHECK(hipMemcpyAsync(d.pin[slot], from + off * wb, nw * wb, hipMemcpyDeviceToHost, s));
             HCHECK(hipEventRecord(d.pin_ev[slot], s));
         }
         if (k > 0) {  // drain the previous block while this one is in flight
             const int ps = (int)((k - 1) & 1);
             HCHECK(hipEventSynchronize(d.pin_ev[ps]));
-            parallel_memcpy((char*)dst + prev_off, d.pin[ps], prev_blk);
+            if (wb == 8) parallel_memcpy(dst + prev_off, d.pin[ps], prev_nw * 8);
+            else parallel_widen(dst + prev_off, d.pin[ps], prev_nw, wb);
         }
         if (!more) break;
-        prev_off = off, prev_blk = blk;
+        prev_off = off, prev_nw = nw;
     }
     return TFHE_OK;
 }
@@ -746,32 +773,59 @@ size_t host_parts(size_t cnt) {
     return std::min(want, std::max<size_t>(1, cnt / 256));
 }
 
-tfhe_status ensure_io_set(Scratch& sc, size_t words) {
-    if (words <= sc.io_words) return TFHE_OK;
-    hipFree(sc.io);
-    sc.io = nullptr, sc.io_words = 0;
-    HCHECK(hipMalloc(&sc.io, words * sizeof(uint64_t)));
-    sc.io_words = words;
+tfhe_status ensure_io_set(Scratch& sc, size_t words, size_t pk_bytes) {
+    if (words > sc.io_words) {
+        hipFree(sc.io);
+        sc.io = nullptr, sc.io_words = 0;
+        HCHECK(hipMalloc(&sc.io, words * sizeof(uint64_t)));
+        sc.io_words = words;
+    }
+    if (pk_bytes > sc.pk_bytes) {
+        hipFree(sc.pk);
+        sc.pk = nullptr, sc.pk_bytes = 0;
+        HCHECK(hipMalloc(&sc.pk, pk_bytes));
+        sc.pk_bytes = pk_bytes;
+    }
     return TFHE_OK;
 }
 
+// PCIe wire width of an array: the narrowest of u16 / u32 / u64 that holds every value (inputs:
+// the OR of the words; outputs: the op's bound).  TFHE_WIRE=0 keeps u64 (A/B runs; read per call).
+bool wire_narrowing() {
+    const char* e = std::getenv("TFHE_WIRE");
+    return !(e && e[0] == '0');
+}
+
+// Value bounds of the runner's arrays (0: unknown): an array crosses PCIe in the narrowest of u16 /
+// u32 / u64 that holds its bound (h2d_staged / d2h_staged).  Inputs are checked as they are packed
+// (an unreduced input goes again as u64); outputs must respect their bound (the op's modulus).
+struct WireLim {
+    uint64_t in1 = 0, in2 = 0, out_in = 0, out = 0;
+};
+
 // out_in: the output rows' initial contents (uploaded into the output set before the kernels of
-// their sub-batch, for ops that work in place on the output, e.g. the blind rotation)
+// their sub-batch, for ops that work in place on the output, e.g. the blind rotation).
 template <typename Op>
 tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
-                          uint64_t* out, size_t wo, Op&& op, const uint64_t* out_in = nullptr) {
+                          uint64_t* out, size_t wo, Op&& op, WireLim wl, const uint64_t* out_in = nullptr) {
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
         const size_t parts = host_parts(cnt);
         const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
         const size_t w_in2 = in2 ? w2 : 0, io_words = sub * (w1 + w_in2 + wo);
+        const bool nar = wire_narrowing();
+        auto width = [nar](uint64_t lim) { return nar && lim ? wire_bytes(lim - 1) : 8; };
+        const int wb1 = width(wl.in1), wb2 = in2 ? width(wl.in2) : 8, wbi = out_in ? width(wl.out_in) : 8;
+        const int wbo = width(wl.out);
+        const size_t pk1 = sub * w1 * wb1, pk2 = sub * w_in2 * wb2, pko = sub * wo * std::max(wbi, wbo);
         SCHECK(ensure_scratch(c, d, sub));
-        SCHECK(ensure_io_set(d.sc, io_words));
-        SCHECK(ensure_io_set(d.sc2, io_words));
+        SCHECK(ensure_io_set(d.sc, io_words, pk1 + pk2 + pko));
+        SCHECK(ensure_io_set(d.sc2, io_words, pk1 + pk2 + pko));
         for (hipEvent_t* e : {&d.h2d_ev[0], &d.h2d_ev[1], &d.k_ev[0], &d.k_ev[1]})
             if (!*e) HCHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         SCHECK(sc_acquire(d, d.stream));
         const hipStream_t cs = d.stream, xs = d.stream2;
         uint64_t* io[2] = {d.sc.io, d.sc2.io};
+        char* pk[2] = {(char*)d.sc.pk, (char*)d.sc2.pk};
         static const bool trace = std::getenv("TFHE_TRACE") != nullptr;
         auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double t0 = trace ? now() : 0;
@@ -781,7 +835,7 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
             const int set = (int)(k & 1);
             HCHECK(hipStreamWaitEvent(xs, d.k_ev[set], 0));
-            return d2h_staged(d, out + off * wo, dout_of(set), b * wo * 8, xs);
+            return d2h_staged(d, out + off * wo, dout_of(set), b * wo, xs, wbo, pk[set] + pk1 + pk2);
         };
         tfhe_status st = TFHE_OK;
         const size_t n_sub = (cnt + sub - 1) / sub;
@@ -789,10 +843,13 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
             const int set = (int)(k & 1);
             uint64_t *din1 = io[set], *din2 = in2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
-            st = h2d_staged(d, din1, in1 + off * w1, b * w1 * 8, xs);
-            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2 * 8, xs);
-            if (st == TFHE_OK && out_in) st = h2d_staged(d, dout, out_in + off * wo, b * wo * 8, xs);
+            st = h2d_staged(d, din1, in1 + off * w1, b * w1, xs, wb1, pk[set]);
+            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2, xs, wb2, pk[set] + pk1);
+            if (st == TFHE_OK && out_in)
+                st = h2d_staged(d, dout, out_in + off * wo, b * wo, xs, wbi, pk[set] + pk1 + pk2);
             if (st != TFHE_OK) break;
+            if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu inputs staged at %.2f ms (wire %d/%d/%d/%d B)\n", k,
+                                    now() - t0, wb1, wb2, wbi, wbo);
             // no early return below this point: both streams are synchronised before returning
             if (hipEventRecord(d.h2d_ev[set], xs) != hipSuccess || hipStreamWaitEvent(cs, d.h2d_ev[set], 0) != hipSuccess) {
                 st = fail(TFHE_ERR_DEVICE, "host batch: event ordering failed");
@@ -807,7 +864,13 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu queued at %.2f ms\n", k, now() - t0);
             if (k > 0) st = d2h(k - 1);
         }
-        if (st == TFHE_OK && n_sub > 0) st = d2h(n_sub - 1);
+        if (st == TFHE_OK && n_sub > 0) {
+            if (trace) {
+                HCHECK(hipStreamSynchronize(cs));
+                std::fprintf(stderr, "[tfhe] last sub-batch's kernels done at %.2f ms\n", now() - t0);
+            }
+            st = d2h(n_sub - 1);
+        }
         const hipError_t e1 = hipStreamSynchronize(cs), e2 = hipStreamSynchronize(xs);
         if (trace) std::fprintf(stderr, "[tfhe] host batch %zu in %zu sub-batches: done %.2f ms\n", cnt, n_sub, now() - t0);
         if (st == TFHE_OK && (e1 != hipSuccess || e2 != hipSuccess))
@@ -1213,39 +1276,13 @@ tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_m
         if (!a || !acc) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
         const tfhe_params& p = c->p;
         const size_t wacc = 2 * (size_t)p.N;
-        // TFHE_EVAL_ACC_PATH (read per call): "legacy" = pageable copies on the compute stream;
-        // "d2d" = the pinned runner with a device copy into the output set; default "inplace" = the
-        // pinned runner, accumulators uploaded straight into the output set and rotated there
-        const char* e = std::getenv("TFHE_EVAL_ACC_PATH");
-        const std::string path = e && e[0] ? e : "inplace";
-        if (path == "legacy") {
-            return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-                const size_t chunk = std::min(cnt, c->max_chunk);
-                SCHECK(ensure_scratch(c, d, chunk));
-                SCHECK(sc_acquire(d, d.stream));
-                for (size_t off = lo; off < lo + cnt; off += chunk) {
-                    const size_t b = std::min(chunk, lo + cnt - off);
-                    HCHECK(hipMemcpyAsync(d.sc.a, a + off * p.n, b * p.n * 8, hipMemcpyHostToDevice, d.stream));
-                    HCHECK(hipMemcpyAsync(d.sc.acc, acc + off * wacc, b * wacc * 8, hipMemcpyHostToDevice, d.stream));
-                    SCHECK(dev_blind_rotate(c, d, d.sc.a, a_mod, d.sc.acc, b));
-                    HCHECK(hipMemcpyAsync(acc + off * wacc, d.sc.acc, b * wacc * 8, hipMemcpyDeviceToHost, d.stream));
-                    HCHECK(hipStreamSynchronize(d.stream));
-                }
-                return TFHE_OK;
-            });
-        }
-        if (path == "d2d")
-            return run_lwe_batch(c, B, a, p.n, acc, wacc, acc, wacc,
-                                 [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
-                                     HCHECK(hipMemcpyAsync(o, i2, b * wacc * 8, hipMemcpyDeviceToDevice, d.stream));
-                                     return dev_blind_rotate(c, d, i1, a_mod, o, b);
-                                 });
+        // the accumulators go straight into the output set and are rotated there
         return run_lwe_batch(
             c, B, a, p.n, nullptr, 0, acc, wacc,
             [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                 return dev_blind_rotate(c, d, i1, a_mod, o, b);
             },
-            acc);
+            WireLim{a_mod, 0, p.Q, p.Q}, acc);
     });
 }
 
@@ -1262,7 +1299,8 @@ tfhe_status tfhe_eval_acc_tv(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t 
                              [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
                                  HCHECK(launch_expand_tv(p.N, tv_len, i2, o, b, d.stream));
                                  return dev_blind_rotate(c, d, i1, a_mod, o, b);
-                             });
+                             },
+                             WireLim{a_mod, p.Q, 0, p.Q});
     });
 }
 
@@ -1293,7 +1331,8 @@ tfhe_status tfhe_mkm_switch(tfhe_ctx* c, size_t B, const uint64_t* ct_ext, uint6
         return run_lwe_batch(c, B, ct_ext, p.N + 1, nullptr, 0, out, p.n + 1,
                              [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                                  return dev_mkm(c, d, i1, fmod, o, b);
-                             });
+                             },
+                             WireLim{p.Q, 0, 0, fmod});
     });
 }
 
@@ -1330,7 +1369,8 @@ tfhe_status tfhe_eval_bin_gate(tfhe_ctx* c, int gate, size_t B, const uint64_t* 
         return run_lwe_batch(c, B, ct1, w, ct2, w, out, w,
                              [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
                                  return dev_gate(c, d, gate, i1, i2, q, o, b);
-                             });
+                             },
+                             WireLim{q, q, 0, q});
     });
 }
 
@@ -1384,7 +1424,8 @@ tfhe_status tfhe_eval_func(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t q
                                    size_t g = 0;
                                    while (c->devs[g].id != d.id) ++g;
                                    return dev_func(c, d, prop, i1, q, d_lut[g] + (per_ct_lut ? off * q : 0), stride, o, b);
-                               });
+                               },
+                               WireLim{q, 0, 0, 0});
         for (size_t g = 0; g < D; ++g)
             if (d_lut[g]) hipSetDevice(c->devs[g].id), hipFree(d_lut[g]);
         return st;
@@ -1401,7 +1442,8 @@ tfhe_status tfhe_eval_floor(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t 
         return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
                              [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                                  return dev_floor(c, d, i1, mod, roundbits, o, b);
-                             });
+                             },
+                             WireLim{mod, 0, 0, 0});
     });
 }
 
@@ -1414,7 +1456,8 @@ tfhe_status tfhe_eval_sign(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t m
         return run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
                              [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                                  return dev_sign(c, d, i1, mod, o, b);
-                             });
+                             },
+                             WireLim{mod, 0, 0, 0});
     });
 }
 
@@ -1571,6 +1614,21 @@ tfhe_status tfhe_host_selftest(const tfhe_params* pin) {
             const uint64_t qt = (uint64_t)(((u128)aa * wp) >> wb);
             const uint64_t r = (uint64_t)(((u128)aa * w - (u128)qt * p.Q) % R) & mask;
             if (r >= 2 * p.Q || r % p.Q != mulmod(aa % p.Q, w, p.Q)) return fail(TFHE_ERR_INTERNAL, "Shoup bound");
+        }
+        // (5) the narrow PCIe wire format's host side (pool jobs above and below the 1 MiB cut)
+        for (size_t n : {(size_t)1000, (size_t)3 << 17}) {
+            std::vector<uint64_t> src(n), back(n, ~0ull);
+            for (size_t i = 0; i < n; ++i) src[i] = (i * 2654435761u) & 0xFFFFFFFFu;
+            if (parallel_or(src.data(), n) >> 32 || wire_bytes(parallel_or(src.data(), n)) != 4)
+                return fail(TFHE_ERR_INTERNAL, "wire width");
+            for (int wb : {2, 4}) {
+                std::vector<uint8_t> packed(n * wb);
+                parallel_narrow(packed.data(), src.data(), n, wb);
+                parallel_widen(back.data(), packed.data(), n, wb);
+                const uint64_t mask = wb == 2 ? 0xFFFFu : 0xFFFFFFFFu;
+                for (size_t i = 0; i < n; ++i)
+                    if (back[i] != (src[i] & mask)) return fail(TFHE_ERR_INTERNAL, "wire narrow/widen");
+            }
         }
         return TFHE_OK;
     });

@@ -7,30 +7,30 @@
 #include <unordered_map>
 
 #include <condition_variable>
-#include <cstring>
+#include <functional>
 #include <mutex>
 
 namespace tfhe {
 
 namespace {
-struct CopyPool {
+// One job at a time over [0, n): worker w takes the w-th of T equal ranges.
+struct HostPool {
     std::mutex call, m;
     std::condition_variable cv, done_cv;
     std::vector<std::thread> workers;
     unsigned T = 0;
     uint64_t gen = 0;
     unsigned pending = 0;
-    char* dst = nullptr;
-    const char* src = nullptr;
-    size_t bytes = 0;
-    CopyPool() {
+    size_t n = 0;
+    const std::function<void(size_t, size_t)>* job = nullptr;
+    HostPool() {
         T = host_threads();
         for (unsigned w = 1; w < T; ++w) workers.emplace_back([this, w] { loop(w); });
         for (auto& t : workers) t.detach();
     }
     void piece(unsigned w) {
-        const size_t per = (bytes + T - 1) / T, lo = std::min(bytes, w * per), hi = std::min(bytes, lo + per);
-        if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+        const size_t per = (n + T - 1) / T, lo = std::min(n, w * per), hi = std::min(n, lo + per);
+        if (hi > lo) (*job)(lo, hi);
     }
     void loop(unsigned w) {
         uint64_t seen = 0;
@@ -45,15 +45,11 @@ struct CopyPool {
             if (--pending == 0) done_cv.notify_one();
         }
     }
-    void run(void* d, const void* s2, size_t n) {
+    void run(size_t count, const std::function<void(size_t, size_t)>& fn) {
         std::lock_guard<std::mutex> one(call);
-        if (T <= 1 || n < (1u << 20)) {
-            std::memcpy(d, s2, n);
-            return;
-        }
         {
             std::lock_guard<std::mutex> lk(m);
-            dst = (char*)d, src = (const char*)s2, bytes = n;
+            n = count, job = &fn;
             pending = T - 1;
             ++gen;
         }
@@ -63,11 +59,58 @@ struct CopyPool {
         done_cv.wait(lk, [&] { return pending == 0; });
     }
 };
+
+// jobs below ~1 MiB of traffic run on the calling thread
+void pool_run(size_t n, size_t bytes, const std::function<void(size_t, size_t)>& fn) {
+    static HostPool* pool = new HostPool();  // intentionally leaked: workers are detached
+    if (pool->T <= 1 || bytes < (1u << 20)) {
+        if (n) fn(0, n);
+        return;
+    }
+    pool->run(n, fn);
+}
 }  // namespace
 
 void parallel_memcpy(void* dst, const void* src, size_t bytes) {
-    static CopyPool* pool = new CopyPool();  // intentionally leaked: workers are detached
-    pool->run(dst, src, bytes);
+    pool_run(bytes, bytes, [&](size_t lo, size_t hi) { std::memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
+}
+
+uint64_t parallel_or(const uint64_t* src, size_t n) {
+    std::atomic<uint64_t> acc{0};
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        uint64_t o = 0;
+        for (size_t i = lo; i < hi; ++i) o |= src[i];
+        acc.fetch_or(o, std::memory_order_relaxed);
+    });
+    return acc.load();
+}
+
+uint64_t parallel_narrow(void* dst, const uint64_t* src, size_t n, int wb) {
+    std::atomic<uint64_t> acc{0};
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        uint64_t o = 0;
+        if (wb == 2) {
+            uint16_t* d = (uint16_t*)dst;
+            for (size_t i = lo; i < hi; ++i) o |= src[i], d[i] = (uint16_t)src[i];
+        } else {
+            uint32_t* d = (uint32_t*)dst;
+            for (size_t i = lo; i < hi; ++i) o |= src[i], d[i] = (uint32_t)src[i];
+        }
+        acc.fetch_or(o, std::memory_order_relaxed);
+    });
+    return acc.load();
+}
+
+void parallel_widen(uint64_t* dst, const void* src, size_t n, int wb) {
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        if (wb == 2) {
+            const uint16_t* s = (const uint16_t*)src;
+            for (size_t i = lo; i < hi; ++i) dst[i] = s[i];
+        } else {
+            const uint32_t* s = (const uint32_t*)src;
+            for (size_t i = lo; i < hi; ++i) dst[i] = s[i];
+        }
+    });
 }
 
 

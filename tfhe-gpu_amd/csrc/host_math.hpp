@@ -48,6 +48,14 @@ void parallel_for(size_t n, F&& f) {
 // creating threads per 8 MiB block would cost as much as the copy.  Thread-safe (one
 // copy at a time); workers are created on first use and live until process exit.
 void parallel_memcpy(void* dst, const void* src, size_t bytes);
+// On the same pool: OR of n words, and the host side of the narrow PCIe wire format: u64 <-> u16 /
+// u32 (wb = 2 or 4 bytes per word); parallel_narrow returns the OR of the words it narrowed (the
+// caller falls back to u64 when a value did not fit).
+uint64_t parallel_or(const uint64_t* src, size_t n);
+uint64_t parallel_narrow(void* dst, const uint64_t* src, size_t n, int wb);
+void parallel_widen(uint64_t* dst, const void* src, size_t n, int wb);
+// Wire bytes per word for values below 2^bits(max_or): 2, 4 or 8.
+inline int wire_bytes(uint64_t max_or) { return max_or < (1ull << 16) ? 2 : (max_or < (1ull << 32) ? 4 : 8); }
 
 using u128 = unsigned __int128;
 

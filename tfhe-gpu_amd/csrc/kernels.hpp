@@ -123,6 +123,9 @@ hipError_t launch_build_testvector(const TvParams& P, const uint64_t* ct, uint64
                                    hipStream_t s);
 // tv[B][tvlen] -> acc[B][2][N]: acc0 = 0, acc1[j * (N / tvlen)] = tv[j], other coefficients 0
 hipError_t launch_expand_tv(uint32_t N, uint32_t tvlen, const uint64_t* tv, uint64_t* acc, size_t B, hipStream_t s);
+// u16 / u32 (wb = 2 / 4 bytes) <-> u64 words: the narrow PCIe wire format of the host-array runner
+hipError_t launch_widen(const void* src, int wb, uint64_t* dst, size_t n, hipStream_t s);
+hipError_t launch_narrow(const uint64_t* src, int wb, void* dst, size_t n, hipStream_t s);
 // acc[B][2][N] (acc0 transposed) -> ext[B][N+1]: a = acc0, b = acc1[0] + b_add mod Q
 hipError_t launch_extract(uint32_t N, uint64_t Q, uint64_t b_add, const uint64_t* acc, uint64_t* ext, size_t B,
                           hipStream_t s);

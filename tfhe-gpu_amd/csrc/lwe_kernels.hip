@@ -243,6 +243,34 @@ hipError_t launch_expand_tv(uint32_t N, uint32_t tvlen, const uint64_t* tv, uint
     return hipGetLastError();
 }
 
+// Narrow PCIe wire format of the host-array runner: u64 words <-> u16 / u32 (engine.hip)
+template <typename W>
+__global__ void k_widen(const W* __restrict__ src, uint64_t* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+template <typename W>
+__global__ void k_narrow(const uint64_t* __restrict__ src, W* __restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = (W)src[i];
+}
+hipError_t launch_widen(const void* src, int wb, uint64_t* dst, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    if (wb == 2) hipLaunchKernelGGL(k_widen<uint16_t>, dim3(g), dim3(256), 0, s, (const uint16_t*)src, dst, n);
+    else if (wb == 4) hipLaunchKernelGGL(k_widen<uint32_t>, dim3(g), dim3(256), 0, s, (const uint32_t*)src, dst, n);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+hipError_t launch_narrow(const uint64_t* src, int wb, void* dst, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    if (wb == 2) hipLaunchKernelGGL(k_narrow<uint16_t>, dim3(g), dim3(256), 0, s, src, (uint16_t*)dst, n);
+    else if (wb == 4) hipLaunchKernelGGL(k_narrow<uint32_t>, dim3(g), dim3(256), 0, s, src, (uint32_t*)dst, n);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // LWE glue, element-wise over [B][n+1]
 // ---------------------------------------------------------------------------
