@@ -52,7 +52,8 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 3  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding */
+#define TFHE_HIP_ABI_VERSION 4  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
+                                   4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows) */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -152,6 +153,17 @@ tfhe_status tfhe_eval_acc_tv(tfhe_ctx* ctx, size_t B, const uint64_t* a, uint64_
                              uint32_t tv_len, uint64_t* acc);
 /* ct_ext[B][N+1] mod Q -> out[B][n+1] mod fmod: ModSwitch(qKS), KeySwitch, ModSwitch(fmod) */
 tfhe_status tfhe_mkm_switch(tfhe_ctx* ctx, size_t B, const uint64_t* ct_ext, uint64_t fmod, uint64_t* out);
+/* Row-pointer forms of the two calls above, for callers whose ciphertexts live in separate
+ * allocations (OpenFHE: one NativeVector per polynomial and per LWE "a", which the drop-in shim
+ * passes as pointers to their u64 storage): the pinned PCIe staging reads and writes the rows where
+ * they are, so no flat copy of the arrays exists on either side.  Same results as the flat calls.
+ *   tfhe_eval_acc_tv_rows: a_rows[s] -> n words; tv[B][tv_len] flat; acc_rows[2s + j] -> polynomial
+ *                          j (N words) of accumulator s (written, acc0 transposed)
+ *   tfhe_mkm_switch_rows:  ext_a_rows[s] -> N words, ext_b[s]; out_a_rows[s] -> n words, out_b[s] */
+tfhe_status tfhe_eval_acc_tv_rows(tfhe_ctx* ctx, size_t B, const uint64_t* const* a_rows, uint64_t a_mod,
+                                  const uint64_t* tv, uint32_t tv_len, uint64_t* const* acc_rows);
+tfhe_status tfhe_mkm_switch_rows(tfhe_ctx* ctx, size_t B, const uint64_t* const* ext_a_rows, const uint64_t* ext_b,
+                                 uint64_t fmod, uint64_t* const* out_a_rows, uint64_t* out_b);
 /* out[c] = sum_k matrix[k][c] * ct[k] mod modulus, c < cols: ct[K][n+1], matrix[K][cols], out[cols][n+1] */
 tfhe_status tfhe_ciphertext_mul_matrix(tfhe_ctx* ctx, size_t K, const uint64_t* ct, size_t cols, const int64_t* matrix,
                                        uint64_t modulus, uint64_t* out);

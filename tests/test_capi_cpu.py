@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol(capi):
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.tfhe_abi_version() == 3
+    assert lib.tfhe_abi_version() == 4
 
 
 @pytest.mark.parametrize("name", ["TOY", "MEDIUM", "STD128", "STD128_OPT", "STD192", "STD192_OPT", "STD256",
@@ -148,4 +148,4 @@ def test_cpp_example_builds_and_links(capi, tmp_path):
                     f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True)
     r = subprocess.run([str(exe), "1", "none"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert r.stdout.strip() == "C-ABI version 3"
+    assert r.stdout.strip() == f"C-ABI version {capi.capi.ABI_VERSION}"

@@ -358,11 +358,11 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 // when THR = 0 and the top digit never wraps (the host checks); otherwise every digit is
 // transformed.  Pass 0's lookup tables hold digits in [-64, 64), so they need LOGG <= 7.
 template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2, int CTS = 1, int DIG = 4, int LOGG = 7,
-          int THR = 0, bool FOLD = true>
+          int THR = 0, bool FOLD = true, bool FLAG = false>
 __global__ void __launch_bounds__(TPC * CTS, MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
-                     uint32_t B) {
+                     uint32_t B, uint32_t* __restrict__ done) {
     constexpr int P = 2 * NCT;
     extern __shared__ __align__(16) int32_t lds[];
     static_assert(CTS == 1 || NCT == 1, "CTS > 1 needs NCT = 1");
@@ -604,6 +604,16 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             g[FN + k] = v1;
         }
     }
+    // FLAG (host-array EvalAcc, engine.hip d2h_flagged): done[4 ct + w] = 1 in pinned host memory once
+    // wave w's accumulator words are in HBM -- its system-scope release waits for its stores and writes
+    // the XCD's L2 back -- so the host can DMA finished ciphertexts while later workgroups still run.
+    // A separate instantiation: the store after the loop changes the loop's register allocation (5
+    // scratch loads per round, +43 instructions), so the device-resident path keeps FLAG = false.
+    if constexpr (FLAG) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)  // lane 0, not `lane`: kept live
+            __hip_atomic_store(done + wg_ct * 4 + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 #ifndef TFHE_FAST4_KERNEL_ONLY  // blind_rotate_fast4_d6.hip includes the kernel template only
@@ -668,13 +678,13 @@ hipError_t launch_blind_rotate_fast4_d6(const f4::FastConst& K, uint32_t n, uint
 
 hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
-                                     size_t B, hipStream_t s) {
+                                     size_t B, hipStream_t s, BRDone* dn) {
     const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
-    auto launch = [&](auto kern, int nct, int xb = 2, int cts = 1) {
+    auto launch = [&](auto kern, int nct, int xb = 2, int cts = 1, uint32_t* done = nullptr) {
         const size_t lb = f4::lds_bytes(2 * nct, xb, cts);
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
         hipLaunchKernelGGL(kern, dim3((unsigned)((B + nct * cts - 1) / (nct * cts))), dim3(f4::TPC * cts), lb, s, Kc,
-                           n, loga, tabs4, bsk, a, acc, (uint32_t)B);
+                           n, loga, tabs4, bsk, a, acc, (uint32_t)B, done);
     };
     // other digit shapes: the default build (variant 60's template arguments) at that shape
     if (sh.dig == 6 && sh.logg == 5 && sh.thr == 0 && sh.fold)  // own translation unit (Makefile)
@@ -688,6 +698,11 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
         return hipGetLastError();
     }
     if (!(sh.dig == 4 && sh.logg == 7 && sh.thr == 0 && sh.fold)) return hipErrorNotSupported;
+    if (dn && dn->flags && variant == 60) {  // the default build with completion flags (FLAG)
+        launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 4, 7, 0, true, true>, 1, 1, 1, dn->flags);
+        dn->written = true;
+        return hipGetLastError();
+    }
     switch (variant) {  // cross-check builds (blind_rotate_fast.hip known_variant)
         case 70: launch(f4::k_blind_rotate_fast4<2, 2>, 2); break;                    // two ciphertexts per wavefront
         case 86: launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 4>, 1, 1, 4); break;  // four per workgroup

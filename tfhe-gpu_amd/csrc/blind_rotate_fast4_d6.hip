@@ -12,7 +12,8 @@ hipError_t launch_blind_rotate_fast4_d6(const f4::FastConst& K, uint32_t n, uint
     auto kern = f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 6, 5, 0, true>;
     const size_t lb = f4::lds_bytes(2, 1, 1);
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-    hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(f4::TPC), lb, s, K, n, loga, tabs4, bsk, a, acc, (uint32_t)B);
+    hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(f4::TPC), lb, s, K, n, loga, tabs4, bsk, a, acc, (uint32_t)B,
+                       nullptr);
     return hipGetLastError();
 }
 

@@ -133,6 +133,11 @@ struct Device {
     hipEvent_t sc_fence = nullptr;
     hipEvent_t h2d_ev[2] = {};  // host-array runner: input of I/O set k landed
     hipEvent_t k_ev[2] = {};    // host-array runner: kernels that use I/O set k done
+    // Completion flags of the host-array EvalAcc (d2h_flagged): pinned host words, 4 per ciphertext,
+    // set by the blind rotation's waves; br_done.flags is non-null only while such a call queues its op.
+    uint32_t* flags = nullptr;
+    size_t flags_words = 0;
+    BRDone br_done{};
 };
 
 // hipMalloc'd buffer owned by one scope (error paths free it too)
@@ -350,6 +355,7 @@ void free_device(Device& d) {
         hipFree(sc->io);
         hipFree(sc->pk);
     }
+    if (d.flags) hipHostFree(d.flags);
     for (int k = 0; k < 2; ++k) {
         if (d.pin_ev[k]) hipEventSynchronize(d.pin_ev[k]), hipEventDestroy(d.pin_ev[k]);
         if (d.pin[k]) hipHostFree(d.pin[k]);
@@ -448,7 +454,8 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     if (amod == 0 || (2ull * c->p.N) % amod != 0) return fail(TFHE_ERR_INVALID_ARGUMENT, "a-modulus must divide 2N");
     const ArenaLayout& L = c->layout;
     if (c->use_fast && (amod & (amod - 1)) == 0) {
-        HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream));
+        HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream,
+                                        d.br_done.flags ? &d.br_done : nullptr));
     } else if (c->use_f64) {
         HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream));
     } else if (c->use_sf) {
@@ -700,7 +707,7 @@ tfhe_status ensure_pinned(Device& d) {
 // pool narrows each block into pinned memory, the DMA moves wb bytes per word into `pk` (device),
 // and one kernel widens pk into dst.  wb is the caller's guess from the array's modulus; a value
 // that does not fit (an unreduced input) sends the whole array again as u64.
-tfhe_status h2d_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t words, hipStream_t s, int wb = 8,
+tfhe_status h2d_staged(Device& d, uint64_t* dst, const HostIn& src, size_t words, hipStream_t s, int wb = 8,
                        void* pk = nullptr) {
     SCHECK(ensure_pinned(d));
     const size_t per = kStageBytes / wb;  // words per block
@@ -710,10 +717,10 @@ tfhe_status h2d_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t wor
         const size_t nw = std::min(per, words - off);
         HCHECK(hipEventSynchronize(d.pin_ev[slot]));  // the DMA that last read this block is done
         if (wb == 8) {
-            parallel_memcpy(d.pin[slot], src + off, nw * 8);
+            parallel_memcpy_in((uint64_t*)d.pin[slot], src, off, nw);
             HCHECK(hipMemcpyAsync(dst + off, d.pin[slot], nw * 8, hipMemcpyHostToDevice, s));
         } else {
-            seen |= parallel_narrow(d.pin[slot], src + off, nw, wb);
+            seen |= parallel_narrow_in(d.pin[slot], src, off, nw, wb);
             HCHECK(hipMemcpyAsync((char*)pk + off * wb, d.pin[slot], nw * wb, hipMemcpyHostToDevice, s));
         }
         HCHECK(hipEventRecord(d.pin_ev[slot], s));
@@ -725,7 +732,7 @@ tfhe_status h2d_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t wor
 }
 // words u64 device -> host; wb < 8 (every value below 2^(8 wb)): one kernel narrows src into pk,
 // the DMA moves wb bytes per word, the host pool widens each block into dst
-tfhe_status d2h_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t words, hipStream_t s, int wb = 8,
+tfhe_status d2h_staged(Device& d, const HostOut& dst, const uint64_t* src, size_t words, hipStream_t s, int wb = 8,
                        void* pk = nullptr) {
     SCHECK(ensure_pinned(d));
     if (wb != 8) HCHECK(launch_narrow(src, wb, pk, words, s));
@@ -744,12 +751,80 @@ tfhe_status d2h_staged(Device& d, uint64_t* dst, const uint64_t* src, size_t wor
         if (k > 0) {  // drain the previous block while this one is in flight
             const int ps = (int)((k - 1) & 1);
             HCHECK(hipEventSynchronize(d.pin_ev[ps]));
-            if (wb == 8) parallel_memcpy(dst + prev_off, d.pin[ps], prev_nw * 8);
-            else parallel_widen(dst + prev_off, d.pin[ps], prev_nw, wb);
+            if (wb == 8) parallel_memcpy_out(dst, prev_off, (const uint64_t*)d.pin[ps], prev_nw);
+            else parallel_widen_out(dst, prev_off, d.pin[ps], prev_nw, wb);
         }
         if (!more) break;
         prev_off = off, prev_nw = nw;
     }
+    return TFHE_OK;
+}
+
+// The host-array EvalAcc's output while its blind rotation still runs.  The launch wrote completion
+// flags (BRDone: 4 words per ciphertext, one per wave, stored in pinned host memory after the wave's
+// accumulator words reached HBM); workgroups are dispatched in ciphertext order, so the ciphertexts of
+// block k finish before most of block k+1's.  For each 8 MiB block the host waits for its flags, the
+// DMA copies it (u64, no narrowing kernel: it would have to wait for the whole launch) on the copy
+// stream, and the host drains the previous block into dst.  Only the last block or two, which finish
+// with the launch's last wave, are exposed after the kernel -- instead of the whole 67 MB.
+// The wait never hangs: if the compute stream completes (or fails) with a flag unset, or 120 s pass,
+// the call fails.
+tfhe_status wait_flags(const uint32_t* flags, size_t lo, size_t hi, hipStream_t cs) {
+    const volatile uint32_t* f = flags;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (size_t i = lo, polls = 0; i < hi; ++polls) {
+        if (f[i] != 0) {
+            ++i;
+            continue;
+        }
+        if ((polls & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(cs);
+            if (q == hipSuccess) {
+                if (f[i] == 0) return fail(TFHE_ERR_INTERNAL, "blind rotation finished without its completion flag");
+            } else if (q != hipErrorNotReady) {
+                return fail(TFHE_ERR_DEVICE, std::string("blind rotation: ") + hipGetErrorString(q));
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+                return fail(TFHE_ERR_DEVICE, "blind rotation: completion flags not set within 120 s");
+            std::this_thread::yield();
+        }
+    }
+    return TFHE_OK;
+}
+
+tfhe_status d2h_flagged(Device& d, const HostOut& dst, const uint64_t* src, size_t cts, size_t wpc, hipStream_t xs,
+                        hipStream_t cs) {
+    SCHECK(ensure_pinned(d));
+    const size_t cpb = std::max<size_t>(1, (kStageBytes / 8) / wpc);  // ciphertexts per block
+    if (cpb * wpc * 8 > kStageBytes) return fail(TFHE_ERR_UNSUPPORTED, "accumulator larger than a staging block");
+    size_t prev_lo = 0, prev_n = 0;
+    for (size_t lo = 0, k = 0;; lo += cpb, ++k) {
+        const int slot = (int)(k & 1);
+        const bool more = lo < cts;
+        const size_t n = more ? std::min(cpb, cts - lo) : 0;
+        if (more) {
+            SCHECK(wait_flags(d.flags, 4 * lo, 4 * (lo + n), cs));
+            HCHECK(hipEventSynchronize(d.pin_ev[slot]));
+            HCHECK(hipMemcpyAsync(d.pin[slot], src + lo * wpc, n * wpc * 8, hipMemcpyDeviceToHost, xs));
+            HCHECK(hipEventRecord(d.pin_ev[slot], xs));
+        }
+        if (k > 0) {
+            const int ps = (int)((k - 1) & 1);
+            HCHECK(hipEventSynchronize(d.pin_ev[ps]));
+            parallel_memcpy_out(dst, prev_lo * wpc, (const uint64_t*)d.pin[ps], prev_n * wpc);
+        }
+        if (!more) break;
+        prev_lo = lo, prev_n = n;
+    }
+    return TFHE_OK;
+}
+
+tfhe_status ensure_flags(Device& d, size_t words) {
+    if (words <= d.flags_words) return TFHE_OK;
+    if (d.flags) HCHECK(hipHostFree(d.flags));
+    d.flags = nullptr, d.flags_words = 0;
+    HCHECK(hipHostMalloc((void**)&d.flags, words * 4, hipHostMallocCoherent | hipHostMallocMapped));
+    d.flags_words = words;
     return TFHE_OK;
 }
 
@@ -795,6 +870,12 @@ bool wire_narrowing() {
     const char* e = std::getenv("TFHE_WIRE");
     return !(e && e[0] == '0');
 }
+// Completion-flag output of the host-array EvalAcc (d2h_flagged); TFHE_ACC_FLAGS=0 turns it off (A/B
+// runs; read per call).
+bool wire_flags() {
+    const char* e = std::getenv("TFHE_ACC_FLAGS");
+    return !(e && e[0] == '0');
+}
 
 // Value bounds of the runner's arrays (0: unknown): an array crosses PCIe in the narrowest of u16 /
 // u32 / u64 that holds its bound (h2d_staged / d2h_staged).  Inputs are checked as they are packed
@@ -805,16 +886,19 @@ struct WireLim {
 
 // out_in: the output rows' initial contents (uploaded into the output set before the kernels of
 // their sub-batch, for ops that work in place on the output, e.g. the blind rotation).
+// Arrays are HostRows views (flat or row pointers); w1 / w2 / wo are their record widths.
 template <typename Op>
-tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
-                          uint64_t* out, size_t wo, Op&& op, WireLim wl, const uint64_t* out_in = nullptr) {
+tfhe_status run_lwe_batch_v(tfhe_ctx* c, size_t B, const HostIn& in1, const HostIn& in2, const HostOut& out, Op&& op,
+                            WireLim wl, const HostIn& out_in, bool flag_out = false) {
+    const size_t w1 = in1.w, w2 = in2.empty() ? 0 : in2.w, wo = out.w;
+    const bool has2 = !in2.empty(), has_oi = !out_in.empty();
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
         const size_t parts = host_parts(cnt);
         const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
-        const size_t w_in2 = in2 ? w2 : 0, io_words = sub * (w1 + w_in2 + wo);
+        const size_t w_in2 = has2 ? w2 : 0, io_words = sub * (w1 + w_in2 + wo);
         const bool nar = wire_narrowing();
         auto width = [nar](uint64_t lim) { return nar && lim ? wire_bytes(lim - 1) : 8; };
-        const int wb1 = width(wl.in1), wb2 = in2 ? width(wl.in2) : 8, wbi = out_in ? width(wl.out_in) : 8;
+        const int wb1 = width(wl.in1), wb2 = has2 ? width(wl.in2) : 8, wbi = has_oi ? width(wl.out_in) : 8;
         const int wbo = width(wl.out);
         const size_t pk1 = sub * w1 * wb1, pk2 = sub * w_in2 * wb2, pko = sub * wo * std::max(wbi, wbo);
         SCHECK(ensure_scratch(c, d, sub));
@@ -835,18 +919,19 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
             const int set = (int)(k & 1);
             HCHECK(hipStreamWaitEvent(xs, d.k_ev[set], 0));
-            return d2h_staged(d, out + off * wo, dout_of(set), b * wo, xs, wbo, pk[set] + pk1 + pk2);
+            return d2h_staged(d, out.sub(off), dout_of(set), b * wo, xs, wbo, pk[set] + pk1 + pk2);
         };
         tfhe_status st = TFHE_OK;
+        bool done_out = false;  // the flagged path drained the output already
         const size_t n_sub = (cnt + sub - 1) / sub;
         for (size_t k = 0; k < n_sub && st == TFHE_OK; ++k) {
             const size_t off = lo + k * sub, b = std::min(sub, lo + cnt - off);
             const int set = (int)(k & 1);
-            uint64_t *din1 = io[set], *din2 = in2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
-            st = h2d_staged(d, din1, in1 + off * w1, b * w1, xs, wb1, pk[set]);
-            if (st == TFHE_OK && in2) st = h2d_staged(d, din2, in2 + off * w2, b * w2, xs, wb2, pk[set] + pk1);
-            if (st == TFHE_OK && out_in)
-                st = h2d_staged(d, dout, out_in + off * wo, b * wo, xs, wbi, pk[set] + pk1 + pk2);
+            uint64_t *din1 = io[set], *din2 = has2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
+            st = h2d_staged(d, din1, in1.sub(off), b * w1, xs, wb1, pk[set]);
+            if (st == TFHE_OK && has2) st = h2d_staged(d, din2, in2.sub(off), b * w2, xs, wb2, pk[set] + pk1);
+            if (st == TFHE_OK && has_oi)
+                st = h2d_staged(d, dout, out_in.sub(off), b * wo, xs, wbi, pk[set] + pk1 + pk2);
             if (st != TFHE_OK) break;
             if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu inputs staged at %.2f ms (wire %d/%d/%d/%d B)\n", k,
                                     now() - t0, wb1, wb2, wbi, wbo);
@@ -855,8 +940,27 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
                 st = fail(TFHE_ERR_DEVICE, "host batch: event ordering failed");
                 break;
             }
+            // flag_out (EvalAcc): one sub-batch lets its blind rotation flag finished ciphertexts
+            const bool flagged = flag_out && n_sub == 1 && wire_flags();
+            if (flagged) {
+                st = ensure_flags(d, 4 * b);
+                if (st != TFHE_OK) break;
+                std::memset(d.flags, 0, 4 * b * sizeof(uint32_t));  // no kernel of an earlier call is left
+                d.br_done = BRDone{};
+                d.br_done.flags = d.flags;
+            }
             st = op(d, din1, din2, dout, b, off);
+            const bool written = flagged && d.br_done.written;
+            d.br_done = BRDone{};
             if (st != TFHE_OK) break;
+            if (written) {  // the blind rotation was the op's last kernel: drain while it runs
+                if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu queued at %.2f ms (flagged output)\n", k, now() - t0);
+                st = d2h_flagged(d, out.sub(off), dout, b, wo, xs, cs);
+                if (trace) std::fprintf(stderr, "[tfhe] flagged output drained at %.2f ms\n", now() - t0);
+                if (st != TFHE_OK) break;
+                done_out = true;
+                continue;
+            }
             if (hipEventRecord(d.k_ev[set], cs) != hipSuccess) {
                 st = fail(TFHE_ERR_DEVICE, "host batch: event record failed");
                 break;
@@ -864,7 +968,7 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu queued at %.2f ms\n", k, now() - t0);
             if (k > 0) st = d2h(k - 1);
         }
-        if (st == TFHE_OK && n_sub > 0) {
+        if (st == TFHE_OK && n_sub > 0 && !done_out) {
             if (trace) {
                 HCHECK(hipStreamSynchronize(cs));
                 std::fprintf(stderr, "[tfhe] last sub-batch's kernels done at %.2f ms\n", now() - t0);
@@ -877,6 +981,15 @@ tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1,
             st = fail(TFHE_ERR_DEVICE, std::string("host batch: ") + hipGetErrorString(e1 != hipSuccess ? e1 : e2));
         return st;
     });
+}
+
+// flat [B][w] arrays
+template <typename Op>
+tfhe_status run_lwe_batch(tfhe_ctx* c, size_t B, const uint64_t* in1, size_t w1, const uint64_t* in2, size_t w2,
+                          uint64_t* out, size_t wo, Op&& op, WireLim wl, const uint64_t* out_in = nullptr,
+                          bool flag_out = false) {
+    return run_lwe_batch_v(c, B, flat_rows(in1, w1), in2 ? flat_rows(in2, w2) : HostIn{}, flat_rows(out, wo),
+                           std::forward<Op>(op), wl, out_in ? flat_rows(out_in, wo) : HostIn{}, flag_out);
 }
 
 tfhe_status check_ctx(tfhe_ctx* c) {
@@ -1282,7 +1395,7 @@ tfhe_status tfhe_eval_acc(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t a_m
             [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
                 return dev_blind_rotate(c, d, i1, a_mod, o, b);
             },
-            WireLim{a_mod, 0, p.Q, p.Q}, acc);
+            WireLim{a_mod, 0, p.Q, p.Q}, acc, true);
     });
 }
 
@@ -1300,7 +1413,29 @@ tfhe_status tfhe_eval_acc_tv(tfhe_ctx* c, size_t B, const uint64_t* a, uint64_t 
                                  HCHECK(launch_expand_tv(p.N, tv_len, i2, o, b, d.stream));
                                  return dev_blind_rotate(c, d, i1, a_mod, o, b);
                              },
-                             WireLim{a_mod, p.Q, 0, p.Q});
+                             WireLim{a_mod, p.Q, 0, p.Q}, nullptr, true);
+    });
+}
+
+tfhe_status tfhe_eval_acc_tv_rows(tfhe_ctx* c, size_t B, const uint64_t* const* a_rows, uint64_t a_mod,
+                                  const uint64_t* tv, uint32_t tv_len, uint64_t* const* acc_rows) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!a_rows || !tv || !acc_rows) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        const tfhe_params& p = c->p;
+        if (tv_len == 0 || tv_len > p.N || p.N % tv_len != 0)
+            return fail(TFHE_ERR_INVALID_ARGUMENT, "test-vector length must divide N");
+        for (size_t s = 0; s < B; ++s)
+            if (!a_rows[s] || !acc_rows[2 * s] || !acc_rows[2 * s + 1])
+                return fail(TFHE_ERR_INVALID_ARGUMENT, "null row pointer");
+        return run_lwe_batch_v(c, B, ptr_rows(a_rows, 1, p.n, (const uint64_t*)nullptr), flat_rows(tv, tv_len),
+                               ptr_rows(acc_rows, 2, p.N, (uint64_t*)nullptr),
+                               [&](Device& d, const uint64_t* i1, const uint64_t* i2, uint64_t* o, size_t b, size_t) {
+                                   HCHECK(launch_expand_tv(p.N, tv_len, i2, o, b, d.stream));
+                                   return dev_blind_rotate(c, d, i1, a_mod, o, b);
+                               },
+                               WireLim{a_mod, p.Q, 0, p.Q}, HostIn{}, true);
     });
 }
 
@@ -1333,6 +1468,24 @@ tfhe_status tfhe_mkm_switch(tfhe_ctx* c, size_t B, const uint64_t* ct_ext, uint6
                                  return dev_mkm(c, d, i1, fmod, o, b);
                              },
                              WireLim{p.Q, 0, 0, fmod});
+    });
+}
+
+tfhe_status tfhe_mkm_switch_rows(tfhe_ctx* c, size_t B, const uint64_t* const* ext_a_rows, const uint64_t* ext_b,
+                                 uint64_t fmod, uint64_t* const* out_a_rows, uint64_t* out_b) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!ext_a_rows || !ext_b || !out_a_rows || !out_b) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        for (size_t s = 0; s < B; ++s)
+            if (!ext_a_rows[s] || !out_a_rows[s]) return fail(TFHE_ERR_INVALID_ARGUMENT, "null row pointer");
+        const tfhe_params& p = c->p;
+        return run_lwe_batch_v(c, B, ptr_rows(ext_a_rows, 1, p.N, ext_b), HostIn{},
+                               ptr_rows(out_a_rows, 1, p.n, out_b),
+                               [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t) {
+                                   return dev_mkm(c, d, i1, fmod, o, b);
+                               },
+                               WireLim{p.Q, 0, 0, fmod}, HostIn{});
     });
 }
 

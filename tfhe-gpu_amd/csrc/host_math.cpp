@@ -113,6 +113,57 @@ void parallel_widen(uint64_t* dst, const void* src, size_t n, int wb) {
     });
 }
 
+// ---- the same over row-pointer views (HostRows); flat views take the loops above ----
+void parallel_memcpy_in(uint64_t* dst, const HostIn& v, size_t off, size_t n) {
+    if (v.flat) return parallel_memcpy(dst, v.flat + off, n * 8);
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        v.walk(off + lo, off + hi, [&](const uint64_t* p, size_t at, size_t len) {
+            std::memcpy(dst + lo + at, p, len * 8);
+        });
+    });
+}
+
+uint64_t parallel_narrow_in(void* dst, const HostIn& v, size_t off, size_t n, int wb) {
+    if (v.flat) return parallel_narrow(dst, v.flat + off, n, wb);
+    std::atomic<uint64_t> acc{0};
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        uint64_t o = 0;
+        v.walk(off + lo, off + hi, [&](const uint64_t* p, size_t at, size_t len) {
+            if (wb == 2) {
+                uint16_t* d = (uint16_t*)dst + lo + at;
+                for (size_t i = 0; i < len; ++i) o |= p[i], d[i] = (uint16_t)p[i];
+            } else {
+                uint32_t* d = (uint32_t*)dst + lo + at;
+                for (size_t i = 0; i < len; ++i) o |= p[i], d[i] = (uint32_t)p[i];
+            }
+        });
+        acc.fetch_or(o, std::memory_order_relaxed);
+    });
+    return acc.load();
+}
+
+void parallel_memcpy_out(const HostOut& v, size_t off, const uint64_t* src, size_t n) {
+    if (v.flat) return parallel_memcpy(v.flat + off, src, n * 8);
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        v.walk(off + lo, off + hi, [&](uint64_t* p, size_t at, size_t len) { std::memcpy(p, src + lo + at, len * 8); });
+    });
+}
+
+void parallel_widen_out(const HostOut& v, size_t off, const void* src, size_t n, int wb) {
+    if (v.flat) return parallel_widen(v.flat + off, src, n, wb);
+    pool_run(n, n * 8, [&](size_t lo, size_t hi) {
+        v.walk(off + lo, off + hi, [&](uint64_t* p, size_t at, size_t len) {
+            if (wb == 2) {
+                const uint16_t* s = (const uint16_t*)src + lo + at;
+                for (size_t i = 0; i < len; ++i) p[i] = s[i];
+            } else {
+                const uint32_t* s = (const uint32_t*)src + lo + at;
+                for (size_t i = 0; i < len; ++i) p[i] = s[i];
+            }
+        });
+    });
+}
+
 
 uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
     uint64_t r = 1 % m;

@@ -57,6 +57,70 @@ void parallel_widen(uint64_t* dst, const void* src, size_t n, int wb);
 // Wire bytes per word for values below 2^bits(max_or): 2, 4 or 8.
 inline int wire_bytes(uint64_t max_or) { return max_or < (1ull << 16) ? 2 : (max_or < (1ull << 32) ? 4 : 8); }
 
+// A host array of records of w u64 words, held either flat ([records][w]) or as row pointers: record
+// s is rows[s k] ... rows[s k + k - 1] (rw words each) followed, when tail is set, by tail[s]
+// (w = k rw + 1).  The row form lets a caller whose ciphertexts live in separate allocations (the
+// drop-in shim: one NativeVector per polynomial) hand them to the PCIe staging directly, with no
+// flat copy on either side.  P is const uint64_t (inputs) or uint64_t (outputs).
+template <typename P>
+struct HostRows {
+    P* flat = nullptr;
+    P* const* rows = nullptr;
+    P* tail = nullptr;
+    size_t k = 1, rw = 0, w = 0;
+    bool empty() const { return !flat && !rows; }
+    HostRows sub(size_t s) const {  // the view from record s on
+        HostRows v = *this;
+        if (flat) v.flat = flat + s * w;
+        if (rows) v.rows = rows + s * k;
+        if (tail) v.tail = tail + s;
+        return v;
+    }
+    // f(p, at, len): words [lo + at, lo + at + len) of the view are p[0 .. len)
+    template <typename F>
+    void walk(size_t lo, size_t hi, F&& f) const {
+        if (flat) {
+            if (hi > lo) f(flat + lo, (size_t)0, hi - lo);
+            return;
+        }
+        for (size_t i = lo; i < hi;) {
+            const size_t s = i / w, r = i % w, j = r / rw;
+            if (j < k) {
+                const size_t in = r - j * rw, len = std::min(rw - in, hi - i);
+                f(rows[s * k + j] + in, i - lo, len);
+                i += len;
+            } else {
+                f(tail + s, i - lo, (size_t)1);
+                i += 1;
+            }
+        }
+    }
+};
+using HostIn = HostRows<const uint64_t>;
+using HostOut = HostRows<uint64_t>;
+template <typename P>
+HostRows<P> flat_rows(P* p, size_t w) {
+    HostRows<P> v;
+    v.flat = p;
+    v.rw = v.w = w;
+    return v;
+}
+template <typename P>
+HostRows<P> ptr_rows(P* const* rows, size_t k, size_t rw, P* tail) {
+    HostRows<P> v;
+    v.rows = rows;
+    v.k = k;
+    v.rw = rw;
+    v.tail = tail;
+    v.w = k * rw + (tail ? 1 : 0);
+    return v;
+}
+// The staging operations over views: words [off, off + n) of v <-> dst / src[0 .. n).
+void parallel_memcpy_in(uint64_t* dst, const HostIn& v, size_t off, size_t n);
+uint64_t parallel_narrow_in(void* dst, const HostIn& v, size_t off, size_t n, int wb);
+void parallel_memcpy_out(const HostOut& v, size_t off, const uint64_t* src, size_t n);
+void parallel_widen_out(const HostOut& v, size_t off, const void* src, size_t n, int wb);
+
 using u128 = unsigned __int128;
 
 inline uint64_t mulmod(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)(((u128)a * b) % m); }

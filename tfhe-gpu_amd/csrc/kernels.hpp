@@ -25,6 +25,15 @@ struct DevTables {
     const uint32_t* eidx;// [N]  NTT(X)[x] = psi^eidx[x]
 };
 
+// Completion flags of a blind rotation (host-array EvalAcc: engine.hip d2h_flagged).  A launcher
+// whose kernel stores flags[ct] = gen in host memory once ciphertext ct's accumulator is in HBM
+// sets written; the others leave it false and the caller waits for the whole launch instead.
+struct BRDone {
+    uint32_t* flags = nullptr;  // pinned host memory, one word per ciphertext
+    uint32_t gen = 0;
+    bool written = false;
+};
+
 // Generic LDS-resident blind rotation: one workgroup per ciphertext.
 //   a[B][n] mod amod, acc[B][2][N] (u64, coefficient) in/out, acc0 transposed on exit.
 //   bsk/bsk_sh: [n][2][dG2][2][N] in W, NTT domain, scaled by N^-1.
@@ -36,7 +45,7 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
 // transforms, one wavefront per ciphertext.  Returns hipErrorNotSupported when the
 // parameters do not match its specialisation.
 hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables& T, const void* bsk_fast, const uint64_t* a,
-                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, BRDone* dn = nullptr);
 bool fast_path_supported(const BRParams& P, int word_bits);
 // Converts the generic device BSK and tables into the fast kernel's Montgomery form.
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
@@ -57,7 +66,7 @@ size_t fast4_table_words();
 hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, hipStream_t s);
 hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
-                                     size_t B, hipStream_t s);
+                                     size_t B, hipStream_t s, BRDone* dn = nullptr);
 
 // Exact-FP64 blind rotation for 2^32 <= Q < 2^40 (STD192 class): keys/tables as centred
 // doubles derived on device from the generic (u64) arena.

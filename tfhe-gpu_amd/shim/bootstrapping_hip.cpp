@@ -26,8 +26,13 @@
 #include "tfhe_hip.h"
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace lbcrypto {
@@ -50,6 +55,60 @@ T* stage(std::vector<T>& v, size_t words) {
     return v.data();
 }
 std::vector<uint64_t> g_a, g_acc, g_tv, g_ext, g_out;
+
+// The u64 storage of a NativeVector: NativeIntegerT<uint64_t> is one uint64_t with no virtual
+// members, and NativeVectorT keeps its elements in one std::vector (mubintvecnat.h:645-651), so
+// the rows can be handed to the engine's staging as plain u64 arrays.
+static_assert(sizeof(NativeInteger) == sizeof(uint64_t), "NativeInteger is not one 64-bit word");
+const uint64_t* words(const NativeVector& v) { return reinterpret_cast<const uint64_t*>(&v[0]); }
+uint64_t* words(NativeVector& v) { return reinterpret_cast<uint64_t*>(&v[0]); }
+uint64_t* words(const NativeVector& v, int) { return const_cast<uint64_t*>(words(v)); }
+
+
+// The ciphertext objects a call replaces (8192 RLWE / LWE objects and their coefficient vectors per
+// batch) are released by one background thread, after the call has returned: freeing them on the
+// caller's thread took 1.6-1.9 ms per 8192 (profiles/r03o), and from the OpenMP workers the frees
+// of blocks another thread allocated serialise on the allocator.  One heap object, intentionally
+// never destroyed (its thread is detached), so process exit does not race it.
+class Reaper {
+   public:
+    static void drop(std::vector<std::shared_ptr<void>>&& batch) {
+        static Reaper* r = new Reaper();
+        {
+            std::lock_guard<std::mutex> lk(r->m_);
+            r->q_.push_back(std::move(batch));
+        }
+        r->cv_.notify_one();
+    }
+
+   private:
+    Reaper() { std::thread([this] { loop(); }).detach(); }
+    void loop() {
+        for (;;) {
+            std::vector<std::shared_ptr<void>> b;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                b = std::move(q_.front());
+                q_.pop_front();
+            }
+            b.clear();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::deque<std::vector<std::shared_ptr<void>>> q_;
+};
+
+template <typename T>
+void release_later(std::vector<std::shared_ptr<T>>& objs) {
+    std::vector<std::shared_ptr<void>> b;
+    b.reserve(objs.size());
+    for (auto& o : objs)
+        if (o) b.emplace_back(std::move(o));
+    objs.clear();
+    if (!b.empty()) Reaper::drop(std::move(b));
+}
 
 struct Timer {
     const bool on;
@@ -135,73 +194,92 @@ void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> pa
     const uint64_t amod = a[0].GetModulus().ConvertToInt();
     const uint64_t factor = amod ? (2ull * N) / amod : 0;  // test-vector stride (binfhe-base-scheme.cpp:1120)
     const uint32_t tvlen = factor ? (uint32_t)(N / factor) : 0;
-    uint64_t* fa = stage(g_a, Bn * n);
+    const auto polyParams = params->GetPolyParams();
+    const NativeInteger Q = params->GetQ();
+    // pass 1: the rows of a (no copy: the staging narrows them from their own storage), and whether
+    // every accumulator is a COEFFICIENT test vector (acc0 = 0, acc1 zero off the stride); the "GPU"
+    // mode of RingGSWAccumulatorCGGI::EvalAcc passes EVALUATION-format accumulators
+    // (rgsw-acc-cggi.cpp:196-205), which take the general path below
+    std::vector<const uint64_t*> arows(Bn);
     uint64_t* ftv = stage(g_tv, Bn * (size_t)tvlen);
-    // pass 1: a, and whether every accumulator is a COEFFICIENT test vector (acc0 = 0, acc1 zero off
-    // the stride); the "GPU" mode of RingGSWAccumulatorCGGI::EvalAcc passes EVALUATION-format
-    // accumulators (rgsw-acc-cggi.cpp:196-205), which take the general path below
-    int sparse = factor >= 1 && (2ull * N) % amod == 0;
-#pragma omp parallel for reduction(&& : sparse)
+    int sparse = factor >= 1 && (2ull * N) % amod == 0, lens_ok = 1;
+#pragma omp parallel for reduction(&& : sparse, lens_ok)
     for (size_t s = 0; s < Bn; ++s) {
-        const NativeVector& as = a[s];
-        for (uint32_t l = 0; l < n; ++l) fa[s * n + l] = as[l].ConvertToInt();
+        lens_ok = lens_ok && a[s].GetLength() == n;
+        arows[s] = words(a[s]);
         if (!sparse) continue;
         const auto& e = (*acc)[s]->GetElements();
-        if (e[0].GetFormat() != Format::COEFFICIENT || e[1].GetFormat() != Format::COEFFICIENT) {
+        if (e[0].GetFormat() != Format::COEFFICIENT || e[1].GetFormat() != Format::COEFFICIENT ||
+            e[0].GetLength() != N || e[1].GetLength() != N) {
             sparse = 0;
             continue;
         }
-        const NativeVector& v0 = e[0].GetValues();
-        const NativeVector& v1 = e[1].GetValues();
-        bool ok = true;
-        for (uint32_t x = 0; x < N && ok; ++x) {
-            ok = v0[x].ConvertToInt() == 0 && (x % factor == 0 || v1[x].ConvertToInt() == 0);
-            if (x % factor == 0) ftv[s * tvlen + x / factor] = v1[x].ConvertToInt();
+        const uint64_t* v0 = words(e[0].GetValues());
+        const uint64_t* v1 = words(e[1].GetValues());
+        uint64_t nz = 0;
+        for (uint32_t x = 0; x < N; ++x) nz |= v0[x];
+        for (uint32_t x = 0; x < N; x += (uint32_t)factor) {
+            ftv[s * tvlen + x / factor] = v1[x];
+            for (uint32_t y = x + 1; y < x + factor; ++y) nz |= v1[y];
         }
-        sparse = sparse && ok;
+        sparse = sparse && nz == 0;
     }
+    if (!lens_ok) OPENFHE_THROW(openfhe_error, "EvalAcc_CUDA: the a vectors differ in length");
     tm.lap(sparse ? "marshal in (test vectors)" : "marshal in", Bn);
-    uint64_t* fac = stage(g_acc, Bn * 2 * N);
     if (sparse) {
-        check(tfhe_eval_acc_tv(g_ctx, Bn, fa, amod, ftv, tvlen, fac), "tfhe_eval_acc_tv");
-    } else {
+        // Results go into the accumulators' own coefficient vectors when this vector holds the only
+        // reference and they have the shape of the result (the callers' fresh test vectors): the
+        // staging writes them in place.  Otherwise into new objects, as the reference does
+        // (bootstrapping.cu:1655-1664); the replaced ones go to the Reaper.
+        std::vector<uint64_t*> rows(2 * Bn);
+        std::vector<RLWECiphertext> fresh(Bn);
 #pragma omp parallel for
-        for (size_t s = 0; s < Bn; ++s)
-            for (uint32_t j = 0; j < 2; ++j) {
-                NativePoly c = (*acc)[s]->GetElements()[j];
-                c.SetFormat(Format::COEFFICIENT);
-                const NativeVector& v = c.GetValues();
-                for (uint32_t x = 0; x < N; ++x) fac[(s * 2 + j) * N + x] = v[x].ConvertToInt();
+        for (size_t s = 0; s < Bn; ++s) {
+            RLWECiphertext& ct = (*acc)[s];
+            bool reuse = ct.use_count() == 1;
+            if (reuse) {
+                const auto& e = ct->GetElements();
+                for (uint32_t j = 0; j < 2 && reuse; ++j)
+                    reuse = e[j].GetFormat() == Format::COEFFICIENT && e[j].GetLength() == N && e[j].GetModulus() == Q;
             }
-        check(tfhe_eval_acc(g_ctx, Bn, fa, amod, fac), "tfhe_eval_acc");
+            RLWECiphertext& dst = reuse ? ct : fresh[s];
+            if (!reuse) {
+                std::vector<NativePoly> res(2);
+                for (uint32_t j = 0; j < 2; ++j) {
+                    res[j] = NativePoly(polyParams, Format::COEFFICIENT, false);
+                    res[j].SetValues(NativeVector(N, Q), Format::COEFFICIENT);
+                }
+                dst = std::make_shared<RLWECiphertextImpl>(std::move(res));
+            }
+            for (uint32_t j = 0; j < 2; ++j) rows[2 * s + j] = words(dst->GetElements()[j].GetValues(), 0);
+        }
+        tm.lap("output rows", Bn);
+        check(tfhe_eval_acc_tv_rows(g_ctx, Bn, arows.data(), amod, ftv, tvlen, rows.data()),
+              "tfhe_eval_acc_tv_rows");  // acc0 already transposed (bootstrapping.cu:675-686)
+        tm.lap("device", Bn);
+        for (size_t s = 0; s < Bn; ++s)
+            if (fresh[s]) std::swap((*acc)[s], fresh[s]);
+        release_later(fresh);
+        tm.lap("marshal out", Bn);
+        return;
     }
+    uint64_t* fa = stage(g_a, Bn * n);
+    uint64_t* fac = stage(g_acc, Bn * 2 * N);
+#pragma omp parallel for
+    for (size_t s = 0; s < Bn; ++s) {
+        std::copy(arows[s], arows[s] + n, fa + s * n);
+        for (uint32_t j = 0; j < 2; ++j) {
+            NativePoly c = (*acc)[s]->GetElements()[j];
+            c.SetFormat(Format::COEFFICIENT);
+            const NativeVector& v = c.GetValues();
+            for (uint32_t x = 0; x < N; ++x) fac[(s * 2 + j) * N + x] = v[x].ConvertToInt();
+        }
+    }
+    check(tfhe_eval_acc(g_ctx, Bn, fa, amod, fac), "tfhe_eval_acc");
     tm.lap("device", Bn);
-    const auto polyParams = params->GetPolyParams();
-    const NativeInteger Q = params->GetQ();
-    // Results go into the accumulators' own coefficient vectors when this vector holds the only
-    // reference and they have the shape of the result (the callers' fresh test vectors): no
-    // allocation.  Otherwise new objects, as the reference does (bootstrapping.cu:1655-1664); the
-    // replaced ones are released on this thread afterwards (freeing another thread's blocks from
-    // the OpenMP workers serialises on the allocator).
     std::vector<RLWECiphertext> old(Bn);
 #pragma omp parallel for
-    for (size_t s = 0; s < Bn; ++s) {  // acc0 already transposed (bootstrapping.cu:675-686)
-        RLWECiphertext& ct = (*acc)[s];
-        bool reuse = ct.use_count() == 1;
-        if (reuse) {
-            const auto& e = ct->GetElements();
-            for (uint32_t j = 0; j < 2 && reuse; ++j)
-                reuse = e[j].GetFormat() == Format::COEFFICIENT && e[j].GetLength() == N && e[j].GetModulus() == Q;
-        }
-        if (reuse) {
-            auto& e = ct->GetElements();
-            for (uint32_t j = 0; j < 2; ++j) {
-                NativeVector& v = const_cast<NativeVector&>(e[j].GetValues());
-                const uint64_t* src = fac + (s * 2 + j) * N;
-                for (uint32_t x = 0; x < N; ++x) v[x] = src[x];
-            }
-            continue;
-        }
+    for (size_t s = 0; s < Bn; ++s) {
         std::vector<NativePoly> res(2);
         for (uint32_t j = 0; j < 2; ++j) {
             NativeVector v(N, Q);
@@ -210,10 +288,10 @@ void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> pa
             res[j] = NativePoly(polyParams, Format::COEFFICIENT, false);
             res[j].SetValues(std::move(v), Format::COEFFICIENT);
         }
-        old[s] = std::move(ct);
-        ct = std::make_shared<RLWECiphertextImpl>(std::move(res));
+        old[s] = std::move((*acc)[s]);
+        (*acc)[s] = std::make_shared<RLWECiphertextImpl>(std::move(res));
     }
-    old.clear();
+    release_later(old);
     tm.lap("marshal out", Bn);
 }
 
@@ -224,26 +302,34 @@ void GPUFFTBootstrap::MKMSwitch_CUDA(const std::shared_ptr<LWECryptoParams> para
     const size_t Bn = ctExt->size();
     if (Bn == 0) return;
     const uint32_t N = params->GetN(), n = params->Getn();
-    uint64_t* in = stage(g_ext, Bn * (N + 1));
-    uint64_t* out = stage(g_out, Bn * (n + 1));
-#pragma omp parallel for
+    // inputs stay in the extracted ciphertexts (their a rows are read in place); outputs are new
+    // objects of length n mod fmod (bootstrapping.cu:1898,1926) whose rows the staging fills
+    std::vector<const uint64_t*> arows(Bn);
+    std::vector<uint64_t*> orows(Bn);
+    uint64_t* bin = stage(g_ext, Bn);
+    uint64_t* bout = stage(g_out, Bn);
+    std::vector<LWECiphertext> fresh(Bn);
+    int lens_ok = 1;
+#pragma omp parallel for reduction(&& : lens_ok)
     for (size_t s = 0; s < Bn; ++s) {
-        const NativeVector& av = (*ctExt)[s]->GetA();
-        for (uint32_t k = 0; k < N; ++k) in[s * (N + 1) + k] = av[k].ConvertToInt();
-        in[s * (N + 1) + N] = (*ctExt)[s]->GetB().ConvertToInt();
+        const LWECiphertext& ct = (*ctExt)[s];
+        lens_ok = lens_ok && ct->GetA().GetLength() == N;
+        arows[s] = words(ct->GetA());
+        bin[s] = ct->GetB().ConvertToInt();
+        fresh[s] = std::make_shared<LWECiphertextImpl>(NativeVector(n, fmod), NativeInteger(0));
+        orows[s] = words(fresh[s]->GetA());
     }
+    if (!lens_ok) OPENFHE_THROW(openfhe_error, "MKMSwitch_CUDA: extracted ciphertext of the wrong length");
     tm.lap("marshal in", Bn);
-    check(tfhe_mkm_switch(g_ctx, Bn, in, fmod.ConvertToInt(), out), "tfhe_mkm_switch");
+    check(tfhe_mkm_switch_rows(g_ctx, Bn, arows.data(), bin, fmod.ConvertToInt(), orows.data(), bout),
+          "tfhe_mkm_switch_rows");
     tm.lap("device", Bn);
-    std::vector<LWECiphertext> old(Bn);  // released on this thread (see EvalAcc_CUDA)
 #pragma omp parallel for
     for (size_t s = 0; s < Bn; ++s) {
-        NativeVector av(n, fmod);  // output modulus fmod (bootstrapping.cu:1898,1926)
-        for (uint32_t k = 0; k < n; ++k) av[k] = out[s * (n + 1) + k];
-        old[s] = std::move((*ctExt)[s]);
-        (*ctExt)[s] = std::make_shared<LWECiphertextImpl>(std::move(av), NativeInteger(out[s * (n + 1) + n]));
+        fresh[s]->SetB(NativeInteger(bout[s]));
+        std::swap((*ctExt)[s], fresh[s]);
     }
-    old.clear();
+    release_later(fresh);  // the extracted inputs
     tm.lap("marshal out", Bn);
 }
 

@@ -12,7 +12,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
-ABI_VERSION = 3  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*)
+ABI_VERSION = 4  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -72,6 +72,8 @@ _SIGS = {
     "tfhe_host_shard_selftest": ([SZ, C.c_int, C.c_int, C.POINTER(C.c_size_t)], C.c_int),
     "tfhe_eval_acc_tv": ([VP, SZ, u64p, U64, u64p, C.c_uint32, u64p], C.c_int),
     "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),
+    "tfhe_eval_acc_tv_rows": ([VP, SZ, VP, U64, u64p, C.c_uint32, VP], C.c_int),
+    "tfhe_mkm_switch_rows": ([VP, SZ, VP, VP, U64, VP, VP], C.c_int),
     "tfhe_ciphertext_mul_matrix": ([VP, SZ, u64p, SZ, i64p, U64, u64p], C.c_int),
     "tfhe_lwe_gpu_setup": ([C.c_int], C.c_int),
     "tfhe_lwe_gpu_clean": ([], C.c_int),
