@@ -22,7 +22,8 @@ DROPIN = os.path.join(ROOT, "oracle", "_ref", "ref_dropin")
 DATA = refvec.load()
 CASES = ["std128_NAND", "std128_AND", "std128_XOR", "std128_XNOR_FAST", "std128_acc_amod1024", "std128_acc_amod512",
          "std128_mkm_fmod2048", "std192_NAND", "arb12_func_cube", "arb12_funcvec", "arb12_floor",
-         "c5a_std128q_sign", "c5a_std128q_decomp", "c5b_sign23_sign", "c5b_sign23_floor"]
+         "c5a_std128q_sign", "c5a_std128q_decomp", "c5b_sign23_sign", "c5b_sign23_floor", "toy4096_funcvec",
+         "toy8192_sign"]
 
 
 def run_dropin(c, tmp, extra=()):

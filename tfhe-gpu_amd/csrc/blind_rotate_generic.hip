@@ -152,9 +152,11 @@ k_blind_rotate_generic(BRParams P, const W* __restrict__ psi, const W* __restric
 
 
 // ---------------------------------------------------------------------------
-// Register-resident variant for N in {1024, 2048} (k_blind_rotate_gen2).
+// Register-resident variant (k_blind_rotate_gen2): N = TH CN, TH = 256 threads for N in {1024, 2048},
+// 1024 threads for N in {4096, 8192} (round 3: the reference dispatches N up to 8192,
+// bootstrapping.cu:772-871; v1 needs (2 + dG2) N words of LDS and stops at N = 4096 with dG2 = 2).
 // The accumulator and the external-product sums live in registers: thread t owns
-// coefficients / NTT slots x = t + 256 k (k < CN = N / 256), so the decomposition, the
+// coefficients / NTT slots x = t + TH k (k < CN), so the decomposition, the
 // MAC (coalesced BSK reads) and the accumulator update need no LDS.  Only the current
 // digit's two polynomials pass through LDS for the transforms (2N words), so a workgroup
 // needs 16-32 KiB instead of (2 + dG2) N words: several workgroups share a CU.  Digits
@@ -261,14 +263,14 @@ __device__ __forceinline__ void lds_ntt_inv_r4(W* buf, uint32_t N, uint32_t logN
     }
 }
 
-template <typename W, int CN>
-__global__ void __launch_bounds__(GEN_THREADS, 2)
+template <typename W, int CN, int TH = GEN_THREADS>
+__global__ void __launch_bounds__(TH, TH == GEN_THREADS ? 2 : 1)
 k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__ psi_sh, const W* __restrict__ ipsi,
                     const W* __restrict__ ipsi_sh, const W* __restrict__ mono, const W* __restrict__ mono_sh,
                     const uint32_t* __restrict__ eidx, const W* __restrict__ bsk, const W* __restrict__ bsk_sh,
                     const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
     extern __shared__ __align__(16) unsigned char smem[];
-    constexpr uint32_t N = GEN_THREADS * CN;
+    constexpr uint32_t N = TH * CN;
     W* buf = reinterpret_cast<W*>(smem);  // [2][N]: the current digit of both polynomials
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const W Q = (W)P.Q, r1 = (W)P.r1;
@@ -278,7 +280,7 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
     uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
     const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
     uint32_t* ex = reinterpret_cast<uint32_t*>(smem + (size_t)2 * N * sizeof(W));  // rotation exponents [n]
-    stage_rot_exponents<GEN_THREADS>(ex, ap, P.n, amod, twoN);
+    stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
     __syncthreads();
     const size_t round_words = (size_t)4 * P.dG2 * N;
 
@@ -286,7 +288,7 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int k = 0; k < CN; ++k) acc[p][k] = (W)g[p * N + t + GEN_THREADS * k];
+        for (int k = 0; k < CN; ++k) acc[p][k] = (W)g[p * N + t + TH * k];
 
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
@@ -314,14 +316,14 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
                     const int64_t d = (c + K) >> shift;
                     int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
                     if (r < 0) r += Qs;
-                    buf[p * N + t + GEN_THREADS * k] = (W)r;
+                    buf[p * N + t + TH * k] = (W)r;
                 }
             __syncthreads();
             lds_ntt_fwd_r4<W>(buf, N, P.logN, Q, psi, psi_sh);
             // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both output polynomials
 #pragma unroll
             for (int k = 0; k < CN; ++k) {
-                const uint32_t x = t + GEN_THREADS * k;
+                const uint32_t x = t + TH * k;
                 const W d0 = buf[x], d1 = buf[N + x];
 #pragma unroll
                 for (int kk = 0; kk < 2; ++kk)
@@ -337,7 +339,7 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
         // S_j = A_0j * NTT(X^a' - 1) + A_1j * NTT(X^-a' - 1) into buf, then INTT
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
-            const uint32_t x = t + GEN_THREADS * k;
+            const uint32_t x = t + TH * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
             const W mp = mono[ip], mps = mono_sh[ip], mn = mono[in], mns = mono_sh[in];
             const W A00 = reduce_full<W>(A[0][0][k], r1, Q), A01 = reduce_full<W>(A[0][1][k], r1, Q);
@@ -351,16 +353,16 @@ k_blind_rotate_gen2(BRParams P, const W* __restrict__ psi, const W* __restrict__
         for (int p = 0; p < 2; ++p)
 #pragma unroll
             for (int k = 0; k < CN; ++k)  // inverse outputs are in [0, 2Q)
-                acc[p][k] = csub<W>(csub<W>(acc[p][k] + buf[p * N + t + GEN_THREADS * k], 2 * Q), Q);
+                acc[p][k] = csub<W>(csub<W>(acc[p][k] + buf[p * N + t + TH * k], 2 * Q), Q);
         __syncthreads();  // buf is rewritten by the next round
     }
     // acc0 -> transpose (X -> X^-1, poly.cpp:762-770) through LDS, reduced values
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int k = 0; k < CN; ++k) buf[p * N + t + GEN_THREADS * k] = acc[p][k];
+        for (int k = 0; k < CN; ++k) buf[p * N + t + TH * k] = acc[p][k];
     __syncthreads();
-    for (uint32_t k = t; k < N; k += GEN_THREADS) {
+    for (uint32_t k = t; k < N; k += TH) {
         const W v = buf[k == 0 ? 0 : N - k];
         g[k] = (uint64_t)(k == 0 ? v : (v == 0 ? (W)0 : (W)(Q - v)));
         g[N + k] = (uint64_t)buf[N + k];
@@ -1273,9 +1275,10 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
         else go3(uint64_t{});
         return hipGetLastError();
     }
-    if (!v1 && (P.N == 1024 || P.N == 2048)) {
+    if (!v1 && (P.N == 1024 || P.N == 2048 || P.N == 4096 || P.N == 8192)) {
         const size_t lds2 = (size_t)2 * P.N * wb + rot_exponent_bytes(P.n);
-        dim3 grid((unsigned)B), block(GEN_THREADS);
+        if (lds2 > 160 * 1024) return hipErrorNotSupported;
+        dim3 grid((unsigned)B), block(P.N >= 4096 ? 1024 : GEN_THREADS);
         auto go = [&](auto kern, auto tag) {
             using W = decltype(tag);
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
@@ -1283,10 +1286,17 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
                                (const W*)T.ipsi_sh, (const W*)T.mono, (const W*)T.mono_sh, T.eidx, (const W*)bsk,
                                (const W*)bsk_sh, a, amod, acc);
         };
-        if (word_bits == 32)
-            P.N == 1024 ? go(k_blind_rotate_gen2<uint32_t, 4>, uint32_t{}) : go(k_blind_rotate_gen2<uint32_t, 8>, uint32_t{});
-        else
-            P.N == 1024 ? go(k_blind_rotate_gen2<uint64_t, 4>, uint64_t{}) : go(k_blind_rotate_gen2<uint64_t, 8>, uint64_t{});
+        auto pick = [&](auto tag) {
+            using W = decltype(tag);
+            switch (P.N) {
+                case 1024: go(k_blind_rotate_gen2<W, 4>, tag); break;
+                case 2048: go(k_blind_rotate_gen2<W, 8>, tag); break;
+                case 4096: go(k_blind_rotate_gen2<W, 4, 1024>, tag); break;
+                default: go(k_blind_rotate_gen2<W, 8, 1024>, tag); break;  // 8192
+            }
+        };
+        if (word_bits == 32) pick(uint32_t{});
+        else pick(uint64_t{});
         return hipGetLastError();
     }
     const size_t lds = (size_t)(2 + P.dG2) * P.N * wb + rot_exponent_bytes(P.n);

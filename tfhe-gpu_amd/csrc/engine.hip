@@ -929,6 +929,8 @@ tfhe_status run_lwe_batch_v(tfhe_ctx* c, size_t B, const HostIn& in1, const Host
             const int set = (int)(k & 1);
             uint64_t *din1 = io[set], *din2 = has2 ? io[set] + sub * w1 : nullptr, *dout = dout_of(set);
             st = h2d_staged(d, din1, in1.sub(off), b * w1, xs, wb1, pk[set]);
+            if (trace) std::fprintf(stderr, "[tfhe] sub-batch %zu input 1 (%s) staged at %.2f ms\n", k,
+                                    in1.flat ? "flat" : "rows", now() - t0);
             if (st == TFHE_OK && has2) st = h2d_staged(d, din2, in2.sub(off), b * w2, xs, wb2, pk[set] + pk1);
             if (st == TFHE_OK && has_oi)
                 st = h2d_staged(d, dout, out_in.sub(off), b * wo, xs, wbi, pk[set] + pk1 + pk2);

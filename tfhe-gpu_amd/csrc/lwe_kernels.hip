@@ -31,8 +31,8 @@ constexpr int MKM_WAVES = 4;
 template <typename KW> struct MkmAcc { using T = uint64_t; };
 template <> struct MkmAcc<uint16_t> { using T = uint32_t; };  // N*dKS*2^16 < 2^32
 
-template <typename KW>
-__global__ void __launch_bounds__(64 * MKM_WAVES)
+template <typename KW, int WAVES = MKM_WAVES>
+__global__ void __launch_bounds__(64 * WAVES)
 k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, const uint64_t* __restrict__ ext,
       uint64_t fmod, uint64_t* __restrict__ out, size_t B, uint32_t split) {
     constexpr uint32_t VEC = 16 / sizeof(KW);
@@ -43,7 +43,7 @@ k_mkm(KSParams P, const KW* __restrict__ kska, const KW* __restrict__ kskb, cons
     // `split` wavefronts per ciphertext; wave s sweeps the column chunks s, s + split, ...
     // (chunk = 64 * VEC columns)
     const uint32_t chunks = (npad + 64 * VEC - 1) / (64 * VEC);
-    const size_t item = (size_t)blockIdx.x * MKM_WAVES + w;
+    const size_t item = (size_t)blockIdx.x * WAVES + w;
     const size_t ct = item / split;
     const uint32_t first = (uint32_t)(item - ct * split);
     if (ct >= B) return;  // whole wavefront; no workgroup barrier below
@@ -108,35 +108,35 @@ hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const v
                       uint64_t fmod, uint64_t* out, size_t B, hipStream_t s) {
     if (B == 0) return hipSuccess;
     if (P.baseKS > 256) return hipErrorNotSupported;
-    const size_t lds = (size_t)MKM_WAVES * P.N * P.dKS;
+    // u16 keys sum in 32 bits: exact while N dKS (qKS - 1) < 2^32; past that the wrap mod 2^32 is
+    // harmless only when qKS divides 2^32
+    if (ksk_bits == 16 && (unsigned __int128)P.N * P.dKS * (P.qKS - 1) >= ((unsigned __int128)1 << 32) &&
+        (P.qKS & (P.qKS - 1)) != 0)
+        return hipErrorNotSupported;
+    // one wavefront per workgroup when four digit arrays (N dKS bytes each) exceed the LDS: N = 8192
+    const bool one = (size_t)MKM_WAVES * P.N * P.dKS > 160 * 1024;
+    const int waves = one ? 1 : MKM_WAVES;
+    const size_t lds = (size_t)waves * P.N * P.dKS;
     if (lds > 160 * 1024) return hipErrorNotSupported;
     // enough wavefronts for the gather's latency (~4096), but no more: every extra wave per
     // ciphertext widens the rows in flight per coefficient past what the L2 holds
     const size_t vec = 16 / (ksk_bits / 8), chunks = (P.n_pad + 64 * vec - 1) / (64 * vec);
     const uint32_t split = (uint32_t)std::max<size_t>(1, std::min(chunks, (4096 + B - 1) / B));
-    dim3 grid((unsigned)((B * split + MKM_WAVES - 1) / MKM_WAVES)), block(64 * MKM_WAVES);
+    dim3 grid((unsigned)((B * split + waves - 1) / waves)), block(64 * waves);
+    auto go = [&](auto kern, auto tag) {
+        using KW = decltype(tag);
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, grid, block, lds, s, P, (const KW*)kska, (const KW*)kskb, ext, fmod, out, B, split);
+    };
+    auto pick = [&](auto tag) {
+        using KW = decltype(tag);
+        if (one) go(k_mkm<KW, 1>, tag);
+        else go(k_mkm<KW>, tag);
+    };
     switch (ksk_bits) {
-        case 16: {
-            auto k = k_mkm<uint16_t>;
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint16_t*)kska, (const uint16_t*)kskb, ext, fmod, out,
-                               B, split);
-            break;
-        }
-        case 32: {
-            auto k = k_mkm<uint32_t>;
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint32_t*)kska, (const uint32_t*)kskb, ext, fmod, out,
-                               B, split);
-            break;
-        }
-        default: {
-            auto k = k_mkm<uint64_t>;
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(k, grid, block, lds, s, P, (const uint64_t*)kska, (const uint64_t*)kskb, ext, fmod, out,
-                               B, split);
-            break;
-        }
+        case 16: pick(uint16_t{}); break;
+        case 32: pick(uint32_t{}); break;
+        default: pick(uint64_t{}); break;
     }
     return hipGetLastError();
 }

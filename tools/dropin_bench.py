@@ -44,6 +44,8 @@ def main():
                            capture_output=True, text=True, env=env, timeout=900)
         if r.returncode:
             sys.exit(r.stderr[-3000:])
+        if os.environ.get("DROPIN_STDERR"):  # e.g. with TFHE_TRACE=1: the engine's staging timeline
+            open(os.environ["DROPIN_STDERR"], "w").write(r.stderr)
         js = json.loads(r.stdout.strip().splitlines()[-1])
         dropin_out = np.fromfile(fo, dtype=np.uint64).reshape(B, p.n + 1)
     phases = {}
