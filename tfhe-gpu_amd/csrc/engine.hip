@@ -1009,11 +1009,18 @@ tfhe_status create_ctx(const tfhe_params* p, int num_gpus, std::unique_ptr<tfhe_
     int count = 0;
     HCHECK(hipGetDeviceCount(&count));
     if (count < 1) return fail(TFHE_ERR_DEVICE, "no HIP device visible");
+    // Test hook: TFHE_LOGICAL_DEVICES=k presents k logical devices, all on physical device 0, each
+    // with its own arena, streams, scratch and host thread -- the multi-device setup, replication
+    // (peer copies: one RCCL communicator cannot hold a device twice), sharding and error paths
+    // run on a one-GPU box (tests/test_gpu_multidevice.py).  Read per setup.
+    const char* lg = std::getenv("TFHE_LOGICAL_DEVICES");
+    const int logical = lg ? std::atoi(lg) : 0;
+    if (logical > 1) count = logical;
     // GPUSetup(numGPUs): numGPUs <= 0 or more than visible uses every visible device
     // (bootstrapping.cu:736-739)
     if (num_gpus < 1 || num_gpus > count) num_gpus = count;
     c->devs.resize(num_gpus);
-    for (int g = 0; g < num_gpus; ++g) c->devs[g].id = g;
+    for (int g = 0; g < num_gpus; ++g) c->devs[g].id = logical > 1 ? 0 : g;
     out = std::move(c);
     return TFHE_OK;
 }
@@ -1134,7 +1141,9 @@ tfhe_status replicate_arena(tfhe_ctx* c, size_t bytes) {
     if (D < 2) return TFHE_OK;
     const auto t0 = std::chrono::steady_clock::now();
     const char* env = std::getenv("TFHE_REPLICATE");
-    const bool want_rccl = !(env && std::strcmp(env, "peer") == 0);
+    bool want_rccl = !(env && std::strcmp(env, "peer") == 0);
+    for (size_t g = 1; g < D; ++g)  // logical devices sharing one GPU (TFHE_LOGICAL_DEVICES)
+        if (c->devs[g].id == c->devs[0].id) want_rccl = false;
     bool done = false;
     if (want_rccl && rccl().ok) {
         const RcclApi& R = rccl();
