@@ -823,7 +823,7 @@ tfhe_status ensure_flags(Device& d, size_t words) {
     if (words <= d.flags_words) return TFHE_OK;
     if (d.flags) HCHECK(hipHostFree(d.flags));
     d.flags = nullptr, d.flags_words = 0;
-    HCHECK(hipHostMalloc((void**)&d.flags, words * 4, hipHostMallocCoherent | hipHostMallocMapped));
+    HCHECK(hipHostMalloc((void**)&d.flags, words * 4, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
     d.flags_words = words;
     return TFHE_OK;
 }

@@ -22,6 +22,7 @@
 #include "device_math.hpp"
 #include "kernels.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -92,11 +93,15 @@ __device__ __forceinline__ uint64_t word_of<uint64_t>(const u32x4& u, int v) {
 // thread and stage.  Block mapping: blocks b and b + 8 run on one XCD (round-robin
 // dealing), so consecutive blocks of one XCD take the ciphertext tiles of ONE column tile:
 // they stream the same KSK segments at about the same time and share them in that XCD's L2.
+// Split over the steps (small batches: too few ciphertext x column tiles to fill the chip): the
+// blocks of split z sum stages [z S, (z + 1) S) and store their partial sums (u64, column n = the
+// B sum) in part[z][ct][n + 1]; k_ks_combine adds the splits and finishes.  nsplit = 1 finishes here.
 template <typename KW, typename ACC, int CT, int CTS, int MAXL, int G>
 __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __restrict__ kska,
                                                  const KW* __restrict__ kskb, const uint32_t* __restrict__ dig,
                                                  const uint64_t* __restrict__ bq, size_t B, size_t Bp, uint32_t nct,
-                                                 uint32_t ncol, uint64_t fmod, uint64_t* __restrict__ out) {
+                                                 uint32_t ncol, uint64_t fmod, uint64_t* __restrict__ out,
+                                                 uint32_t nsplit, uint64_t* __restrict__ part) {
     constexpr int VEC = 16 / sizeof(KW);           // KSK words per 16-byte piece
     constexpr int PIECES = CT / VEC;               // pieces per row segment
     constexpr int STRIDE = CT * sizeof(KW) + 16;   // LDS row pitch: consecutive rows start 4 banks apart
@@ -105,7 +110,8 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     extern __shared__ __align__(16) unsigned char sm[];
     const uint32_t bks = P.baseKS, dks = P.dKS, npad = P.n_pad, n = P.n;
     const uint32_t th = threadIdx.x;
-    const uint32_t L = blockIdx.x, k = L >> 3;
+    const uint32_t per_split = gridDim.x / nsplit, split = blockIdx.x / per_split;
+    const uint32_t L = blockIdx.x - split * per_split, k = L >> 3;
     const uint32_t col_tile = (k / nct) * 8 + (L & 7), ct_tile = k % nct;
     if (col_tile >= ncol) return;  // whole workgroup
     const uint32_t c0 = col_tile * CT;
@@ -186,23 +192,24 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     }
 #pragma unroll
     for (int st = 0; st < G; ++st) bX[st] = bY[st] = 0;
-    const uint32_t stages = P.N * dks / G;  // even (ks_tiled_supported)
-    KS_LOAD(stgX, bX, dX, 0u);
-    KS_LOAD(stgY, bY, dY, 1u);
-    for (uint32_t g = 0; g < stages; g += 2) {
+    const uint32_t stages = P.N * dks / G;  // even (ks_tiled_supported); nsplit divides stages / 2
+    const uint32_t s_len = stages / nsplit, s_lo = split * s_len, s_hi = s_lo + s_len;
+    KS_LOAD(stgX, bX, dX, s_lo);
+    KS_LOAD(stgY, bY, dY, s_lo + 1);
+    for (uint32_t g = s_lo; g < s_hi; g += 2) {
         // the last two stages reload their own rows (unconditional loads keep the counts exact)
         KS_STORE(stgX, bX, g);
         uint32_t dXc[CTS];
 #pragma unroll
         for (int c = 0; c < CTS; ++c) dXc[c] = dX[c];
-        KS_LOAD(stgX, bX, dX, min(g + 2, stages - 2));
+        KS_LOAD(stgX, bX, dX, min(g + 2, s_hi - 2));
         __syncthreads();
         KS_SUM(dXc, g);
         KS_STORE(stgY, bY, g + 1);
         uint32_t dYc[CTS];
 #pragma unroll
         for (int c = 0; c < CTS; ++c) dYc[c] = dY[c];
-        KS_LOAD(stgY, bY, dY, min(g + 3, stages - 1));
+        KS_LOAD(stgY, bY, dY, min(g + 3, s_hi - 1));
         __syncthreads();
         KS_SUM(dYc, g + 1);
     }
@@ -210,6 +217,19 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
 #undef KS_STORE
 #undef KS_SUM
 
+    if (nsplit > 1) {  // partial sums for k_ks_combine
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) {
+            const size_t ct = t0 + th + KT * c;
+            if (ct >= B) continue;
+            uint64_t* o = part + ((size_t)split * B + ct) * (size_t)(n + 1);
+#pragma unroll
+            for (int kk = 0; kk < CT; ++kk)
+                if (c0 + kk < n) o[c0 + kk] = (uint64_t)acc[c][kk];
+            if (bcol) o[n] = bsum[c];
+        }
+        return;
+    }
     const uint64_t qks = P.qKS;
 #pragma unroll
     for (int c = 0; c < CTS; ++c) {
@@ -231,9 +251,42 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     }
 }
 
+// sum of the splits' partial sums (u64; u32 partials that wrapped mod 2^32 only when qKS divides
+// 2^32, launch_ks_tiled), then the key switch's finish as in k_ks_tiled
+__global__ void __launch_bounds__(256) k_ks_combine(KSParams P, const uint64_t* __restrict__ part, uint32_t nsplit,
+                                                    const uint64_t* __restrict__ bq, size_t B, uint64_t fmod,
+                                                    uint64_t* __restrict__ out) {
+    const uint32_t n = P.n;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * (n + 1)) return;
+    const size_t ct = i / (n + 1);
+    const uint32_t col = (uint32_t)(i - ct * (n + 1));
+    uint64_t sum = 0;
+    for (uint32_t z = 0; z < nsplit; ++z) sum += part[(size_t)z * B * (n + 1) + i];
+    const uint64_t qks = P.qKS, r = sum % qks;
+    if (col < n) {
+        out[i] = round_qQ(r == 0 ? 0 : qks - r, fmod, qks);  // 0 - sum
+    } else {
+        const uint64_t x = bq[ct];
+        out[i] = round_qQ(x >= r ? x - r : x + (qks - r), fmod, qks);  // b - sum
+    }
+}
+
+// Splits for a batch: enough blocks for two per CU (512), at most kMaxSplit, dividing the stage pairs
+constexpr uint32_t kMaxSplit = 4, kSplitMaxB = 2048;
+uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B) {
+    const char* e = std::getenv("TFHE_KS_SPLIT");  // A/B runs (read per call): 1 = no split
+    const uint32_t cap = e ? (uint32_t)std::max(1, std::atoi(e)) : kMaxSplit;
+    const uint32_t pairs = P.N * P.dKS / (2 * GMAX);
+    uint32_t z = 1;
+    while (2 * z <= std::min(cap, kMaxSplit) && B <= kSplitMaxB && blocks * z < 512 && pairs % (2 * z) == 0) z *= 2;
+    return z;
+}
+
 template <typename KW, typename ACC, int CT, int CTS, int G = 4>
 hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, const uint32_t* dig,
-                        const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, hipStream_t s) {
+                        const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, uint64_t* part,
+                        hipStream_t s) {
     constexpr int STRIDE = CT * sizeof(KW) + 16;
     const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
     const size_t lpt = ((size_t)G * P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT;
@@ -245,8 +298,14 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = (P.n_pad + CT - 1) / CT;
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp, nct,
-                       ncol, fmod, out);
+    const uint32_t nsplit = ks_nsplit(P, blocks, B);
+    hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp,
+                       nct, ncol, fmod, out, nsplit, part);
+    if (nsplit > 1) {
+        const size_t words = B * (P.n + 1);
+        hipLaunchKernelGGL(k_ks_combine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, part, nsplit, bq,
+                           B, fmod, out);
+    }
     return hipGetLastError();
 }
 
@@ -256,9 +315,13 @@ size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; 
 
 }  // namespace
 
+size_t ks_tiled_part_words(const KSParams& P, size_t B) {  // split partial sums (ks_nsplit)
+    return (size_t)kMaxSplit * std::min(B, (size_t)kSplitMaxB) * (P.n + 1);
+}
+
 size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
     const size_t Bp = ks_tiled_bp(B);
-    return (size_t)P.N * P.dKS * Bp + Bp * sizeof(uint64_t);
+    return (size_t)P.N * P.dKS * Bp + Bp * sizeof(uint64_t) + ks_tiled_part_words(P, B) * sizeof(uint64_t);
 }
 
 bool ks_tiled_supported(const KSParams& P) {
@@ -276,6 +339,7 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     const size_t Bp = ks_tiled_bp(B);
     uint32_t* dig = static_cast<uint32_t*>(scratch);
     uint64_t* bq = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(scratch) + (size_t)P.N * P.dKS * Bp);
+    uint64_t* part = bq + Bp;
     const size_t lds_dig = (size_t)P.dKS * DIG_TILE * DIG_TILE;
     hipError_t e = hipFuncSetAttribute((const void*)k_ks_digits, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig);
     if (e != hipSuccess) return e;
@@ -286,16 +350,17 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     const int cts = ev ? std::atoi(ev) : 1;
     switch (ksk_bits) {
         case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
-            return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+            return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
         case 32:
-            if (acc32)
-                return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
-                                : launch_tiled<uint32_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
-            return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
-                            : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+            // u32 sums also when they wrap mod 2^32 harmlessly: qKS a power of two (STD128Q: 2^25)
+            if (acc32 || (P.qKS & (P.qKS - 1)) == 0)
+                return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
+                                : launch_tiled<uint32_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
+            return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
+                            : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
         default:
-            return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s)
-                            : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, s);
+            return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
+                            : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
     }
 }
 
