@@ -30,6 +30,8 @@ namespace tfhe {
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a native vector: stays in registers
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));  // two packed u16 column sums (v_pk_add_u16)
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));  // a 16-byte piece of u16 key words
 
 constexpr int KT = 256;         // threads per workgroup
 constexpr int DIG_TILE = 64;    // ciphertexts x coefficients per k_ks_digits block
@@ -96,7 +98,10 @@ __device__ __forceinline__ uint64_t word_of<uint64_t>(const u32x4& u, int v) {
 // Split over the steps (small batches: too few ciphertext x column tiles to fill the chip): the
 // blocks of split z sum stages [z S, (z + 1) S) and store their partial sums (u64, column n = the
 // B sum) in part[z][ct][n + 1]; k_ks_combine adds the splits and finishes.  nsplit = 1 finishes here.
-template <typename KW, typename ACC, int CT, int CTS, int MAXL, int G>
+// PK (u16 keys, qKS a power of two <= 2^16): the column sums are kept mod 2^16 as packed u16 pairs --
+// each 16-byte piece of 8 key words is 4 v_pk_add_u16, with no unpacking -- which is exact mod qKS
+// because qKS divides 2^16.
+template <typename KW, typename ACC, int CT, int CTS, int MAXL, int G, bool PK = false>
 __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __restrict__ kska,
                                                  const KW* __restrict__ kskb, const uint32_t* __restrict__ dig,
                                                  const uint64_t* __restrict__ bq, size_t B, size_t Bp, uint32_t nct,
@@ -106,6 +111,7 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     constexpr int PIECES = CT / VEC;               // pieces per row segment
     constexpr int STRIDE = CT * sizeof(KW) + 16;   // LDS row pitch: consecutive rows start 4 banks apart
     static_assert(CT % VEC == 0, "column tile is whole pieces");
+    static_assert(!PK || sizeof(KW) == 2, "packed sums are for u16 keys");
     static_assert(G == 2 || G == 4, "a stage is half or all of a digit word");
     extern __shared__ __align__(16) unsigned char sm[];
     const uint32_t bks = P.baseKS, dks = P.dKS, npad = P.n_pad, n = P.n;
@@ -170,8 +176,16 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
                 const unsigned char* r = b_ + st * step_bytes + d * STRIDE;                         \
                 _Pragma("unroll") for (int p = 0; p < PIECES; ++p) {                                \
                     const u32x4 u = *reinterpret_cast<const u32x4*>(r + p * 16);                    \
-                    _Pragma("unroll") for (int v = 0; v < VEC; ++v)                                 \
-                        acc[c][p * VEC + v] += (ACC)word_of<KW>(u, v);                              \
+                    if constexpr (PK) {                                                             \
+                        const u16x8 h = *reinterpret_cast<const u16x8*>(r + p * 16);                \
+                        apk[c][4 * p + 0] += __builtin_shufflevector(h, h, 0, 1);                   \
+                        apk[c][4 * p + 1] += __builtin_shufflevector(h, h, 2, 3);                   \
+                        apk[c][4 * p + 2] += __builtin_shufflevector(h, h, 4, 5);                   \
+                        apk[c][4 * p + 3] += __builtin_shufflevector(h, h, 6, 7);                   \
+                    } else {                                                                        \
+                        _Pragma("unroll") for (int v = 0; v < VEC; ++v)                             \
+                            acc[c][p * VEC + v] += (ACC)word_of<KW>(u, v);                          \
+                    }                                                                               \
                 }                                                                                   \
                 if (bcol) bsum[c] += (uint64_t)bb[(((gg) & 1) * G + st) * bks + d];                 \
             }                                                                                       \
@@ -182,14 +196,22 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     u32x4 stgX[MAXL], stgY[MAXL];
     BW bX[G], bY[G];
     uint32_t dX[CTS], dY[CTS];
-    ACC acc[CTS][CT];
+    ACC acc[CTS][PK ? 1 : CT];
+    u16x2 apk[CTS][PK ? CT / 2 : 1];
     uint64_t bsum[CTS];
 #pragma unroll
     for (int c = 0; c < CTS; ++c) {
         bsum[c] = 0;
 #pragma unroll
-        for (int kk = 0; kk < CT; ++kk) acc[c][kk] = 0;
+        for (int kk = 0; kk < (PK ? 1 : CT); ++kk) acc[c][kk] = 0;
+#pragma unroll
+        for (int kk = 0; kk < (PK ? CT / 2 : 1); ++kk) apk[c][kk] = u16x2{0, 0};
     }
+    // column kk's sum (PK: mod 2^16)
+    auto colsum = [&](int c, int kk) -> uint64_t {
+        if constexpr (PK) return (uint64_t)apk[c][kk >> 1][kk & 1];
+        else return (uint64_t)acc[c][kk];
+    };
 #pragma unroll
     for (int st = 0; st < G; ++st) bX[st] = bY[st] = 0;
     const uint32_t stages = P.N * dks / G;  // even (ks_tiled_supported); nsplit divides stages / 2
@@ -225,7 +247,7 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
             uint64_t* o = part + ((size_t)split * B + ct) * (size_t)(n + 1);
 #pragma unroll
             for (int kk = 0; kk < CT; ++kk)
-                if (c0 + kk < n) o[c0 + kk] = (uint64_t)acc[c][kk];
+                if (c0 + kk < n) o[c0 + kk] = colsum(c, kk);
             if (bcol) o[n] = bsum[c];
         }
         return;
@@ -240,7 +262,7 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
         for (int kk = 0; kk < CT; ++kk) {
             const uint32_t col = c0 + kk;
             if (col < n) {
-                const uint64_t r = (uint64_t)acc[c][kk] % qks;
+                const uint64_t r = colsum(c, kk) % qks;
                 o[col] = round_qQ(r == 0 ? 0 : qks - r, fmod, qks);  // 0 - sum
             }
         }
@@ -283,7 +305,7 @@ uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B) {
     return z;
 }
 
-template <typename KW, typename ACC, int CT, int CTS, int G = 4>
+template <typename KW, typename ACC, int CT, int CTS, int G = 4, bool PK = false>
 hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, const uint32_t* dig,
                         const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, uint64_t* part,
                         hipStream_t s) {
@@ -291,8 +313,8 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
     const size_t lpt = ((size_t)G * P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT;
     if (lds > 80 * 1024 || lpt > 8) return hipErrorNotSupported;
-    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2, G> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4, G>
-                                                                     : k_ks_tiled<KW, ACC, CT, CTS, 8, G>;
+    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2, G, PK> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4, G, PK>
+                                                                         : k_ks_tiled<KW, ACC, CT, CTS, 8, G, PK>;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
@@ -350,6 +372,10 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     const int cts = ev ? std::atoi(ev) : 1;
     switch (ksk_bits) {
         case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
+            // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (TFHE_KS_PK=0: u32 sums, A/B runs)
+            if ((P.qKS & (P.qKS - 1)) == 0 && P.qKS <= (1u << 16) && !(std::getenv("TFHE_KS_PK") &&
+                                                                        std::getenv("TFHE_KS_PK")[0] == '0'))
+                return launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
             return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
         case 32:
             // u32 sums also when they wrap mod 2^32 harmlessly: qKS a power of two (STD128Q: 2^25)
