@@ -186,7 +186,7 @@ def cpu_baseline_reference(p, seconds, gpu_sample):
 
     threads, visible = host_threads()
     g1, g2, gout = gpu_sample
-    per_gate_s = 0.3  # single-thread OpenFHE STD128 gate, measured here (0.144-0.27 s)
+    per_gate_s = 0.12  # one OpenFHE STD128 gate per thread on the GPU box (profiles/r03z: 800 pairs, 16 threads, 5.9 s)
     K = max(len(g1), int(seconds * threads / per_gate_s))
     rs = np.random.default_rng(5)
     c1 = np.concatenate([g1, rs.integers(0, p.q, (K - len(g1), p.n + 1), dtype=np.uint64)])
