@@ -375,9 +375,7 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
             // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (TFHE_KS_PK=0: u32 sums, A/B runs)
             if ((P.qKS & (P.qKS - 1)) == 0 && P.qKS <= (1u << 16) && !(std::getenv("TFHE_KS_PK") &&
                                                                         std::getenv("TFHE_KS_PK")[0] == '0'))
-                return cts == 4   ? launch_tiled<uint16_t, uint32_t, 32, 4, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
-                       : cts == 2 ? launch_tiled<uint16_t, uint32_t, 32, 2, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
-                                  : launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
+                return launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
             return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
         case 32:
             // u32 sums also when they wrap mod 2^32 harmlessly: qKS a power of two (STD128Q: 2^25)
