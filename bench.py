@@ -426,6 +426,13 @@ def main():
         valu["held_clock_ghz"] = round(gui / 8 / (pass_ns * 1e-9 if pass_ns else br_ms * 1e-3) / 1e9, 2)
         valu["note"] += ("; busy_frac = SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8); held_clock_ghz = "
                          "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass, MI355X_MICROARCH.md 'DVFS give-back')")
+        if peak_mm and peak_src.get("held_clock_ghz"):
+            # the same peak scaled to the clock the part holds under this kernel (power-limited): how much
+            # of the gap is issue efficiency and how much is clock
+            peak_k = peak_mm * valu["held_clock_ghz"] / peak_src["held_clock_ghz"]
+            roofline["frac_at_kernel_clock"] = round(achieved_mm / peak_k, 3)
+            roofline["note"] += (f"; frac_at_kernel_clock = achieved / (peak x {valu['held_clock_ghz']} GHz held under "
+                                 f"the kernel / {peak_src['held_clock_ghz']} GHz held under the microbenchmark)")
 
     # ---- the same gates through the host-array entry point (PCIe + host staging included) ----
     host_array = None
