@@ -1152,10 +1152,11 @@ tfhe_status replicate_arena(tfhe_ctx* c, size_t bytes) {
         for (size_t g = 0; g < D; ++g) ids[g] = c->devs[g].id;
         if (R.init_all(comms.data(), (int)D, ids.data()) == ncclSuccess) {
             ncclResult_t r = R.group_start();
-            for (size_t g = 0; g < D && r == ncclSuccess; ++g) {
+            for (size_t g = 0; g < D && r == ncclSuccess; ++g) {  // no early return inside the group
                 Device& d = c->devs[g];
-                HCHECK(hipSetDevice(d.id));
-                r = R.bcast(c->devs[0].arena, d.arena, bytes, ncclUint8, 0, comms[g], d.stream);
+                r = hipSetDevice(d.id) == hipSuccess
+                        ? R.bcast(c->devs[0].arena, d.arena, bytes, ncclUint8, 0, comms[g], d.stream)
+                        : ncclUnhandledCudaError;
             }
             const ncclResult_t r2 = R.group_end();
             bool synced = r == ncclSuccess && r2 == ncclSuccess;
