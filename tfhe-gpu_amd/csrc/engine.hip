@@ -671,9 +671,15 @@ tfhe_status run_shards(size_t D, size_t B, Select&& select, Body&& body) {
         size_t lo, cnt;
         shard_span(B, D, g, &lo, &cnt);
         th.emplace_back([&, g, lo, cnt] {
-            st[g] = select(g);
-            if (st[g] == TFHE_OK && cnt > 0) st[g] = body(g, lo, cnt);
-            if (st[g] != TFHE_OK) msg[g] = g_last_error;  // thread_local: this thread's message
+            try {  // an exception must not leave a worker thread (std::terminate)
+                st[g] = select(g);
+                if (st[g] == TFHE_OK && cnt > 0) st[g] = body(g, lo, cnt);
+                if (st[g] != TFHE_OK) msg[g] = g_last_error;  // thread_local: this thread's message
+            } catch (const std::exception& e) {
+                st[g] = TFHE_ERR_INTERNAL, msg[g] = e.what();
+            } catch (...) {
+                st[g] = TFHE_ERR_INTERNAL, msg[g] = "unknown exception";
+            }
         });
     }
     for (auto& t : th) t.join();
