@@ -93,3 +93,22 @@ def test_default_threshold_routes_small_batches_to_gather(ks_ctx):
     assert np.array_equal(a, b)
     one = _with_min("1", lambda: ctx.MKMSwitch(ext[:1], op.q))
     assert np.array_equal(one, orc.mkm_switch(np.ascontiguousarray(ext[:1]), op.q))
+
+
+@pytest.mark.parametrize("cts", ["1", "2"])
+def test_tiled_keyswitch_ciphertexts_per_thread(ks_ctx, cts):
+    """Both tile depths (one or two ciphertexts per thread; the default picks by key width and
+    batch) equal the gather form."""
+    name, op, ctx, orc = ks_ctx
+    ext = _ext(op, 1029, 13)
+    old = os.environ.get("TFHE_KS_CTS")
+    os.environ["TFHE_KS_CTS"] = cts
+    try:
+        tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, op.q))
+    finally:
+        if old is None:
+            os.environ.pop("TFHE_KS_CTS")
+        else:
+            os.environ["TFHE_KS_CTS"] = old
+    gather = _with_min("0", lambda: ctx.MKMSwitch(ext, op.q))
+    assert np.array_equal(tiled, gather)

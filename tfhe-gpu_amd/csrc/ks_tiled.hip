@@ -368,8 +368,12 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     // every ciphertext tile of Bp gets digits (zeros past B), so k_ks_tiled reads no garbage
     const dim3 g1((unsigned)(Bp / DIG_TILE), (P.N + 1 + DIG_TILE - 1) / DIG_TILE);
     hipLaunchKernelGGL(k_ks_digits, g1, dim3(256), lds_dig, s, P, ext, dig, bq, B, Bp);
-    const char* ev = std::getenv("TFHE_KS_CTS");  // ciphertexts per thread (A/B runs)
-    const int cts = ev ? std::atoi(ev) : 1;
+    // ciphertexts per thread: two halve the KSK segments streamed per ciphertext; they pay for u64 keys
+    // (ARB12 B = 4096 13.8 -> 12.5 ms, logQ = 23 B = 1024 4.06 -> 3.66) and for u32 keys at large
+    // batches (STD192 8192 5.81 -> 5.24), not for STD128Q at 1024 (1.26 -> 1.40) or the packed u16
+    // form (profiles/r03ks, r03ks2, r03z).  TFHE_KS_CTS overrides (A/B runs and tests; read per call).
+    const char* ev = std::getenv("TFHE_KS_CTS");
+    const int cts = ev ? std::atoi(ev) : (ksk_bits == 64 || (ksk_bits == 32 && B >= 4096)) ? 2 : 1;
     switch (ksk_bits) {
         case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
             // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (TFHE_KS_PK=0: u32 sums, A/B runs)
