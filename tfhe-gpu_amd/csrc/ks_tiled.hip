@@ -127,30 +127,47 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     const uint32_t stage_bytes = G * step_bytes;
     KW* bb = reinterpret_cast<KW*>(sm + 2 * stage_bytes);  // [2][G][baseKS] B entries
     const uint32_t npieces = bks * PIECES;                  // per step
-    const uint32_t total = G * npieces;                     // per stage
 
-    // Staging is branch-free (clamped addresses, no exec-masked loads), so the compiler's
-    // wait counters stay exact, and written without lambdas, so the staging registers are not
-    // demoted to scratch.  Two register sets (X, Y) alternate: the rows of stage g+2 are issued
-    // while those of g+1 are in flight.  Pieces past n_pad read in-row words of another column
-    // instead of zeros: those columns (>= n_pad >= n) are never written out.
+    // Staging slots: slot l of a thread moves one 16-byte piece of step st_l = l / lps of a stage
+    // (lps = slots per step, uniform), piece r = (l % lps) KT + th of that step's baseKS x PIECES.
+    // Everything lane-dependent (the piece's offset in its step's KSK block and in LDS) is fixed for
+    // the whole launch; per stage only the uniform step bases change (scalar arithmetic: s / dKS by
+    // a magic multiply, exact for s < 2^32 / dKS), so a staged load is one global_load with a scalar
+    // base and a 32-bit lane offset.  Loads are branch-free (clamped pieces, no exec-masked loads),
+    // so the compiler's wait counters stay exact, and written without lambdas, so the staging
+    // registers are not demoted to scratch.  Two register sets (X, Y) alternate: the rows of stage
+    // g+2 are issued while those of g+1 are in flight.  Pieces past n_pad read in-row words of
+    // another column instead of zeros: those columns (>= n_pad >= n) are never written out.
+    const uint32_t lps = (npieces + KT - 1) / KT;
+    const uint64_t dmagic = ((1ull << 32) + dks - 1) / dks;  // ceil(2^32 / dKS)
+    const uint32_t bd = bks * dks;
+    uint32_t st_of[MAXL], loff[MAXL], sto[MAXL];  // step (uniform), KSK lane offset (bytes), LDS offset
+#pragma unroll
+    for (int l = 0; l < MAXL; ++l) {
+        const uint32_t st = (uint32_t)l / lps, r = ((uint32_t)l - st * lps) * KT + th;
+        const uint32_t rr = min(r, npieces - 1);
+        const uint32_t v = rr / PIECES, pc = rr - v * PIECES;
+        const uint32_t col = min(c0 + pc * VEC, npad - VEC);
+        st_of[l] = min(st, (uint32_t)G - 1);
+        loff[l] = (v * dks * npad + col) * (uint32_t)sizeof(KW);
+        sto[l] = (st < (uint32_t)G && r < npieces) ? st * step_bytes + v * STRIDE + pc * 16 : ~0u;
+    }
+    const uint32_t vb = min(th, bks - 1) * dks;  // B column: this lane's row v, in KW words
 #define KS_LOAD(STG, BSTG, DGV, gg)                                                                 \
     do {                                                                                            \
         _Pragma("unroll") for (int c = 0; c < CTS; ++c)                                             \
             DGV[c] = dig[(size_t)((gg) * G / 4) * Bp + t0 + th + KT * c] >> (8 * (((gg) * G) % 4)); \
         _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
-            const uint32_t idx = min(th + l * KT, total - 1);                                       \
-            const uint32_t st = idx / npieces, r = idx - st * npieces;                              \
-            const uint32_t v = r / PIECES, pc = r - v * PIECES;                                     \
-            const uint32_t s_ = (gg) * G + st, i = s_ / dks, j = s_ - i * dks;                      \
-            const uint32_t col = min(c0 + pc * VEC, npad - VEC);                                    \
-            STG[l] = *reinterpret_cast<const u32x4*>(kska + (((size_t)i * bks + v) * dks + j) * npad + col); \
+            const uint32_t s_ = (gg) * G + st_of[l];                                                \
+            const uint32_t i = (uint32_t)(((uint64_t)s_ * dmagic) >> 32), j = s_ - i * dks;         \
+            const char* pb = reinterpret_cast<const char*>(kska) + ((size_t)i * bd + j) * npad * sizeof(KW); \
+            STG[l] = *reinterpret_cast<const u32x4*>(pb + loff[l]);                                 \
         }                                                                                           \
         if (bcol) {                                                                                 \
-            const uint32_t v = min(th, bks - 1);                                                    \
             _Pragma("unroll") for (int st = 0; st < G; ++st) {                                      \
-                const uint32_t s_ = (gg) * G + st, i = s_ / dks, j = s_ - i * dks;                  \
-                BSTG[st] = kskb[((size_t)i * bks + v) * dks + j];                                   \
+                const uint32_t s_ = (gg) * G + st;                                                  \
+                const uint32_t i = (uint32_t)(((uint64_t)s_ * dmagic) >> 32), j = s_ - i * dks;     \
+                BSTG[st] = kskb[(size_t)i * bd + j + vb];                                           \
             }                                                                                       \
         }                                                                                           \
     } while (0)
@@ -158,10 +175,7 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     do {                                                                                            \
         unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                          \
         _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
-            const uint32_t idx = th + l * KT;                                                       \
-            const uint32_t st = idx / npieces, r = idx - st * npieces;                              \
-            const uint32_t v = r / PIECES, pc = r - v * PIECES;                                     \
-            if (idx < total) *reinterpret_cast<u32x4*>(b_ + st * step_bytes + v * STRIDE + pc * 16) = STG[l]; \
+            if (sto[l] != ~0u) *reinterpret_cast<u32x4*>(b_ + sto[l]) = STG[l];                     \
         }                                                                                           \
         if (bcol && th < bks) {                                                                     \
             _Pragma("unroll") for (int st = 0; st < G; ++st) bb[(((gg) & 1) * G + st) * bks + th] = BSTG[st]; \
@@ -311,7 +325,8 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
                         hipStream_t s) {
     constexpr int STRIDE = CT * sizeof(KW) + 16;
     const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
-    const size_t lpt = ((size_t)G * P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT;
+    // staging slots per thread and stage: G steps, ceil(pieces per step / KT) slots each (k_ks_tiled)
+    const size_t lpt = (size_t)G * ((P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT);
     if (lds > 80 * 1024 || lpt > 8) return hipErrorNotSupported;
     auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2, G, PK> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4, G, PK>
                                                                          : k_ks_tiled<KW, ACC, CT, CTS, 8, G, PK>;
