@@ -362,7 +362,9 @@ size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
 }
 
 bool ks_tiled_supported(const KSParams& P) {
-    return P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (8 * GMAX) == 0;  // even stage count
+    // even stage count; step indices s < N dKS far below 2^32 / dKS (k_ks_tiled's magic-multiply s / dKS)
+    return P.dKS >= 1 && P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (8 * GMAX) == 0 &&
+           (uint64_t)P.N * P.dKS < (1ull << 24);
 }
 
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
