@@ -828,7 +828,8 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 if (t == 0) wflag[(i + 1) & 1] = 0;
                 if (wv) wflag[i & 1] = 1;
             }
-            if (sync) __syncthreads();  // other waves may still read their blocks
+            // other waves may still read their blocks (PROBE bit 2: timing experiment without it)
+            if (sync && !(PROBE & 4)) __syncthreads();
             if (!CORR && l + 1 == LD) f64w_ntt_fwd<RED, true>(buf, v, d, psi, K);
             else f64w_ntt_fwd<RED>(buf, v, d, psi, K);
         };
@@ -1093,6 +1094,12 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             const char* e = std::getenv("TFHE_F64W_PROBE");
             return e && e[0] ? e[0] - '0' : 0;
         }();
+        if (probe == 4) {  // timing only (results invalid): STD192 without the barrier before digit 1's pass A
+            const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
+            if (!(x && x[0] == '1') || red || wrap || ld != 2 || mtw != 3) return hipErrorInvalidValue;
+            go(k_blind_rotate_f64w<false, false, 2, 3, 4>);
+            return hipGetLastError();
+        }
         if (probe != 0) {  // STD128Q's instance only
             if (!(red && wrap && ld == 1 && mtw == 3)) return hipErrorInvalidValue;
             if (probe == 2) go(k_blind_rotate_f64w<true, true, 1, 3, 2>);
