@@ -1,45 +1,54 @@
 #!/usr/bin/env python3
-"""bench.py -- bootstraps/sec of the batched STD128 GINX bootstrap on MI355X.
+"""bench.py -- bootstraps/sec of the batched GINX bootstrap on MI355X.
 
-Workload (BASELINE.json configs[1]): STD128 (n=512, N=1024, Q=2^27-2^11+1,
-baseG=2^7) EvalBinGate(NAND), batch 8192 per GPU.  One step = one vector
-EvalBinGate call over the batch with both input vectors already resident in HBM:
-test vector -> blind rotation (n external products) -> extraction -> MKM, all on
-device (the fused tfhe_eval_bin_gate_device entry point).  One bootstrap per gate.
+Default workload (BASELINE.json configs[1], "C2"): STD128 (n=512, N=1024, Q=2^27-2^11+1,
+baseG=2^7) EvalBinGate(NAND), batch 8192 per GPU.  One step = one vector EvalBinGate call
+over the batch with both input vectors already resident in HBM: test vector -> blind
+rotation (n external products) -> extraction -> MKM, all on device (the fused
+tfhe_eval_bin_gate_device entry point).  One bootstrap per gate.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-one process per GPU; the key image is built once on rank 0 and broadcast over
-RCCL/xGMI (torch.distributed, backend "nccl" = RCCL), then every rank bootstraps
-its own 8192-ciphertext shard with no data-path collective (weak scaling).
+--config selects the other SURVEY.md 8(d) configurations, measured the same way (device-resident
+step, the dominant kernel timed alone, the matching VALU peak, PMC from a per-config record, the
+reference's CPU path on the same context, keys and inputs):
+  C3   STD128 arbFunc logQ=12 throw=1, EvalFunc(x^3 mod 8) (arbitrary LUT: 2 bootstraps), 4096 per GPU
+  C4   STD192 EvalBinGate(NAND), 8192 per GPU (65536 on 8 GPUs)
+  C5a  STD128Q EvalSign, ciphertext modulus 2^23 (15 bootstraps each), 1024 in all (strong scaling)
+  C5b  STD128 logQ=23 throw=1 EvalSign, modulus 2^23 (7 bootstraps each), 1024 in all (strong scaling)
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process
+per GPU; the key image is built once on rank 0 and broadcast over RCCL/xGMI (torch.distributed,
+backend "nccl" = RCCL), then every rank bootstraps its own shard with no data-path collective.
+WORLD_SIZE must equal --gpus (exit status 2 otherwise).
 
 Extra JSON fields:
-  roofline      the blind-rotation kernel (the dominant one), timed alone with HIP
-                events on its stream.  Its bound is integer VALU issue:
-                bound "valu-int", achieved = the algorithmic modular multiplies of
-                SURVEY 8(d) (n[(dG2+2)(N/2)log2 N + 4 dG2 N + 4N] per bootstrap) per
-                second, peak = the microbenchmarked signed-Montgomery modmul rate of
-                gfx950 (tools/microbench/valu_rates.hip, --valu-peak-json), frac = their
-                ratio.  traffic = PMC HBM bytes per launch (rocprofv3 FETCH_SIZE x2 +
-                WRITE_SIZE, MI355X_MICROARCH.md corrections; --pmc-json), hbm_frac =
-                traffic / kernel time / 8 TB/s, effective_keystream_tbs = SURVEY B_alg
-                (BSK + KS gather + LWE I/O per bootstrap, no cross-ciphertext reuse) x
-                batch / kernel time.
-  valu          PMC view of the same kernel: VALU instructions, issue and busy
-                fractions, the clock the part held under it.
-  host_array    the same gates through the host-array entry point (tfhe_eval_bin_gate:
-                PCIe copies, pinned staging and the host thread included), same inputs.
-  dropin        the reference's own, unchanged vector EvalBinGate (OpenFHE BinFHE code compiled from
-                its sources, oracle/_ref/ref_dropin) running on this GPU through the drop-in shim
-                (tfhe-gpu_amd/shim/bootstrapping_hip.cpp -> the seven boundary symbols): end-to-end
-                bootstraps/s of the unchanged caller, the shim's own time per call (marshalling +
-                device, TFHE_SHIM_TIMING) against the host-array API, and its outputs checked
-                against the benchmarked device-resident outputs (same keys, same inputs).
-  cpu_baseline  the REFERENCE's own OpenFHE CPU path (oracle/_ref/ref_kat: the
-                unchanged vector EvalBinGate with the reference's CPU accumulator and
-                key switch behind the GPU symbols, OpenMP over ciphertexts) on a bounded
-                sample of the same workload with the same keys on this host's cores
-                (rank 0, N = 1 only), which also checks the benchmarked GPU outputs bit
-                for bit; the C restatement (oracle/) when ref_kat is not built.
+  dist          backend and world size torch.distributed reports, per-rank blind-rotation kernel
+                times (max / min), the key broadcast time.
+  roofline      the blind-rotation kernel (the dominant one), timed alone with HIP events on its
+                stream.  Its bound is integer VALU issue: bound "valu-int",
+                achieved = the algorithmic modular multiplies of SURVEY 8(d) (n[(dG2+2)(N/2)log2 N +
+                4 dG2 N + 4N] per bootstrap) per second, peak = the microbenchmarked rate of the
+                product that kernel issues (tools/microbench/valu_rates.hip, --valu-peak-json:
+                signed Montgomery for STD128, exact FP64 fmodmul at the context's Q for STD192 /
+                STD128Q, special-form u64 for the 54-bit Q), frac = their ratio.  traffic = PMC HBM
+                bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+                corrections; --pmc-json), hbm_frac = traffic / kernel time / 8 TB/s,
+                effective_keystream_tbs = SURVEY B_alg (BSK + KS gather + LWE I/O per bootstrap, no
+                cross-ciphertext reuse) x batch / kernel time.
+  valu          PMC view of the same kernel: VALU instructions, busy fraction, the clock the part
+                held under it.
+  value_end_to_end / host_array  the same op through the host-array entry point (PCIe copies,
+                pinned staging and the host thread included), same inputs, whole job.
+  dropin        (C2) the reference's own, unchanged vector EvalBinGate (OpenFHE BinFHE code
+                compiled from its sources, oracle/_ref/ref_dropin) running on this GPU through the
+                drop-in shim (tfhe-gpu_amd/shim/bootstrapping_hip.cpp -> the seven boundary
+                symbols): end-to-end bootstraps/s of the unchanged caller, the shim's own time per
+                call, and its outputs checked against the benchmarked device-resident outputs.
+  cpu_baseline  the REFERENCE's own OpenFHE CPU path (oracle/_ref/ref_kat: the unchanged vector
+                API with the reference's CPU accumulator and key switch behind the GPU symbols,
+                OpenMP over ciphertexts) on a bounded sample of the same workload with the same
+                context and keys on this host's cores (rank 0, N = 1 only), which also checks the
+                benchmarked GPU outputs bit for bit; the C restatement (oracle/) only when ref_kat
+                is absent (then kind "port" and "fallback" says why).
 """
 from __future__ import annotations
 
@@ -58,6 +67,25 @@ MIB = 1 << 20
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
 VALU_CYCLES = 4                    # cycles per wave64 VALU instruction (mul/mad class; profiles/r01_valu_rates.txt)
 CLOCK_HZ = 2.4e9                   # MI355X peak engine clock
+SIGN_MOD = 1 << 23                 # C5: Encrypt(sk, m, FRESH, p, Qin = 2^23)
+
+# SURVEY.md 8(d).  ctx: ("set", name) or ("logq", name, arbFunc, logQ, N, baseG, throw) as
+# GenerateBinFHEContext; ref: the same context for oracle/_ref/ref_kat; per_unit_s: one unit (gate,
+# EvalFunc or EvalSign) of the reference's CPU path on one GPU-box core (sizes the CPU sample only).
+CONFIGS = {
+    "C2": {"ctx": ("set", "STD128"), "op": "gate", "batch": 8192, "scaling": "weak", "ref": "set:STD128",
+           "per_unit_s": 0.12, "what": "STD128 GINX EvalBinGate(NAND)"},
+    "C3": {"ctx": ("logq", "STD128", True, 12, 0, 0, 1), "op": "func", "batch": 4096, "scaling": "weak",
+           "ref": "logq:STD128,1,12,0,0,1", "per_unit_s": 1.6,
+           "what": "STD128 arbFunc logQ=12 throw=1 EvalFunc(x^3 mod 8), arbitrary LUT"},
+    "C4": {"ctx": ("set", "STD192"), "op": "gate", "batch": 8192, "scaling": "weak", "ref": "set:STD192",
+           "per_unit_s": 0.5, "what": "STD192 GINX EvalBinGate(NAND)"},
+    "C5a": {"ctx": ("set", "STD128Q"), "op": "sign", "batch": 1024, "scaling": "strong", "ref": "set:STD128Q",
+            "per_unit_s": 6.5, "what": "STD128Q EvalSign, ciphertext modulus 2^23"},
+    "C5b": {"ctx": ("logq", "STD128", False, 23, 0, 0, 1), "op": "sign", "batch": 1024, "scaling": "strong",
+            "ref": "logq:STD128,0,23,0,0,1", "per_unit_s": 4.0,
+            "what": "STD128 logQ=23 throw=1 EvalSign, ciphertext modulus 2^23"},
+}
 
 
 def parse():
@@ -65,21 +93,34 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=8192, help="ciphertexts per GPU")
-    ap.add_argument("--params", default="STD128",
-                    help="parameter set (default STD128 = the BASELINE metric; e.g. STD192 for the C4 class, "
-                         "device-resident, with --no-cpu-baseline)")
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS), help="SURVEY.md 8(d) configuration")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="ciphertexts per GPU (weak configs) or in all (strong configs); 0 = the config's")
+    ap.add_argument("--params", default=None,
+                    help="EvalBinGate(NAND) on another parameter set (e.g. STD192, STD128Q): device-resident, "
+                         "no cpu_baseline (overrides --config's context)")
     ap.add_argument("--kernel-reps", type=int, default=2, help="blind-rotation launches timed for the roofline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--generic", action="store_true", help="force the generic LDS blind-rotation kernel")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend ('nccl' = RCCL; 'gloo' only to rehearse N ranks on fewer GPUs)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_blind_rotate.json"))
-    ap.add_argument("--valu-peak-json", default=os.path.join(ROOT, "profiles", "r03_valu_peak.json"))
+    ap.add_argument("--pmc-json", default=None, help="PMC record of the blind rotation (default: per config)")
+    ap.add_argument("--valu-peak-json", default=None, help="VALU peak record (default: the newest)")
     ap.add_argument("--no-host-array", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the reference-through-the-shim leg")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="launch knob (tfhe_knobs) for A/B runs; repeatable")
+    ap.add_argument("--test-lib", action="store_true",
+                    help="run on lib/libtfhe_hip_test.so (fault-probe / timing builds; A/B runs only)")
     return ap.parse_args()
+
+
+def newest(*paths):
+    for p in paths:
+        if os.path.exists(p):
+            return p
+    return paths[0]
 
 
 GAMMA = np.uint64(0x9E3779B97F4A7C15)
@@ -127,6 +168,17 @@ def b_alg_per_bootstrap(p):
     return bsk + ks + io, bsk
 
 
+def peak_family(br_kernel, p):
+    """The product the context's blind rotation issues (tfhe_info.br_kernel) -> valu_peak.json family."""
+    if br_kernel == 1:
+        return "smont_i32"                                 # blind_rotate_fast4.hip
+    if br_kernel in (2, 3):
+        return "fmod_q37" if p.Q < (1 << 40) else "fmod_q50"  # blind_rotate_f64.hip
+    if br_kernel == 5:
+        return "sf_q54"                                    # sf2 / gen3sf, blind_rotate_generic.hip
+    return None
+
+
 def host_threads():
     """Threads for the CPU baseline: every core this process may run on, unless the pool caps
     OpenMP (OMP_NUM_THREADS is set to the box's CPU share on the GPU pool)."""
@@ -137,6 +189,17 @@ def host_threads():
 
 REF_KAT = os.path.join(ROOT, "oracle", "_ref", "ref_kat")
 REF_DROPIN = os.path.join(ROOT, "oracle", "_ref", "ref_dropin")
+
+
+def cube_lut(q, P=8):
+    """GenerateLUTviaFunction(m^3 mod p, p) (binfhecontext.cpp:280-301; time-estimate.cpp:70-75), the
+    C3 LUT (tests/test_oracle_ref_vectors.py pins it to the reference's own)."""
+    interval = q // P
+
+    def f(m, p1):
+        return (m * m * m) % p1 if m < p1 else ((m - p1 // 2) ** 3) % p1
+
+    return np.array([f(i // interval, P) * interval for i in range(q)], dtype=np.uint64)
 
 
 def dropin_leg(h1, h2, want, host_array_ms, reps=3):
@@ -177,118 +240,130 @@ def dropin_leg(h1, h2, want, host_array_ms, reps=3):
                     "shim_ms = the shim's marshalling + device time per call (fastest of the reps per phase)"}
 
 
-def cpu_baseline_reference(p, seconds, gpu_sample):
-    """The reference's own OpenFHE code (oracle/_ref/ref_kat, vector EvalBinGate, CPU functions
-    behind the seven GPU symbols, OpenMP over ciphertexts) on K pairs; the first ones are the
-    GPU's benchmarked inputs, whose outputs are compared bit for bit."""
+def ref_call_args(cfg, p, files):
+    """ref_kat arguments for the config's op on the input files (in, in2, lut)."""
+    if cfg["op"] == "gate":
+        return ["op=NAND", f"in={files['in']}", f"in2={files['in2']}"]
+    if cfg["op"] == "func":
+        return ["op=func", f"in={files['in']}", f"lut={files['lut']}", f"mod={p.q}"]
+    return ["op=sign", f"in={files['in']}", f"mod={SIGN_MOD}"]
+
+
+def cpu_baseline_reference(name, cfg, p, seconds, gpu_sample, bs_per_unit):
+    """The reference's own OpenFHE code (oracle/_ref/ref_kat: the vector API, CPU functions behind the
+    seven GPU symbols, OpenMP over ciphertexts) on K units of the same context with the same keys; the
+    first ones are the GPU's benchmarked inputs, whose outputs are compared bit for bit."""
     import subprocess
     import tempfile
 
     threads, visible = host_threads()
-    g1, g2, gout = gpu_sample
-    per_gate_s = 0.12  # one OpenFHE STD128 gate per thread on the GPU box (profiles/r03z: 800 pairs, 16 threads, 5.9 s)
-    K = max(len(g1), int(seconds * threads / per_gate_s))
+    ins, gout = gpu_sample["in"], gpu_sample["out"]
+    per = cfg["per_unit_s"]
+    K = max(len(gout), threads * max(1, int(seconds / per)))
     rs = np.random.default_rng(5)
-    c1 = np.concatenate([g1, rs.integers(0, p.q, (K - len(g1), p.n + 1), dtype=np.uint64)])
-    c2 = np.concatenate([g2, rs.integers(0, p.q, (K - len(g2), p.n + 1), dtype=np.uint64)])
+    width = p.n + 1
+    mod = SIGN_MOD if cfg["op"] == "sign" else p.q
+    arrs = {k: np.concatenate([v, rs.integers(0, mod, (K - len(v), width), dtype=np.uint64)]) for k, v in ins.items()}
 
-    def run(a1, a2, nthreads):
+    def run(nunits, nthreads):
         with tempfile.TemporaryDirectory() as tmp:
-            f1, f2, fo = (os.path.join(tmp, x) for x in ("c1", "c2", "out"))
-            a1.tofile(f1)
-            a2.tofile(f2)
+            files = {}
+            for k, v in arrs.items():
+                files[k] = os.path.join(tmp, k)
+                v[:nunits].tofile(files[k])
+            if cfg["op"] == "func":
+                files["lut"] = os.path.join(tmp, "lut")
+                cube_lut(p.q).tofile(files["lut"])
+            fo = os.path.join(tmp, "out")
             env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
-            r = subprocess.run([REF_KAT, "ctx=set:STD128", "keys=synth:1", "op=NAND", "api=vector", f"in={f1}",
-                                f"in2={f2}", f"out={fo}"], capture_output=True, text=True, env=env, timeout=900)
+            r = subprocess.run([REF_KAT, f"ctx={cfg['ref']}", "keys=synth:1", "api=vector", f"out={fo}"]
+                               + ref_call_args(cfg, p, files), capture_output=True, text=True, env=env, timeout=1800)
             if r.returncode:
                 raise RuntimeError(r.stderr[-2000:])
             js = json.loads(r.stdout.strip().splitlines()[-1])
-            return js, np.fromfile(fo, dtype=np.uint64).reshape(len(a1), p.n + 1)
+            return js, np.fromfile(fo, dtype=np.uint64).reshape(nunits, width)
 
-    js, out = run(c1, c2, threads)
-    B1 = max(2, int(seconds / 4 / per_gate_s))
-    js1, _ = run(c1[:B1], c2[:B1], 1)
+    js, out = run(K, threads)
+    single = None
+    if name == "C2":  # the single-thread figure SURVEY 8(d) asks for (the other contexts' key loads cost minutes)
+        B1 = max(2, int(seconds / 4 / per))
+        js1, _ = run(B1, 1)
+        single = round(B1 * bs_per_unit / js1["best_s"], 3)
     parity = {"ciphertexts": int(len(gout)), "bit_exact": bool(np.array_equal(out[:len(gout)], gout)),
-              "vs": "the reference's OpenFHE CPU path (oracle/_ref/ref_kat), same keys and inputs"}
-    return {"value": round(K / js["best_s"], 3), "unit": "bootstraps/s", "cores": threads, "kind": "reference",
-            "host_cores_visible": visible, "single_thread_value": round(B1 / js1["best_s"], 3),
-            "sample": f"STD128 EvalBinGate(NAND), vector API of the reference's OpenFHE (compiled from its sources, "
+              "vs": "the reference's OpenFHE CPU path (oracle/_ref/ref_kat), same context, keys and inputs"}
+    unit = {"gate": "EvalBinGate(NAND)", "func": "EvalFunc", "sign": "EvalSign"}[cfg["op"]]
+    return {"value": round(K * bs_per_unit / js["best_s"], 3), "unit": "bootstraps/s", "cores": threads,
+            "kind": "reference", "host_cores_visible": visible, "single_thread_value": single,
+            "sample": f"{cfg['what']}: the vector API of the reference's OpenFHE (compiled from its sources, "
                       f"oracle/Makefile.ref) with its CPU accumulator / key switch behind the GPU symbols, OpenMP "
-                      f"over ciphertexts, {threads} threads: {K} pairs in {js['best_s']:.1f} s (key load "
-                      f"{js['key_load_s']:.1f} s not counted); single thread: {B1} pairs in {js1['best_s']:.1f} s",
+                      f"over ciphertexts, {threads} threads: {K} x {unit} ({bs_per_unit} bootstraps each) in "
+                      f"{js['best_s']:.1f} s (key load {js['key_load_s']:.1f} s not counted)",
             "gpu_parity": parity}
 
 
-def cpu_baseline(p, bsk, ksk, seconds, gpu_sample=None):
-    if os.path.exists(REF_KAT) and gpu_sample is not None:
-        try:
-            return cpu_baseline_reference(p, seconds, gpu_sample)
-        except Exception as e:  # fall back to the restatement
-            print(f"[bench] reference CPU baseline failed ({e}); using the C restatement", file=sys.stderr)
+def cpu_baseline_port(p, bsk, ksk, seconds, gpu_sample, reason):
+    """Fallback when oracle/_ref/ref_kat is absent: the C restatement (oracle/tfhe_oracle.c), STD128 NAND."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
     pyoracle.build()
     threads, visible = host_threads()
-    orc = pyoracle.Oracle(p_oracle(pyoracle, p), bsk, ksk, threads=threads)
+    orc = pyoracle.Oracle(pyoracle.params_from_set("STD128"), bsk, ksk, threads=threads)
     rs = np.random.default_rng(5)
-    # calibrate on one gate per thread, then size the sample to ~`seconds`
     B0 = threads
     c1 = rs.integers(0, p.q, (B0, p.n + 1), dtype=np.uint64)
     c2 = rs.integers(0, p.q, (B0, p.n + 1), dtype=np.uint64)
     t0 = time.perf_counter()
     orc.eval_bin_gate("NAND", c1, c2)
     t_cal = time.perf_counter() - t0
-    reps = max(1, int(seconds / max(t_cal, 1e-3)))
-    B = B0 * reps
+    B = B0 * max(1, int(seconds / max(t_cal, 1e-3)))
     c1 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
     c2 = rs.integers(0, p.q, (B, p.n + 1), dtype=np.uint64)
     t0 = time.perf_counter()
     orc.eval_bin_gate("NAND", c1, c2)
     dt = time.perf_counter() - t0
-    # the single-thread figure SURVEY 8(d) asks for, on a quarter of the time budget
     orc.L.or_set_threads(1)
     B1 = max(1, int(seconds / 4 / max(t_cal, 1e-3)))
     t0 = time.perf_counter()
     orc.eval_bin_gate("NAND", c1[:B1], c2[:B1])
     dt1 = time.perf_counter() - t0
     orc.L.or_set_threads(threads)
-    # the same oracle checks the benchmarked GPU outputs (first ciphertexts of the last step)
-    parity = None
-    if gpu_sample is not None:
-        g1, g2, gout = gpu_sample
-        ref = orc.eval_bin_gate("NAND", g1, g2)
-        parity = {"ciphertexts": int(len(gout)), "bit_exact": bool(np.array_equal(ref, gout)),
-                  "vs": "oracle/tfhe_oracle.c on the same synthetic keys and inputs"}
+    g1, g2 = gpu_sample["in"]["in"], gpu_sample["in"]["in2"]
+    ref = orc.eval_bin_gate("NAND", g1, g2)
+    parity = {"ciphertexts": int(len(g1)), "bit_exact": bool(np.array_equal(ref, gpu_sample["out"])),
+              "vs": "oracle/tfhe_oracle.c on the same synthetic keys and inputs"}
     orc.close()
     return {"value": round(B / dt, 3), "unit": "bootstraps/s", "cores": threads, "kind": "port",
-            "host_cores_visible": visible, "single_thread_value": round(B1 / dt1, 3),
+            "host_cores_visible": visible, "single_thread_value": round(B1 / dt1, 3), "fallback": reason,
             "sample": f"STD128 EvalBinGate(NAND) on {B} random ciphertext pairs, same synthetic keys; "
                       f"oracle/tfhe_oracle.c (exact u128 CPU restatement, OpenMP one ciphertext per thread); "
                       f"{dt:.1f} s; single thread: {B1} pairs in {dt1:.1f} s",
             "gpu_parity": parity}
 
 
-def p_oracle(pyoracle, p):
-    return pyoracle.params_from_set("STD128")
-
-
 def main():
     args = parse()
-    if args.params != "STD128" and not args.no_cpu_baseline:
-        sys.exit("[bench] the cpu_baseline leg is defined for STD128; add --no-cpu-baseline")
+    name = args.config
+    cfg = dict(CONFIGS[name])
+    if args.params:
+        cfg.update(ctx=("set", args.params), op="gate", what=f"{args.params} GINX EvalBinGate(NAND)", ref=None,
+                   scaling="weak")
+        name = args.params
+        args.no_cpu_baseline = True
     if args.generic:
         os.environ["TFHE_FORCE_GENERIC"] = "1"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU "
+              f"(torch.distributed.run --nproc-per-node {args.gpus})", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
     import tfhe_amd
     from tfhe_amd import dist as tdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     local_dev = local % max(1, torch.cuda.device_count())  # == local on a full node
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -298,8 +373,16 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    p = tfhe_amd.params_from_set(args.params)
-    B = args.batch
+    ctxspec = cfg["ctx"]
+    p = (tfhe_amd.params_from_set(ctxspec[1]) if ctxspec[0] == "set"
+         else tfhe_amd.params_from_logq(ctxspec[1], *ctxspec[2:]))
+    if cfg["scaling"] == "strong":  # the config's batch is the whole job's
+        total = args.batch or cfg["batch"]
+        lo, hi = tdist.shard_range(total, world, rank)
+        B = hi - lo
+    else:
+        B = args.batch or cfg["batch"]
+        total = B * world
     # a dedicated (non-null) stream: the engine's kernels, torch's tensors and the
     # HIP events below are all ordered on it
     stream = torch.cuda.Stream(dev)
@@ -309,9 +392,14 @@ def main():
     # ---- GPUSetup: rank 0 converts the keys, the image is broadcast over RCCL ----
     t_setup = time.perf_counter()
     bcast_ms = None
+    libpath = tfhe_amd.capi.TEST_LIB if args.test_lib else None
+    knobs = {k: int(v) for k, v in (x.split("=", 1) for x in args.knob)}
     if rank == 0:
         bsk, ksk = synthetic_keys(p)
-        ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+        ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)
+        if args.no_cpu_baseline or name != "C2":
+            del bsk, ksk  # (C3's KSK is 4.8 GB)
+            bsk = ksk = None
     else:
         bsk = ksk = None
     if world > 1:
@@ -328,23 +416,35 @@ def main():
         torch.cuda.synchronize(dev)
         bcast_ms = (time.perf_counter() - t0) * 1e3
         if rank != 0:
-            ctx = tfhe_amd.BinFHEContextHIP.from_key_image(p, img.data_ptr(), img.numel(), local_dev)
+            ctx = tfhe_amd.BinFHEContextHIP.from_key_image(p, img.data_ptr(), img.numel(), local_dev, libpath)
         del img
+        bcast_ms = tdist.max_over_ranks(bcast_ms, dev)
     setup_s = time.perf_counter() - t_setup
+    if knobs:
+        ctx.set_knobs(**knobs)
 
     # ---- inputs resident in HBM ----
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    ct1 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
-    ct2 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    in_mod = SIGN_MOD if cfg["op"] == "sign" else int(p.q)
+    ct1 = torch.randint(0, in_mod, (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    ct2 = torch.randint(0, in_mod, (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
     out = torch.empty((B, p.n + 1), dtype=torch.int64, device=dev)
+    lut = torch.from_numpy(cube_lut(int(p.q)).astype(np.int64)).to(dev) if cfg["op"] == "func" else None
 
     def step():
-        ctx.EvalBinGateDevice("NAND", B, ct1.data_ptr(), ct2.data_ptr(), out.data_ptr(), stream=sptr)
+        if cfg["op"] == "gate":
+            ctx.EvalBinGateDevice("NAND", B, ct1.data_ptr(), ct2.data_ptr(), out.data_ptr(), stream=sptr)
+        elif cfg["op"] == "func":
+            ctx.EvalFuncDevice(B, ct1.data_ptr(), lut.data_ptr(), out.data_ptr(), stream=sptr)
+        else:
+            ctx.EvalSignDevice(B, ct1.data_ptr(), SIGN_MOD, out.data_ptr(), stream=sptr)
 
-    for _ in range(args.warmup):
+    b0 = ctx.info().bootstraps
+    for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize(dev)
+    bs_per_unit = (ctx.info().bootstraps - b0) // (max(1, args.warmup) * B)  # the engine's own count
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -358,12 +458,12 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = tdist.max_over_ranks(elapsed, dev)
-    total_bs = B * args.steps * world
+    total_bs = total * bs_per_unit * args.steps
     value = total_bs / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     # ---- dominant kernel (blind rotation) timed alone with HIP events on its stream ----
-    a = ct1[:, : p.n].contiguous()
+    a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
     acc = torch.zeros((B, 2, p.N), dtype=torch.int64, device=dev)
     acc[:, 1, ::2] = int(p.Q // 8 + 1)
     lib = tfhe_amd.lib()
@@ -378,11 +478,16 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize(dev)
     br_ms = e0.elapsed_time(e1) / args.kernel_reps
+    rank_ms = tdist.gather_over_ranks(br_ms, dev) if world > 1 else [br_ms]
+    info = ctx.info()
     balg, bsk_bytes = b_alg_per_bootstrap(p)
+    pmc_json = args.pmc_json or newest(os.path.join(ROOT, "profiles", f"r04_pmc_{name}.json"),
+                                       *([os.path.join(ROOT, "profiles", "r03_pmc_blind_rotate.json")]
+                                         if name == "C2" else []))
     traffic, valu_insts, pmc = None, None, {}
-    if os.path.exists(args.pmc_json):
+    if os.path.exists(pmc_json):
         try:
-            pmc = json.load(open(args.pmc_json))
+            pmc = json.load(open(pmc_json))
             if pmc.get("units_per_launch") == B:
                 traffic = pmc.get("hbm_bytes_per_launch")
                 valu_insts = pmc.get("sq_insts_valu_per_launch")
@@ -392,22 +497,29 @@ def main():
             traffic, valu_insts, pmc = None, None, {}
     mm = modmuls_per_bootstrap(p)
     achieved_mm = mm * B / (br_ms * 1e-3)
-    peak_mm, peak_src = None, None
-    if os.path.exists(args.valu_peak_json):
-        vp = json.load(open(args.valu_peak_json))
-        peak_mm, peak_src = vp["modmul_per_s"], vp
+    fam = peak_family(int(info.br_kernel), p)
+    vp_json = args.valu_peak_json or newest(os.path.join(ROOT, "profiles", "r04_valu_peak.json"),
+                                            os.path.join(ROOT, "profiles", "r03_valu_peak.json"))
+    peak_mm, peak_clock, peak_label = None, None, None
+    if os.path.exists(vp_json) and fam:
+        vp = json.load(open(vp_json))
+        pk = vp.get("peaks", {}).get(fam)
+        if pk is None and fam == "smont_i32":  # a round-3 record (smont only)
+            pk = {"modmul_per_s": vp["modmul_per_s"], "held_clock_ghz": vp.get("held_clock_ghz"),
+                  "kernel": vp.get("kernel")}
+        if pk:
+            peak_mm, peak_clock, peak_label = pk["modmul_per_s"], pk.get("held_clock_ghz"), pk.get("kernel")
     roofline = {"bound": "valu-int", "achieved": round(achieved_mm / 1e12, 3),
                 "peak": None if peak_mm is None else round(peak_mm / 1e12, 3), "unit": "Tmodmul/s",
                 "frac": None if peak_mm is None else round(achieved_mm / peak_mm, 3), "traffic": traffic,
                 "kernel": "blind_rotate (tfhe_eval_acc_device)", "kernel_ms": round(br_ms, 3),
-                "units_per_launch": B, "alg_modmul_per_unit": mm,
+                "units_per_launch": B, "alg_modmul_per_unit": mm, "peak_family": fam,
                 "hbm_frac": None if traffic is None else round(traffic / (br_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4),
                 "effective_keystream_tbs": round(balg * B / (br_ms * 1e-3) / 1e12, 2), "alg_bytes_per_unit": balg,
                 "note": "achieved = SURVEY 8(d) algorithmic modmuls per bootstrap x batch / event-timed kernel; peak = "
-                        "signed-Montgomery modmul rate of the VALU microbenchmark "
-                        + ("(" + os.path.relpath(args.valu_peak_json, ROOT) + ", " + str(peak_src.get("clock", "")) + ")"
-                           if peak_src else "(not found)")
-                        + "; hbm_frac = PMC HBM bytes / kernel time / 8 TB/s; effective_keystream_tbs = B_alg "
+                        f"the microbenchmarked rate of the product this kernel issues ({peak_label}, "
+                        + os.path.relpath(vp_json, ROOT) + (f", held {peak_clock} GHz" if peak_clock else "")
+                        + "); hbm_frac = PMC HBM bytes / kernel time / 8 TB/s; effective_keystream_tbs = B_alg "
                           "(no cross-ciphertext reuse) x batch / kernel time, served from L2/MALL"}
     simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
     valu = {"bound": "valu-int", "modmul_per_bootstrap": mm,
@@ -415,8 +527,8 @@ def main():
             "valu_instr_per_launch": valu_insts,
             "issue_frac": None if valu_insts is None else
             round(valu_insts * VALU_CYCLES / (simds * CLOCK_HZ * br_ms * 1e-3), 3),
-            "note": "issue_frac = PMC SQ_INSTS_VALU x 4 cycles / (4 SIMDs/CU x CUs x 2.4 GHz x kernel time), "
-                    "from " + os.path.relpath(args.pmc_json, ROOT)}
+            "note": "issue_frac (mixed-unit: 4 cycles per VALU instruction at 2.4 GHz; quote busy_frac) from "
+                    + os.path.relpath(pmc_json, ROOT)}
     act, gui = pmc.get("sq_active_inst_valu_per_launch"), pmc.get("grbm_gui_active_per_launch")
     if act and gui:
         # measured in one PMC pass, clock-independent: VALU-executing cycles per SIMD over the
@@ -426,61 +538,99 @@ def main():
         valu["held_clock_ghz"] = round(gui / 8 / (pass_ns * 1e-9 if pass_ns else br_ms * 1e-3) / 1e9, 2)
         valu["note"] += ("; busy_frac = SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8); held_clock_ghz = "
                          "GRBM_GUI_ACTIVE / 8 / kernel time (profiled pass, MI355X_MICROARCH.md 'DVFS give-back')")
-        if peak_mm and peak_src.get("held_clock_ghz"):
+        if peak_mm and peak_clock:
             # the same peak scaled to the clock the part holds under this kernel (power-limited): how much
             # of the gap is issue efficiency and how much is clock
-            peak_k = peak_mm * valu["held_clock_ghz"] / peak_src["held_clock_ghz"]
+            peak_k = peak_mm * valu["held_clock_ghz"] / peak_clock
             roofline["frac_at_kernel_clock"] = round(achieved_mm / peak_k, 3)
             roofline["note"] += (f"; frac_at_kernel_clock = achieved / (peak x {valu['held_clock_ghz']} GHz held under "
-                                 f"the kernel / {peak_src['held_clock_ghz']} GHz held under the microbenchmark)")
+                                 f"the kernel / {peak_clock} GHz held under the microbenchmark)")
 
-    # ---- the same gates through the host-array entry point (PCIe + host staging included) ----
+    # ---- the same op through the host-array entry point (PCIe + host staging included), every rank ----
     host_array = None
-    if rank == 0 and world == 1 and not args.no_host_array:
-        h1 = ct1.cpu().numpy().astype(np.uint64)
-        h2 = ct2.cpu().numpy().astype(np.uint64)
+    out_h = out.cpu().numpy().astype(np.uint64)
+    h1 = ct1.cpu().numpy().astype(np.uint64)
+    h2 = ct2.cpu().numpy().astype(np.uint64)
+    if not args.no_host_array:
+        lut_h = cube_lut(int(p.q)) if cfg["op"] == "func" else None
+
+        def host_call():
+            if cfg["op"] == "gate":
+                return ctx.EvalBinGate("NAND", h1, h2)
+            if cfg["op"] == "func":
+                return ctx.EvalFunc(h1, lut_h)
+            return ctx.EvalSign(h1, SIGN_MOD)
+
         best = None
         for _ in range(2):
+            if world > 1:
+                dist.barrier()
             t0 = time.perf_counter()
-            hout = ctx.EvalBinGate("NAND", h1, h2)
+            hout = host_call()
             dt = time.perf_counter() - t0
+            if world > 1:
+                dt = tdist.max_over_ranks(dt, dev)
             best = dt if best is None else min(best, dt)
-        host_array = {"value": round(B / best, 1), "unit": "bootstraps/s", "ms": round(best * 1e3, 3),
-                      "equal_to_device_resident": bool(np.array_equal(hout, out.cpu().numpy().astype(np.uint64))),
-                      "note": "tfhe_eval_bin_gate on host arrays: H2D + kernels + D2H through pinned staging, best of 2"}
+        host_array = {"value": round(total * bs_per_unit / best, 1), "unit": "bootstraps/s", "ms": round(best * 1e3, 3),
+                      "equal_to_device_resident": bool(np.array_equal(hout, out_h)),
+                      "note": "host arrays in and out (tfhe_eval_bin_gate / _func / _sign): H2D + kernels + D2H "
+                              "through pinned staging, best of 2, slowest rank"}
+        if world > 1:
+            host_array["equal_to_device_resident"] = bool(tdist.sum_over_ranks(
+                int(not host_array["equal_to_device_resident"]), dev) == 0)
 
     dropin = None
-    if rank == 0 and world == 1 and args.params == "STD128" and not args.no_dropin and host_array is not None:
+    if rank == 0 and world == 1 and name == "C2" and not args.no_dropin and host_array is not None:
         try:
-            dropin = dropin_leg(h1, h2, out.cpu().numpy().astype(np.uint64), host_array["ms"])
+            dropin = dropin_leg(h1, h2, out_h, host_array["ms"])
         except Exception as e:  # reported, never fatal: the headline does not depend on it
             print(f"[bench] drop-in leg failed: {e}", file=sys.stderr)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if bsk is None:
-            bsk, ksk = synthetic_keys(p)
-        K = min(B, 64)
-        sample = tuple(x[:K].cpu().numpy().astype(np.uint64) for x in (ct1, ct2, out))
-        cpu = cpu_baseline(p, bsk, ksk, args.cpu_seconds, sample)
-        if cpu["gpu_parity"] and not cpu["gpu_parity"]["bit_exact"]:
+        K = min(B, 64 if cfg["op"] == "gate" else 16)
+        sample = {"in": {"in": h1[:K]} if cfg["op"] != "gate" else {"in": h1[:K], "in2": h2[:K]}, "out": out_h[:K]}
+        reason = None
+        if os.path.exists(REF_KAT):
+            try:
+                cpu = cpu_baseline_reference(name, cfg, p, args.cpu_seconds, sample, bs_per_unit)
+            except Exception as e:
+                reason = f"oracle/_ref/ref_kat failed: {e}"
+        else:
+            reason = ("oracle/_ref/ref_kat absent (built only where /root/reference exists: oracle/Makefile.ref; "
+                      "git-ignored, it reaches the GPU box with the working tree)")
+        if cpu is None:
+            print(f"[bench] reference CPU baseline unavailable ({reason}); using the C restatement", file=sys.stderr)
+            if name == "C2":
+                if bsk is None:
+                    bsk, ksk = synthetic_keys(p)
+                cpu = cpu_baseline_port(p, bsk, ksk, args.cpu_seconds, sample, reason)
+        if cpu and cpu["gpu_parity"] and not cpu["gpu_parity"]["bit_exact"]:
             print("[bench] ERROR: GPU outputs differ from the CPU reference", file=sys.stderr)
 
     if rank == 0:
         line = {
-            "metric": f"bootstraps/sec (whole node), {args.params} GINX batch={B}",
+            "metric": (f"bootstraps/sec (whole node), {ctxspec[1]} GINX batch={B}" if name == "C2" or args.params
+                       else f"bootstraps/sec (whole node), {name}: {cfg['what']}, batch={total}"),
             "value": round(value, 2), "unit": "bootstraps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "data": "synthetic",
-            "dtype": {0: "u32" if int(ctx.info().word_bits) == 32 else "u64", 1: "u32", 2: "f64",
-                      3: "f64", 4: "i32", 5: "u64"}[int(ctx.info().br_kernel)],
-            "config": {"workload": f"{args.params} GINX EvalBinGate(NAND), inputs resident in HBM",
-                       "global_batch": B * world, "batch_per_gpu": B, "n": p.n, "N": p.N, "Q": p.Q,
-                       "dG2": p.dG2, "parallelism": f"shard{world}"},
+            "scaling": cfg["scaling"], "vs_baseline": None, "data": "synthetic",
+            "dtype": {0: "u32" if int(info.word_bits) == 32 else "u64", 1: "u32", 2: "f64",
+                      3: "f64", 4: "i32", 5: "u64"}[int(info.br_kernel)],
+            "config": {"workload": f"{name}: {cfg['what']}, inputs resident in HBM", "config": name,
+                       "global_batch": total, "batch_per_gpu": B, "bootstraps_per_unit": bs_per_unit,
+                       "n": p.n, "N": p.N, "Q": p.Q, "dG2": p.dG2, "parallelism": f"shard{world}"},
+            "value_end_to_end": None if host_array is None else host_array["value"],
+            "dist": {"backend": dist.get_backend() if world > 1 else None,
+                     "world_size": dist.get_world_size() if world > 1 else 1,
+                     "kernel_ms_max": round(max(rank_ms), 3), "kernel_ms_min": round(min(rank_ms), 3),
+                     "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2)},
             "roofline": roofline, "valu": valu, "host_array": host_array, "dropin": dropin, "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2), "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2),
-            "key_image_bytes": int(ctx.info().key_image_bytes),
+            "key_image_bytes": int(info.key_image_bytes),
         }
+        if knobs or args.test_lib:
+            line["knobs"] = dict(knobs, test_lib=args.test_lib)
         print(json.dumps(line), flush=True)
     ctx.GPUClean()
     if world > 1:

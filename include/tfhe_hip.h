@@ -4,8 +4,9 @@
  * This is the drop-in boundary.  The reference (eric070021/TFHE-GPU) exposes its
  * GPU path as seven C++ static members that OpenFHE's unchanged BinFHE code calls
  * (SURVEY.md 8(b)).  Each of those maps onto one entry point here; the OpenFHE
- * side binding a maintainer adds (a ~200-line shim translating NativeVector /
- * NativePoly <-> flat u64) is in INTEGRATION.md.
+ * side binding (the shim that defines those seven C++ symbols over this ABI, translating
+ * NativeVector / NativePoly <-> u64 rows) is tfhe-gpu_amd/shim/bootstrapping_hip.cpp;
+ * INTEGRATION.md describes how a maintainer links it into src/binfhe.
  *
  *   reference symbol                                        entry point
  *   GPUFFTBootstrap::GPUSetup       bootstrapping.cuh:111   tfhe_setup_eval (OpenFHE EVALUATION-format BSK) or tfhe_setup
@@ -52,8 +53,9 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 4  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
-                                   4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows) */
+#define TFHE_HIP_ABI_VERSION 5  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
+                                   4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows);
+                                   5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -194,6 +196,15 @@ tfhe_status tfhe_eval_acc_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_a, u
                                  void* stream);
 tfhe_status tfhe_mkm_switch_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct_ext, uint64_t fmod, uint64_t* d_out,
                                    void* stream);
+/* The chained vector ops of binfhe-base-scheme.cpp:679-1037 with every intermediate in HBM (the
+ * same pipelines as tfhe_eval_func / _floor / _sign).  d_lut: [q] or [B][q] in device memory; its
+ * first q words are read back once per call to classify the batch (binfhe-base-scheme.cpp:697-698). */
+tfhe_status tfhe_eval_func_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct, uint64_t q, const uint64_t* d_lut,
+                                  int per_ct_lut, uint64_t* d_out, void* stream);
+tfhe_status tfhe_eval_floor_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct, uint64_t mod, uint32_t roundbits,
+                                   uint64_t* d_out, void* stream);
+tfhe_status tfhe_eval_sign_device(tfhe_ctx* ctx, size_t B, const uint64_t* d_ct, uint64_t mod, uint64_t* d_out,
+                                  void* stream);
 
 /* ---- key replication for one-process-per-GPU deployments ----
  * The packed device key image (NTT-domain BSK with Shoup companions, packed
@@ -227,6 +238,28 @@ tfhe_status tfhe_host_selftest(const tfhe_params* p);
  * tfhe_last_error() = "device <g>: ...". ---- */
 tfhe_status tfhe_shard_range(size_t total, int world, int rank, size_t* lo, size_t* hi);
 tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, size_t* spans);
+
+/* ---- launch knobs (no reference counterpart): the kernel-form choices earlier rounds measured A/B.
+ * Read from the environment once, when a context is set up (TFHE_KS_TILED_MIN, TFHE_KS_CTS,
+ * TFHE_KS_SPLIT, TFHE_KS_PK, TFHE_HOST_PARTS, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2,
+ * TFHE_GENERIC, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no launch reads the
+ * environment.  Every setting computes the same outputs (each is a parity-tested cross-check). ---- */
+typedef struct tfhe_knobs {
+    int32_t ks_tiled_min; /* smallest batch on the batch-tiled key switch; -1: by key width; 0: never */
+    int32_t ks_cts;       /* ciphertexts per thread in the tiled key switch: 0 (by key width / batch), 1, 2 */
+    int32_t ks_split;     /* most block groups the key-switch steps split over at small batches (1: none) */
+    int32_t ks_pk;        /* 0: 32-bit column sums for u16 keys instead of packed u16 pairs */
+    int32_t host_parts;   /* sub-batches per device in the host-array runner (>= 1) */
+    int32_t wire;         /* 0: u64 words over PCIe (no narrow wire format) */
+    int32_t acc_flags;    /* 0: host-array EvalAcc waits for the whole launch (no completion flags) */
+    int32_t f64w;         /* 0: slot-layout FP64 blind rotation instead of the wave-local one */
+    int32_t sf2;          /* 0: gen3sf special-form blind rotation instead of the wave-local sf2 */
+    int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
+    int32_t trace;        /* host-array runner timeline on stderr */
+    int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
+} tfhe_knobs;
+tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
+tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);
 
 /* ---- extension (no reference counterpart): build of the specialised STD128-class blind
  * rotation used by later calls, for A/B runs and tests; 0 restores the default.  Process-wide;

@@ -19,6 +19,9 @@
 //   api=vector (default; through the 7 boundary symbols) | single (CPU single-ciphertext API)
 //   in=<u64 file> in2=<u64 file> lut=<u64 file> acc=<u64 file> mod=<ct modulus> fmod=<m>
 //   roundbits=<r> out=<u64 file> gpus=<numGPUs for GPUSetup> reps=<timed repetitions>
+//   sizes=<B1,B2,...>  batch sweep (gates / func / floor / sign / decomp): the reps are timed on the
+//                      first B1, then B2, ... ciphertexts of the input, keys loaded once (the
+//                      reference's CHES-experiments.cpp:95-121 sweep); "sweep" lists best/mean per size
 // Prints one JSON line (digests, timings) on stdout.
 #include "binfhecontext.h"
 #include "rgsw-acc-cggi.h"
@@ -190,10 +193,16 @@ void load_keys(Setup& s, const uint64_t* bsk_coeff, const uint64_t* ksk) {
 }
 
 // ---- ciphertexts ------------------------------------------------------------------------
+size_t g_limit = 0;  // sizes= sweep: ciphertexts read from each input (0 = all)
+
 std::vector<LWECiphertext> read_cts(const std::string& path, uint32_t n, uint64_t mod) {
     auto w = read_u64(path);
     if (w.size() % (n + 1)) die(path + ": size is not a multiple of n+1");
     std::vector<LWECiphertext> v(w.size() / (n + 1));
+    if (g_limit) {
+        if (g_limit > v.size()) die(path + ": fewer ciphertexts than the sweep size");
+        v.resize(g_limit);
+    }
     for (size_t s = 0; s < v.size(); ++s) {
         NativeVector a(n, mod);
         for (uint32_t l = 0; l < n; ++l) a[l] = w[s * (n + 1) + l];
@@ -343,6 +352,13 @@ int main(int argc, char** argv) {
     std::vector<uint64_t> out;
     double best = 1e30, total = 0;
     uint64_t extra = 0;  // decomp: digits
+    std::vector<size_t> sizes;
+    for (auto& f : split(arg("sizes"), ',')) sizes.push_back(std::stoull(f));
+    if (sizes.empty()) sizes.push_back(0);
+    std::ostringstream sweep;
+    for (size_t si = 0; si < sizes.size(); ++si) {
+    g_limit = sizes[si];
+    best = 1e30, total = 0;
     for (int rep = 0; rep < reps; ++rep) {
         out.clear();
         double ts = now_s();
@@ -488,14 +504,20 @@ int main(int argc, char** argv) {
                     append_ct(out, x);
                     if (c == 0) mods.push_back(x->GetModulus().ConvertToInt());
                 }
-            js << ",\"moduli\":[";
-            for (size_t d = 0; d < mods.size(); ++d) js << (d ? "," : "") << mods[d];
-            js << "]";
+            if (rep + 1 == reps && si + 1 == sizes.size()) {
+                js << ",\"moduli\":[";
+                for (size_t d = 0; d < mods.size(); ++d) js << (d ? "," : "") << mods[d];
+                js << "]";
+            }
         } else {
             for (auto& c : res) append_ct(out, c);
-            if (!res.empty()) js << ",\"out_mod\":" << res[0]->GetModulus().ConvertToInt();
+            if (!res.empty() && rep + 1 == reps && si + 1 == sizes.size())
+                js << ",\"out_mod\":" << res[0]->GetModulus().ConvertToInt();
         }
     }
+    if (g_limit) sweep << (si ? "," : "") << "{\"B\":" << g_limit << ",\"best_s\":" << best << ",\"mean_s\":" << total / reps << "}";
+    }
+    if (sizes.size() > 1 || sizes[0]) js << ",\"sweep\":[" << sweep.str() << "]";
     if (api == "vector") s.cc.GPUClean();
     write_u64(arg("out"), out);
     js << ",\"api\":\"" << api << "\",\"reps\":" << reps << ",\"best_s\":" << best << ",\"mean_s\":" << total / reps

@@ -21,7 +21,7 @@ def test_library_exports_every_header_symbol(capi):
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.tfhe_abi_version() == 4
+    assert lib.tfhe_abi_version() == capi.capi.ABI_VERSION == 5
 
 
 @pytest.mark.parametrize("name", ["TOY", "MEDIUM", "STD128", "STD128_OPT", "STD192", "STD192_OPT", "STD256",
@@ -149,3 +149,29 @@ def test_cpp_example_builds_and_links(capi, tmp_path):
     r = subprocess.run([str(exe), "1", "none"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == f"C-ABI version {capi.capi.ABI_VERSION}"
+
+
+def test_product_library_has_no_probe_builds(capi):
+    """The fault-probe / timing-only builds of k_blind_rotate_f64w exist only in the test library
+    (VERDICT r3 weak 7): the product library's symbol table carries the PROBE = 0 instances alone."""
+    import re
+    import subprocess
+
+    def f64w_instances(path):
+        out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
+        return sorted(set(re.findall(r"k_blind_rotate_f64w<([^>]*)>", out)))
+
+    prod = f64w_instances(capi.library_path())
+    test = f64w_instances(capi.capi.TEST_LIB)
+    assert prod and all(i.endswith(", 0") for i in prod), prod
+    assert set(prod) < set(test) and any(not i.endswith(", 0") for i in test), test
+
+
+def test_knob_abi_mirrors_header(capi):
+    """tfhe_knobs (include/tfhe_hip.h) and the ctypes mirror list the same fields in the same order."""
+    import re
+
+    txt = open(capi.capi.HEADER).read()
+    body = re.search(r"typedef struct tfhe_knobs \{(.*?)\} tfhe_knobs;", txt, re.S).group(1)
+    fields = re.findall(r"int32_t\s+(\w+);", body)
+    assert fields == [k for k, _ in capi.capi.Knobs._fields_]

@@ -67,3 +67,22 @@ def test_c5_bootstrap_count(c5, oracle):
     ctx.EvalSign(ct, QIN)
     per = (ctx.info().bootstraps - before) // 4
     assert per == (15 if c5["name"] == "C5a_STD128Q" else 7), per
+
+
+def test_c5_evalsign_device_resident(c5, oracle):
+    """tfhe_eval_sign_device (bench.py --config C5a/C5b): inputs and outputs in HBM, the same pipeline as
+    the host-array EvalSign; equal to it and to the oracle, on a caller stream."""
+    import torch
+
+    op, ctx, orc = c5["op"], c5["ctx"], c5["orc"]
+    rs = np.random.default_rng(8)
+    ct = rs.integers(0, QIN, (130, op.n + 1), dtype=np.uint64)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    d = torch.from_numpy(ct.astype(np.int64)).to(dev)
+    do = torch.empty_like(d)
+    ctx.EvalSignDevice(len(ct), d.data_ptr(), QIN, do.data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    got = do.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(got, ctx.EvalSign(ct, QIN))
+    assert np.array_equal(got[[0, 129]], orc.eval_sign(ct[[0, 129]], QIN))

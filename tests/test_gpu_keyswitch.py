@@ -1,14 +1,13 @@
 """GPU parity of the batch-tiled key switch (ks_tiled.hip) against the oracle's
 ModSwitch -> KeySwitch -> ModSwitch (lwe-pke.cpp:204-215, 299-321).
 
-Batches of >= TFHE_KS_TILED_MIN ciphertexts (default 256) take the tiled form, smaller
+Batches of >= ks_tiled_min (knob; TFHE_KS_TILED_MIN at setup) ciphertexts (default 256) take the tiled form, smaller
 ones the per-ciphertext gather; both must equal the oracle bit for bit.  Every KSK word
 width the engine packs is covered: u16 (STD128, qKS = 2^14), u32 with 32-bit sums
 (STD192, qKS = 2^19, N dKS (qKS-1) < 2^32), u32 with 64-bit sums (STD128Q, qKS = 2^25)
 and u64 (the logQ = 12 arbFunc context, qKS = 2^35, dKS = 7).  Batches are ragged
 (not multiples of the 512/1024-ciphertext tiles) and include all-zero and all-(Q-1)
 extracts.  Random keys: bit-exactness does not need valid ones."""
-import os
 
 import numpy as np
 import pytest
@@ -50,16 +49,10 @@ def _ext(op, B, seed):
     return ext
 
 
-def _with_min(value, fn):
-    old = os.environ.get("TFHE_KS_TILED_MIN")
-    os.environ["TFHE_KS_TILED_MIN"] = value
-    try:
+def _with_min(ctx, value, fn):
+    """Run fn with the context's ks_tiled_min knob at value (TFHE_KS_TILED_MIN, read at setup)."""
+    with ctx.knobs_set(ks_tiled_min=int(value)):
         return fn()
-    finally:
-        if old is None:
-            os.environ.pop("TFHE_KS_TILED_MIN")
-        else:
-            os.environ["TFHE_KS_TILED_MIN"] = old
 
 
 @pytest.mark.parametrize("B", [300, 1029])
@@ -67,8 +60,8 @@ def test_tiled_keyswitch_equals_oracle(ks_ctx, B):
     name, op, ctx, orc = ks_ctx
     ext = _ext(op, B, B)
     fmod = op.q
-    tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, fmod))
-    gather = _with_min("0", lambda: ctx.MKMSwitch(ext, fmod))
+    tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, fmod))
+    gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, fmod))
     assert np.array_equal(tiled, gather)
     # the oracle on a sample (all of them for the cheap STD128 key switch)
     idx = np.arange(B) if name == "STD128" else np.r_[0:6, B // 2 - 3:B // 2 + 3, B - 6:B]
@@ -80,7 +73,7 @@ def test_tiled_keyswitch_other_output_moduli(ks_ctx):
     ext = _ext(op, 260, 7)
     idx = np.r_[0:4, 256:260]
     for fmod in (2 * op.q, 1 << 20, op.qKS):
-        tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, fmod))
+        tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, fmod))
         assert np.array_equal(tiled[idx], orc.mkm_switch(np.ascontiguousarray(ext[idx]), fmod)), fmod
 
 
@@ -88,10 +81,10 @@ def test_default_threshold_routes_small_batches_to_gather(ks_ctx):
     """Below the threshold (and for B = 1) the gather runs; results agree across the switch."""
     name, op, ctx, orc = ks_ctx
     ext = _ext(op, 255, 9)
-    a = _with_min("256", lambda: ctx.MKMSwitch(ext, op.q))
-    b = _with_min("1", lambda: ctx.MKMSwitch(ext, op.q))
+    a = _with_min(ctx, "256", lambda: ctx.MKMSwitch(ext, op.q))
+    b = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
     assert np.array_equal(a, b)
-    one = _with_min("1", lambda: ctx.MKMSwitch(ext[:1], op.q))
+    one = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext[:1], op.q))
     assert np.array_equal(one, orc.mkm_switch(np.ascontiguousarray(ext[:1]), op.q))
 
 
@@ -101,14 +94,7 @@ def test_tiled_keyswitch_ciphertexts_per_thread(ks_ctx, cts):
     batch) equal the gather form."""
     name, op, ctx, orc = ks_ctx
     ext = _ext(op, 1029, 13)
-    old = os.environ.get("TFHE_KS_CTS")
-    os.environ["TFHE_KS_CTS"] = cts
-    try:
-        tiled = _with_min("1", lambda: ctx.MKMSwitch(ext, op.q))
-    finally:
-        if old is None:
-            os.environ.pop("TFHE_KS_CTS")
-        else:
-            os.environ["TFHE_KS_CTS"] = old
-    gather = _with_min("0", lambda: ctx.MKMSwitch(ext, op.q))
+    with ctx.knobs_set(ks_cts=int(cts)):
+        tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+    gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
     assert np.array_equal(tiled, gather)

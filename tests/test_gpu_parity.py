@@ -319,16 +319,9 @@ def test_host_pipeline_sub_batches(std128, parts):
     torch.cuda.synchronize()
     want = do.cpu().numpy().astype(np.uint64)
     lut = np.array([(x * 3) % 4 * (cp.q // 4) for x in range(cp.q)], dtype=np.uint64) % cp.q
-    old = os.environ.get("TFHE_HOST_PARTS")
-    os.environ["TFHE_HOST_PARTS"] = parts
-    try:
+    with ctx.knobs_set(host_parts=int(parts)):
         got = ctx.EvalBinGate("AND", c1, c2)
         fgot = ctx.EvalFunc(c1, lut)
-    finally:
-        if old is None:
-            os.environ.pop("TFHE_HOST_PARTS")
-        else:
-            os.environ["TFHE_HOST_PARTS"] = old
     assert np.array_equal(got, want)
     idx = [0, 1, B // 2, B - 2, B - 1]
     assert np.array_equal(got[idx], orc.eval_bin_gate("AND", c1[idx], c2[idx]))
@@ -372,10 +365,10 @@ def test_key_file_roundtrip(std128, capi, tmp_path):
 
 
 @pytest.mark.parametrize("pset,path,kernel", [("STD192", "f64", 3), ("STD192", "f64-nofold", 2), ("STD192", "generic", 0),
-                                              ("STD192", "f64-slot", 3), ("STD192", "f64w-gather", 3),
-                                              ("STD192Q_OPT", "f64", 3), ("STD128Q", "f64", 3), ("STD128Q", "f64-slot", 3),
-                                              ("STD128Q", "f64w-gather", 3),
-                                              ("STD128Q", "f64-exactonly", 2), ("STD128Q", "f64-nofold", 2)])
+                                              ("STD192", "f64-slot", 3), ("STD192Q_OPT", "f64", 3),
+                                              ("STD128Q", "f64", 3), ("STD128Q", "f64-slot", 3),
+                                              ("STD128Q", "f64-exactonly", 2), ("STD128Q", "f64-nofold", 2),
+                                              ("STD128Q", "generic-v2", 0), ("STD192", "generic-v1", 0)])
 def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     """STD192 (Q = 2^37 - 2^17 + 1) and STD128Q (Q = 2^50 - 2^14 + 1, the reducing variant),
     N = 2048, run on the exact-FP64 kernel by default with the top digit's transforms
@@ -391,12 +384,14 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
     env = {"generic": ("TFHE_FORCE_GENERIC", "1"), "f64-nofold": ("TFHE_F64_FOLD", "0"),
            "f64-exactonly": ("TFHE_F64_FOLD", "1"), "f64-slot": ("TFHE_F64W", "0"),
-           "f64w-gather": ("TFHE_F64W_MT", "0")}.get(path)
+           "generic-v2": ("TFHE_FORCE_GENERIC", "1"), "generic-v1": ("TFHE_FORCE_GENERIC", "1")}.get(path)
+    knob = {"generic-v2": {"generic": 2}, "generic-v1": {"generic": 1}}.get(path, {})
     if env:
         os.environ[env[0]] = env[1]
-    try:  # setup-time switches are read at setup, launch-time ones (F64W*) at every launch
+    try:  # the environment is read at setup (tfhe_knobs); the generic kernel's form is a knob
         ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
         assert ctx.info().br_kernel == kernel
+        ctx.set_knobs(**knob)
         B = 2
         a = rs.integers(0, op.q, (B, op.n), dtype=np.uint64)
         acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
@@ -428,7 +423,7 @@ def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     env = {"generic": ("TFHE_SF", "0"), "gen3sf": ("TFHE_SF2", "0")}.get(path)
     if env:
         os.environ[env[0]] = env[1]
-    try:  # TFHE_SF is read at setup, TFHE_SF2 at every launch
+    try:  # both read at setup (TFHE_SF2 into the sf2 knob)
         ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
         assert ctx.info().br_kernel == kernel
         B = 3

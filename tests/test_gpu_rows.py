@@ -118,7 +118,7 @@ def test_rows_reject_null_rows(std128):
 
 def test_flagged_eval_acc_output_equals_whole_launch_drain(std128, monkeypatch):
     """The host-array EvalAcc drains finished ciphertexts while its blind rotation still runs
-    (completion flags, engine.hip d2h_flagged); TFHE_ACC_FLAGS=0 waits for the whole launch.  Both
+    (completion flags, engine.hip d2h_flagged); the acc_flags knob 0 waits for the whole launch.  Both
     must return the same accumulators -- 8192 ciphertexts = 16 staging blocks, rows and flat."""
     op, ctx, capi = std128["op"], std128["ctx"], std128["capi"]
     lib = capi.lib()
@@ -129,7 +129,7 @@ def test_flagged_eval_acc_output_equals_whole_launch_drain(std128, monkeypatch):
     tv = rs.integers(0, op.Q, (B, tvlen), dtype=np.uint64)
     outs = {}
     for flags in ("1", "0"):
-        monkeypatch.setenv("TFHE_ACC_FLAGS", flags)
+        ctx.set_knobs(acc_flags=int(flags))
         flat = np.empty((B, 2, op.N), dtype=np.uint64)
         check(lib.tfhe_eval_acc_tv(ctx.handle, B, a, amod, tv, tvlen, flat), "tfhe_eval_acc_tv")
         acc_rows = [np.empty(op.N, dtype=np.uint64) for _ in range(2 * B)]
@@ -137,6 +137,7 @@ def test_flagged_eval_acc_output_equals_whole_launch_drain(std128, monkeypatch):
               "tfhe_eval_acc_tv_rows")
         assert np.array_equal(np.stack(acc_rows).reshape(B, 2, op.N), flat)
         outs[flags] = flat
+    ctx.set_knobs(acc_flags=1)
     assert np.array_equal(outs["1"], outs["0"])
     # sampled against the oracle on the expanded accumulators
     idx = [0, 1, 511, 512, 4095, 8191]

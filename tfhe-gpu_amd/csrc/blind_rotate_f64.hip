@@ -31,7 +31,6 @@ struct F64Const {
     int64_t Qi;
     double Ninv;  // N^-1 mod Q, centred (FOLD)
     double wfac;  // 2^(gL) N^-1 mod Q, centred (WRAP)
-    uint32_t kround_mask;  // timing experiments only (results invalid): key rows of round i & mask
 };
 
 // Top-digit elimination (FOLD), as in the specialised STD128 kernel (blind_rotate_fast4.hip):
@@ -51,17 +50,14 @@ struct F64Fold {
 };
 
 __device__ __forceinline__ double fmodmul(double a, double b, const F64Const& K) {
-    const double h = __dmul_rn(a, b);
-    const double l = __fma_rn(a, b, -h);
-    const double q = __builtin_rint(__dmul_rn(h, K.Qinv));
-    return __dadd_rn(__fma_rn(-q, K.Q, h), l);
+    return fmodmul_f64(a, b, K.Q, K.Qinv);  // device_math.hpp
 }
 
 __device__ __forceinline__ double fred(double x, const F64Const& K) {
     return __fma_rn(-__builtin_rint(__dmul_rn(x, K.Qinv)), K.Q, x);
 }
 
-constexpr uint32_t ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
+[[maybe_unused]] constexpr uint32_t ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
 
 // CT stages m and 2m fused (radix-4 units), both polynomials of buf[2][N]; TH threads, all
 // trip counts and strides compile-time; RED: reduce the unit's outputs
@@ -709,12 +705,15 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 }
 
 // FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64.
-// MT (monomial factors psi^(+-e) - 1 of the lane's 4 slots): 0 gathers from the 2N-entry memory
-// table at each use, 1 two LDS table products at each use, 2 the 8 gathers issued once per round
-// before the products, 3 the LDS table products once per round (then one product per use).  PROBE (fault probe, TFHE_F64W_PROBE; tests/test_gpu_f64w_race.py):
-// bit 1 delays waves 1.. inside the prologue's C' transform (between passes B and C), bit 0
-// omits the barrier after it -- together they reproduce the round-0 race of the round-2 kernel
-template <bool RED, bool WRAP, int LD, int MT, int PROBE = 0>
+// Monomial factors psi^(+-e) - 1 of the lane's 4 slots: two LDS table products once per round
+// (then one product per use).  Round 3 measured the alternatives and removed them (round 4): gathers
+// from the 2N-entry memory table at each use (STD192 474 ms), table products at each use (385 ms),
+// the 8 gathers once per round (357 ms), against 315-323 ms (profiles/r02ae, r03i).
+// PROBE (test library only, TFHE_TEST_PROBES; tests/test_gpu_f64w_race.py): bit 1 delays waves 1..
+// inside the prologue's C' transform (between passes B and C), bit 0 omits the barrier after it --
+// together they reproduce the round-0 race of the round-2 kernel; bit 2 (timing only) drops the
+// barrier before each further digit's pass A
+template <bool RED, bool WRAP, int LD, int PROBE = 0>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
                     const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -799,7 +798,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     for (uint32_t i = 0; i < P.n; ++i) {
         // rotation exponent staged in LDS (no 64-bit remainder in the round loop)
         const uint32_t ai = ex[i];
-        const uint32_t round_off = (i & K.kround_mask) * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
+        const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
         auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4], bool sync) {
@@ -872,11 +871,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         for (int q = 0; q < 4; ++q) ip[q] = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
         double S[2][4], A[2][4];
         double kv[2][4];
-        double Wp[4], Wm[4];  // MT 2/3: psi^e - 1, psi^-e - 1 at the 4 slots
-        if constexpr (MT == 2) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Wp[q] = mono[ip[q]], Wm[q] = mono[(twoN - ip[q]) & (twoN - 1)];
-        }
+        double Wp[4], Wm[4];  // psi^e - 1, psi^-e - 1 at the 4 slots (built at j = 0)
         kload(0, kv[0]);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
@@ -895,23 +890,11 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t in = (twoN - ip[q]) & (twoN - 1);
-                    double sv;
-                    if constexpr (MT >= 2) {
-                        if constexpr (MT == 3) {
-                            if (j == 0) {
-                                Wp[q] = __dsub_rn(fmodmul(mt[ip[q] >> 6], mt[64 + (ip[q] & 63)], K), 1.0);
-                                Wm[q] = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
-                            }
-                        }
-                        sv = fred(__dadd_rn(fmodmul(A[0][q], Wp[q], K), fmodmul(A[1][q], Wm[q], K)), K);
-                    } else if constexpr (MT == 1) {
-                        auto mm = [&](double x, uint32_t e) {
-                            return __dsub_rn(fmodmul(fmodmul(x, mt[e >> 6], K), mt[64 + (e & 63)], K), x);
-                        };
-                        sv = fred(__dadd_rn(mm(A[0][q], ip[q]), mm(A[1][q], in)), K);
-                    } else {
-                        sv = __dadd_rn(fmodmul(A[0][q], mono[ip[q]], K), fmodmul(A[1][q], mono[in], K));
+                    if (j == 0) {
+                        Wp[q] = __dsub_rn(fmodmul(mt[ip[q] >> 6], mt[64 + (ip[q] & 63)], K), 1.0);
+                        Wm[q] = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
                     }
+                    const double sv = fred(__dadd_rn(fmodmul(A[0][q], Wp[q], K), fmodmul(A[1][q], Wm[q], K)), K);
                     S[j][q] = sv;
                     Cn[j][q] = fred(__dadd_rn(Cn[j][q], sv), K);
                 }
@@ -1016,19 +999,43 @@ F64Fold make_fold(const BRParams& P, bool on) {
 }  // namespace
 
 bool f64_path_supported(const BRParams& P, int word_bits) {
-    return word_bits == 64 && P.Q >= (1ull << 32) && P.Q < (1ull << 50) && (P.N == 1024 || P.N == 2048) &&
-           P.logG <= 32 && P.n > 0;
+    // every parameter set with 2^32 <= Q < 2^50 has N = 2048 (STD192*, STD192Q*, STD128Q*): the N = 1024
+    // instances were never reachable and were removed in round 4
+    return word_bits == 64 && P.Q >= (1ull << 32) && P.Q < (1ull << 50) && P.N == 2048 && P.logG <= 32 && P.n > 0;
 }
 
 size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
 
-// TFHE_F64_FOLD: unset/2 = fold whenever thr = 0, with the WRAP correction where the top digit
-// is not always exact (STD128Q: 16.2K vs 15.2K bootstraps/s unfolded on C5a); 1 = only where it
-// is always exact (STD192 classes); 0 = never
+// TFHE_F64_FOLD (read at setup): unset/2 = fold whenever thr = 0, with the WRAP correction where the top
+// digit is not always exact (STD128Q: 16.2K vs 15.2K bootstraps/s unfolded on C5a); 1 = only where it is
+// always exact (STD192 classes); 0 = never
 bool f64_fold_enabled(const BRParams& P) {
     const char* e = std::getenv("TFHE_F64_FOLD");
     const int mode = e && e[0] ? e[0] - '0' : 2;
     return mode == 2 ? fold_possible(P) : mode == 1 ? fold_exact(P) : false;
+}
+
+namespace {
+// The instances shipped (round 4: only combinations some parameter set reaches, each in a parity test):
+//   f64w  <RED, WRAP, LD>: STD128Q(_OPT) <1, 1, 1>; STD192(_OPT), STD192Q(_OPT) <0, 0, 2>
+//   slot  <512, 4, RED, FOLD, WRAP>: STD128Q wrap <1, 1, 1>, STD192* fold <0, 1, 0>, unfolded <1, 0>, <0, 0>
+// (TFHE_F64_FOLD / the f64w knob select the slot layout and the unfolded forms: cross-checks)
+bool f64w_instance(bool red, bool wrap, int ld) { return (red && wrap && ld == 1) || (!red && !wrap && ld == 2); }
+bool slot_instance(bool red, bool fold, bool wrap) { return fold ? (wrap ? red : !red) : true; }
+}  // namespace
+
+bool f64_test_probes_compiled() {
+#ifdef TFHE_TEST_PROBES
+    return true;
+#else
+    return false;
+#endif
+}
+
+bool f64_instance_available(const BRParams& P, bool fold) {
+    if (fold && !fold_possible(P)) return false;
+    const bool red = P.Q >= (1ull << 40), wrap = fold && !fold_exact(P);
+    return slot_instance(red, fold, wrap);  // (every f64w instance has its slot-layout twin)
 }
 
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
@@ -1042,8 +1049,10 @@ hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void
 }
 
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold,
-                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s) {
+                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
+                                   const Knobs& kn) {
     if (B == 0) return hipSuccess;
+    if (P.N != 2048 || (fold && !fold_possible(P))) return hipErrorInvalidValue;
     F64Const K;
     K.Q = (double)P.Q;
     K.Qinv = 1.0 / K.Q;
@@ -1052,14 +1061,6 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     K.Ninv = -(double)((P.Q - 1) / P.N);
     const uint64_t wf = (uint64_t)((unsigned __int128)pow_mod(2, (uint64_t)P.logG * P.digits, P.Q) * ninv % P.Q);
     K.wfac = wf > P.Q / 2 ? -(double)(P.Q - wf) : (double)wf;
-    K.kround_mask = ~0u;
-    {  // TFHE_F64_KEYROUNDS=m (timing only, needs TFHE_TIMING_EXPERIMENTS=1): rounds read the key
-       // rows of round i & (m - 1), an L2-resident set (results invalid)
-        const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
-        const char* e = std::getenv("TFHE_F64_KEYROUNDS");
-        if (x && x[0] == '1' && e && e[0]) K.kround_mask = (uint32_t)std::atoi(e) - 1;
-    }
-    if (fold && !fold_possible(P)) return hipErrorInvalidValue;
     const bool wrap = fold && !fold_exact(P);
     // psi, ipsi, two polynomials, monomial tables, rotation exponents
     const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
@@ -1069,78 +1070,31 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
                            amod, acc);
     };
     const bool red = P.Q >= (1ull << 40);
-    // wave-local N = 2048 kernel for the folded sets with 2 or 3 digits (TFHE_F64W=0: the
-    // slot-layout kernel below)
-    const bool no_w = [] {  // read per launch (tests and A/B runs switch it)
-        const char* e = std::getenv("TFHE_F64W");
-        return e && e[0] == '0';
-    }();
-    const int mtw = [] {  // TFHE_F64W_MT=0..3 (k_blind_rotate_f64w's MT; read per launch)
-        const char* e = std::getenv("TFHE_F64W_MT");
-        return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
-    }();
+    const int ld = (int)P.digits - 1;
     // f64w addresses the keys with 32-bit byte offsets (buffer resource)
     const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
-    if (!no_w && fits32 && P.N == 2048 && fold && (P.digits == 2 || P.digits == 3)) {
-        // MT 1 (tables) against 0 (gathers): STD192 474 -> 385 ms, STD128Q 319 -> 288 ms (profiles/r02ae);
-        // 3 against 1: 323 -> 315 ms, 254 -> 245 ms; 2 (gathers once per round): 357 / 292 ms (profiles/r03i)
-        const int ld = (int)P.digits - 1;
-#define F64W_GO(R, W, L)                                                                     \
-    (mtw == 0   ? go(k_blind_rotate_f64w<R, W, L, 0>)                                         \
-     : mtw == 1 ? go(k_blind_rotate_f64w<R, W, L, 1>)                                         \
-     : mtw == 2 ? go(k_blind_rotate_f64w<R, W, L, 2>)                                         \
-                : go(k_blind_rotate_f64w<R, W, L, 3>))
-        const int probe = [] {  // fault probe, read per launch (tests/test_gpu_f64w_race.py)
-            const char* e = std::getenv("TFHE_F64W_PROBE");
-            return e && e[0] ? e[0] - '0' : 0;
-        }();
-        if (probe == 4) {  // timing only (results invalid): STD192 without the barrier before digit 1's pass A
-            const char* x = std::getenv("TFHE_TIMING_EXPERIMENTS");
-            if (!(x && x[0] == '1') || red || wrap || ld != 2 || mtw != 3) return hipErrorInvalidValue;
-            go(k_blind_rotate_f64w<false, false, 2, 3, 4>);
-            return hipGetLastError();
-        }
-        if (probe != 0) {  // STD128Q's instance only
-            if (!(red && wrap && ld == 1 && mtw == 3)) return hipErrorInvalidValue;
-            if (probe == 2) go(k_blind_rotate_f64w<true, true, 1, 3, 2>);
-            else if (probe == 3) go(k_blind_rotate_f64w<true, true, 1, 3, 3>);
+    if (kn.f64w && fits32 && fold && f64w_instance(red, wrap, ld)) {
+#ifdef TFHE_TEST_PROBES
+        // test library only (lib/libtfhe_hip_test.so): the fault probe of tests/test_gpu_f64w_race.py
+        // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
+        // round-2 race, wrong results) and a timing-only build (4: STD192 without the barrier before
+        // digit 1's pass A, results invalid; tools/f64w_barrier_probe.sh)
+        if (kn.probe != 0) {
+            if (kn.probe == 4 && !red && !wrap && ld == 2) go(k_blind_rotate_f64w<false, false, 2, 4>);
+            else if (kn.probe == 2 && red && wrap && ld == 1) go(k_blind_rotate_f64w<true, true, 1, 2>);
+            else if (kn.probe == 3 && red && wrap && ld == 1) go(k_blind_rotate_f64w<true, true, 1, 3>);
             else return hipErrorInvalidValue;
             return hipGetLastError();
         }
-        if (red) {
-            if (wrap) ld == 1 ? F64W_GO(true, true, 1) : F64W_GO(true, true, 2);
-            else ld == 1 ? F64W_GO(true, false, 1) : F64W_GO(true, false, 2);
-        } else {
-            if (wrap) ld == 1 ? F64W_GO(false, true, 1) : F64W_GO(false, true, 2);
-            else ld == 1 ? F64W_GO(false, false, 1) : F64W_GO(false, false, 2);
-        }
-#undef F64W_GO
+#endif
+        if (red) go(k_blind_rotate_f64w<true, true, 1>);
+        else go(k_blind_rotate_f64w<false, false, 2>);
         return hipGetLastError();
     }
-    // TFHE_F64_MT (A/B runs): 1 = LDS monomial tables for every set, 0 = gathers for every set;
-    // default: tables for Q < 2^40 (STD192 class), gathers for the reducing sets (STD128Q class)
-    const int mt_mode = [] {  // read per launch (tests and A/B runs switch it)
-        const char* e = std::getenv("TFHE_F64_MT");
-        return e && e[0] ? e[0] - '0' : 2;
-    }();
-    if (mt_mode != 2 && P.N == 2048 && fold) {
-        const bool on = mt_mode == 1;
-        if (wrap) red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, true, true>) : go(k_blind_rotate_f64<512, 4, true, true, true, false>))
-                      : (on ? go(k_blind_rotate_f64<512, 4, false, true, true, true>) : go(k_blind_rotate_f64<512, 4, false, true, true, false>));
-        else red ? (on ? go(k_blind_rotate_f64<512, 4, true, true, false, true>) : go(k_blind_rotate_f64<512, 4, true, true, false, false>))
-                 : (on ? go(k_blind_rotate_f64<512, 4, false, true, false, true>) : go(k_blind_rotate_f64<512, 4, false, true, false, false>));
-        return hipGetLastError();
-    }
-    if (wrap) {
-        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, true, true>) : go(k_blind_rotate_f64<256, 4, false, true, true>);
-        else red ? go(k_blind_rotate_f64<512, 4, true, true, true>) : go(k_blind_rotate_f64<512, 4, false, true, true>);
-    } else if (fold) {
-        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, true>) : go(k_blind_rotate_f64<256, 4, false, true>);
-        else red ? go(k_blind_rotate_f64<512, 4, true, true>) : go(k_blind_rotate_f64<512, 4, false, true>);
-    } else {
-        if (P.N == 1024) red ? go(k_blind_rotate_f64<256, 4, true, false>) : go(k_blind_rotate_f64<256, 4, false, false>);
-        else red ? go(k_blind_rotate_f64<512, 4, true, false>) : go(k_blind_rotate_f64<512, 4, false, false>);
-    }
+    if (!slot_instance(red, fold, wrap)) return hipErrorNotSupported;
+    if (wrap) go(k_blind_rotate_f64<512, 4, true, true, true>);
+    else if (fold) go(k_blind_rotate_f64<512, 4, false, true>);
+    else red ? go(k_blind_rotate_f64<512, 4, true, false>) : go(k_blind_rotate_f64<512, 4, false, false>);
     return hipGetLastError();
 }
 

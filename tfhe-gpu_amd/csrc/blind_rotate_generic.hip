@@ -673,23 +673,12 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
 // (y' = x + 2Q - v, 11 stages < 23 Q), the inverse folds its pure sums once per pass
 // (x -> (x mod 2^54) + (x >> 54) c, one mad), the accumulator update folds once and subtracts
 // Q at most once.  tools/bounds_sf.py checks every bound of this schedule.
-constexpr uint32_t SF_K = 54;
+// (SF_K and sf_mul live in device_math.hpp, shared with the VALU microbenchmark)
 
 struct SfC {
     uint64_t Q, Q2, Q9;  // Q, 2Q (forward offset), 9Q (inverse offset)
     uint32_t c;
 };
-
-__device__ __forceinline__ uint64_t sf_mul(uint64_t a, uint64_t w0, uint64_t w1, uint32_t c) {
-    const uint32_t a0 = (uint32_t)a & 0x7fffffffu, a1 = (uint32_t)(a >> 31);  // a1 < 2^30
-    uint64_t P = (uint64_t)a0 * (uint32_t)w0;
-    P += (uint64_t)a1 * (uint32_t)w1;                                        // < 2^64
-    uint64_t H = (uint64_t)a0 * (uint32_t)(w0 >> 32) + (P >> 32);
-    H += (uint64_t)a1 * (uint32_t)(w1 >> 32);                                // < 2^54
-    const uint32_t hs = (uint32_t)(H >> (SF_K - 32));
-    const uint64_t L = ((H & ((1ull << (SF_K - 32)) - 1)) << 32) | (uint32_t)P;
-    return L + (uint64_t)hs * c;
-}
 __device__ __forceinline__ uint64_t sf_fold(uint64_t x, uint32_t c) {
     return (x & ((1ull << SF_K) - 1)) + (uint64_t)(uint32_t)(x >> SF_K) * c;
 }
@@ -1250,17 +1239,11 @@ __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ i
 
 hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const DevTables& T, const void* bsk,
                                        const void* bsk_sh, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B,
-                                       hipStream_t s) {
+                                       hipStream_t s, const Knobs& kn) {
     if (B == 0) return hipSuccess;
     const size_t wb = word_bits == 32 ? 4 : 8;
-    static const bool v1 = [] {
-        const char* e = std::getenv("TFHE_GENERIC_V1");
-        return e && e[0] == '1';
-    }();
-    static const bool no_gen3 = [] {
-        const char* e = std::getenv("TFHE_GENERIC_GEN3");
-        return e && e[0] == '0';
-    }();
+    const bool v1 = kn.generic == 1;       // all digits in LDS (cross-check)
+    const bool no_gen3 = kn.generic == 2;  // v2 also at N = 2048 (cross-check)
     if (!v1 && !no_gen3 && P.N == G3_N) {
         const size_t lds = (size_t)4 * G3_N * wb + rot_exponent_bytes(P.n);  // two polynomials, forward twiddles, a'_i
         auto go3 = [&](auto tag) {
@@ -1346,7 +1329,8 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
 }
 
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
-                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s) {
+                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
+                                  const Knobs& kn) {
     if (B == 0) return hipSuccess;
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
     SfC K;
@@ -1354,10 +1338,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     const uint64_t* w1 = (const uint64_t*)sf;
     const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8 + rot_exponent_bytes(P.n);  // two polynomials, forward twiddles, monomial tables, a'_i
-    const bool no_sf2 = [] {  // read per launch (tests and A/B runs switch it)
-        const char* e = std::getenv("TFHE_SF2");
-        return e && e[0] == '0';
-    }();
+    const bool no_sf2 = !kn.sf2;  // gen3sf (cross-check)
     // sf2 addresses the keys with 32-bit byte offsets (buffer resources)
     const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
     if (!no_sf2 && fits32 && (P.digits == 1 || P.digits == 2)) {

@@ -55,6 +55,34 @@ __device__ __forceinline__ W reduce_full(W x, W r1, W Q) {
     return csub<W>(x - WordOps<W>::mulhi(x, r1) * Q, Q);
 }
 
+// Exact FP64 modular product (the arithmetic of blind_rotate_f64.hip; also timed alone by
+// tools/microbench/valu_rates.hip, which includes this header, for that kernel's roofline peak).
+// a, b integers held exactly in doubles with |a b| < 2^102:
+//     h = a*b (rounded), l = fma(a, b, -h)          a*b = h + l exactly
+//     q = rint(h / Q),   r = fma(-q, Q, h) + l      r = a*b - qQ exactly, |r| <~ Q/2
+__device__ __forceinline__ double fmodmul_f64(double a, double b, double Q, double Qinv) {
+    const double h = __dmul_rn(a, b);
+    const double l = __fma_rn(a, b, -h);
+    const double q = __builtin_rint(__dmul_rn(h, Qinv));
+    return __dadd_rn(__fma_rn(-q, Q, h), l);
+}
+
+// Special-form product for Q = 2^54 - c, c < 2^20 (the sf kernels of blind_rotate_generic.hip;
+// also timed alone by tools/microbench/valu_rates.hip).  The constant w is held as (W0, W1) =
+// (w, w 2^31 mod Q); for a lazily reduced a < 2^61, a0 = a mod 2^31, a1 = a >> 31:
+//     S = a0 W0 + a1 W1 < 2^86,   r = (S mod 2^54) + (S >> 54) c  <  2^54 + 2^32 c,   r = a w mod Q
+constexpr uint32_t SF_K = 54;
+__device__ __forceinline__ uint64_t sf_mul(uint64_t a, uint64_t w0, uint64_t w1, uint32_t c) {
+    const uint32_t a0 = (uint32_t)a & 0x7fffffffu, a1 = (uint32_t)(a >> 31);  // a1 < 2^30
+    uint64_t P = (uint64_t)a0 * (uint32_t)w0;
+    P += (uint64_t)a1 * (uint32_t)w1;                                        // < 2^64
+    uint64_t H = (uint64_t)a0 * (uint32_t)(w0 >> 32) + (P >> 32);
+    H += (uint64_t)a1 * (uint32_t)(w1 >> 32);                                // < 2^54
+    const uint32_t hs = (uint32_t)(H >> (SF_K - 32));
+    const uint64_t L = ((H & ((1ull << (SF_K - 32)) - 1)) << 32) | (uint32_t)P;
+    return L + (uint64_t)hs * c;
+}
+
 // lwe-pke.cpp:41-46 RoundqQ: floor(0.5 + (double)v * (double)q / (double)Q) % q,
 // with explicitly rounded IEEE operations (no contraction, no fast-math).
 __device__ __forceinline__ uint64_t round_qQ(uint64_t v, uint64_t q, uint64_t Q) {

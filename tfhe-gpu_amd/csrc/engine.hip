@@ -180,6 +180,7 @@ struct tfhe_ctx {
     int replicate_method = TFHE_REPLICATE_NONE;
     double replicate_ms = 0;
     size_t max_chunk = 65536;  // the reference's max_bootstapping_num, bootstrapping.cuh:140
+    Knobs kn{};                // launch choices: environment at setup, tfhe_set_knobs afterwards
     ~tfhe_ctx();  // frees every device's arena, scratch, streams (error paths included)
 };
 
@@ -188,8 +189,33 @@ namespace {
 // ---------------------------------------------------------------------------
 // setup helpers
 // ---------------------------------------------------------------------------
+// Launch knobs from the environment, once per context (tfhe_setup*): the A/B switches of earlier rounds'
+// measurements.  Afterwards only tfhe_set_knobs changes them; no launch reads the environment.
+Knobs knobs_from_env() {
+    Knobs k;
+    auto num = [](const char* name, int32_t& dst) {
+        const char* e = std::getenv(name);
+        if (e && e[0]) dst = (int32_t)std::atoi(e);
+    };
+    num("TFHE_KS_TILED_MIN", k.ks_tiled_min);
+    num("TFHE_KS_CTS", k.ks_cts);
+    num("TFHE_KS_SPLIT", k.ks_split);
+    num("TFHE_KS_PK", k.ks_pk);
+    num("TFHE_HOST_PARTS", k.host_parts);
+    num("TFHE_WIRE", k.wire);
+    num("TFHE_ACC_FLAGS", k.acc_flags);
+    num("TFHE_F64W", k.f64w);
+    num("TFHE_SF2", k.sf2);
+    num("TFHE_GENERIC", k.generic);
+    if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
+    if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;
+    k.trace = std::getenv("TFHE_TRACE") != nullptr;
+    return k;
+}
+
 tfhe_status init_derived(tfhe_ctx* c) {
     const tfhe_params& p = c->p;
+    c->kn = knobs_from_env();
     c->word_bits = word_bits_for(p);
     c->ksk_bits = ksk_bits_for(p.qKS);
     c->layout = arena_layout(p, c->word_bits);
@@ -213,6 +239,8 @@ tfhe_status init_derived(tfhe_ctx* c) {
     c->use_fast = fast_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     c->use_f64 = f64_path_supported(c->br, c->word_bits) && !(force && force[0] == '1');
     c->f64_fold = c->use_f64 && f64_fold_enabled(c->br);
+    if (c->use_f64 && !f64_instance_available(c->br, c->f64_fold)) c->f64_fold = false;
+    if (c->use_f64 && !f64_instance_available(c->br, c->f64_fold)) c->use_f64 = false;
     // Q = 2^54 - c: the special-form kernel (TFHE_SF=0 keeps the Shoup gen3 kernel)
     const char* sfe = std::getenv("TFHE_SF");
     c->use_sf = !c->use_fast && !c->use_f64 && sf_path_supported(c->br, c->word_bits) &&
@@ -432,12 +460,12 @@ tfhe_status ensure_scratch(tfhe_ctx* c, Device& d, size_t B) {
     return TFHE_OK;
 }
 
-size_t ks_tiled_min(int ksk_bits);
+size_t ks_tiled_min(const tfhe_ctx* c);
 
 // The tiled key switch's digit planes alone, for the device-resident key switch (which needs
 // none of the bootstrap scratch): grown to B only when the tiled form will run.
 tfhe_status ensure_ks_scratch(tfhe_ctx* c, Device& d, size_t B) {
-    const size_t tmin = ks_tiled_min(c->ksk_bits);
+    const size_t tmin = ks_tiled_min(c);
     if (!ks_tiled_supported(c->ks) || tmin == 0 || B < tmin || B <= d.sc.ks_cap) return TFHE_OK;
     if (d.sc_fence) HCHECK(hipEventSynchronize(d.sc_fence));
     hipFree(d.sc.ks);
@@ -457,12 +485,12 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream,
                                         d.br_done.flags ? &d.br_done : nullptr));
     } else if (c->use_f64) {
-        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream));
+        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream, c->kn));
     } else if (c->use_sf) {
-        HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream));
+        HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream, c->kn));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
-                                           amod, acc, B, d.stream));
+                                           amod, acc, B, d.stream, c->kn));
     }
     c->bootstraps += B;
     return TFHE_OK;
@@ -473,19 +501,18 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
 // latency: the tiled kernel's workgroups each sweep all N dKS rows, ~1 ms for STD128 at any
 // batch up to 8192, while the u16 gather costs 1.87 ms per 8192 (crossover ~4400); for
 // u32/u64 keys the gather is 2-10x slower already at 1024 (profiles/r02_ks).
-size_t ks_tiled_min(int ksk_bits) {
-    const char* e = std::getenv("TFHE_KS_TILED_MIN");  // read per call: tests and A/B runs switch it
-    if (e) return (size_t)std::strtoull(e, nullptr, 10);
-    return ksk_bits == 16 ? 4096 : 256;
+size_t ks_tiled_min(const tfhe_ctx* c) {
+    if (c->kn.ks_tiled_min >= 0) return (size_t)c->kn.ks_tiled_min;  // knob (TFHE_KS_TILED_MIN)
+    return c->ksk_bits == 16 ? 4096 : 256;
 }
 
 // the tiled form runs when d.sc.ks holds B ciphertexts (ensure_scratch / ensure_ks_scratch)
 tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, uint64_t* out, size_t B) {
     if (fmod < 2) return fail(TFHE_ERR_INVALID_ARGUMENT, "fmod < 2");
-    const size_t tmin = ks_tiled_min(c->ksk_bits);
+    const size_t tmin = ks_tiled_min(c);
     if (tmin && B >= tmin && d.sc.ks && B <= d.sc.ks_cap) {
         const hipError_t e = launch_ks_tiled(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb,
-                                             ext, fmod, out, B, d.sc.ks, d.stream);
+                                             ext, fmod, out, B, d.sc.ks, d.stream, c->kn);
         if (e != hipErrorNotSupported) {
             HCHECK(e);
             return TFHE_OK;
@@ -848,9 +875,8 @@ tfhe_status ensure_flags(Device& d, size_t words) {
 // blind rotations (2048 workgroups each: a launch tail apiece), the key switches (~1 ms each at
 // any batch) and the runtime's blit kernels for the sub-8 MiB copies, which run beside the
 // blind rotation, cost more than the 3.4 ms of PCIe they hide.
-size_t host_parts(size_t cnt) {
-    const char* e = std::getenv("TFHE_HOST_PARTS");  // read per call (A/B runs)
-    const size_t want = e ? (size_t)std::max(1, std::atoi(e)) : 1;
+size_t host_parts(const tfhe_ctx* c, size_t cnt) {
+    const size_t want = (size_t)std::max(1, c->kn.host_parts);  // knob (TFHE_HOST_PARTS)
     return std::min(want, std::max<size_t>(1, cnt / 256));
 }
 
@@ -871,17 +897,8 @@ tfhe_status ensure_io_set(Scratch& sc, size_t words, size_t pk_bytes) {
 }
 
 // PCIe wire width of an array: the narrowest of u16 / u32 / u64 that holds every value (inputs:
-// the OR of the words; outputs: the op's bound).  TFHE_WIRE=0 keeps u64 (A/B runs; read per call).
-bool wire_narrowing() {
-    const char* e = std::getenv("TFHE_WIRE");
-    return !(e && e[0] == '0');
-}
-// Completion-flag output of the host-array EvalAcc (d2h_flagged); TFHE_ACC_FLAGS=0 turns it off (A/B
-// runs; read per call).
-bool wire_flags() {
-    const char* e = std::getenv("TFHE_ACC_FLAGS");
-    return !(e && e[0] == '0');
-}
+// the OR of the words; outputs: the op's bound); the wire knob 0 (TFHE_WIRE=0) keeps u64.  The
+// completion-flag output of the host-array EvalAcc (d2h_flagged) follows the acc_flags knob.
 
 // Value bounds of the runner's arrays (0: unknown): an array crosses PCIe in the narrowest of u16 /
 // u32 / u64 that holds its bound (h2d_staged / d2h_staged).  Inputs are checked as they are packed
@@ -899,10 +916,10 @@ tfhe_status run_lwe_batch_v(tfhe_ctx* c, size_t B, const HostIn& in1, const Host
     const size_t w1 = in1.w, w2 = in2.empty() ? 0 : in2.w, wo = out.w;
     const bool has2 = !in2.empty(), has_oi = !out_in.empty();
     return for_each_shard(c, B, [&](Device& d, size_t lo, size_t cnt) -> tfhe_status {
-        const size_t parts = host_parts(cnt);
+        const size_t parts = host_parts(c, cnt);
         const size_t sub = std::min((cnt + parts - 1) / parts, c->max_chunk);
         const size_t w_in2 = has2 ? w2 : 0, io_words = sub * (w1 + w_in2 + wo);
-        const bool nar = wire_narrowing();
+        const bool nar = c->kn.wire != 0;
         auto width = [nar](uint64_t lim) { return nar && lim ? wire_bytes(lim - 1) : 8; };
         const int wb1 = width(wl.in1), wb2 = has2 ? width(wl.in2) : 8, wbi = has_oi ? width(wl.out_in) : 8;
         const int wbo = width(wl.out);
@@ -916,7 +933,7 @@ tfhe_status run_lwe_batch_v(tfhe_ctx* c, size_t B, const HostIn& in1, const Host
         const hipStream_t cs = d.stream, xs = d.stream2;
         uint64_t* io[2] = {d.sc.io, d.sc2.io};
         char* pk[2] = {(char*)d.sc.pk, (char*)d.sc2.pk};
-        static const bool trace = std::getenv("TFHE_TRACE") != nullptr;
+        const bool trace = c->kn.trace != 0;
         auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         const double t0 = trace ? now() : 0;
         auto dout_of = [&](int set) { return io[set] + sub * (w1 + w_in2); };
@@ -949,7 +966,7 @@ tfhe_status run_lwe_batch_v(tfhe_ctx* c, size_t B, const HostIn& in1, const Host
                 break;
             }
             // flag_out (EvalAcc): one sub-batch lets its blind rotation flag finished ciphertexts
-            const bool flagged = flag_out && n_sub == 1 && wire_flags();
+            const bool flagged = flag_out && n_sub == 1 && c->kn.acc_flags != 0;
             if (flagged) {
                 st = ensure_flags(d, 4 * b);
                 if (st != TFHE_OK) break;
@@ -1377,6 +1394,32 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
     });
 }
 
+static_assert(sizeof(tfhe_knobs) == sizeof(Knobs), "tfhe_knobs mirrors tfhe::Knobs field by field");
+
+tfhe_status tfhe_get_knobs(tfhe_ctx* c, tfhe_knobs* out) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (!out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null output");
+        std::memcpy(out, &c->kn, sizeof(Knobs));
+        return TFHE_OK;
+    });
+}
+
+tfhe_status tfhe_set_knobs(tfhe_ctx* c, const tfhe_knobs* in) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (!in) return fail(TFHE_ERR_INVALID_ARGUMENT, "null knobs");
+        Knobs k;
+        std::memcpy(&k, in, sizeof(Knobs));
+        if (k.generic < 0 || k.generic > 2 || k.ks_cts < 0 || k.ks_cts > 2 || k.ks_split < 1 || k.host_parts < 1)
+            return fail(TFHE_ERR_INVALID_ARGUMENT, "knob out of range");
+        if (k.probe != 0 && !f64_test_probes_compiled())
+            return fail(TFHE_ERR_UNSUPPORTED, "probe builds exist only in the test library (libtfhe_hip_test.so)");
+        c->kn = k;
+        return TFHE_OK;
+    });
+}
+
 tfhe_status tfhe_shard_range(size_t total, int world, int rank, size_t* lo, size_t* hi) {
     if (world < 1 || rank < 0 || rank >= world || !lo || !hi) return fail(TFHE_ERR_INVALID_ARGUMENT, "bad world/rank");
     size_t l, cnt;
@@ -1545,6 +1588,28 @@ tfhe_status tfhe_eval_bin_gate(tfhe_ctx* c, int gate, size_t B, const uint64_t* 
     });
 }
 
+extern "C++" {  // (templates need C++ linkage inside the extern "C" block)
+namespace {
+// Frame of the device-resident fused ops: the device holding d_out, scratch for B ciphertexts, the
+// caller's stream (ordered after every earlier user of the device's scratch, sc_fence).
+template <typename F>
+tfhe_status run_device_op(tfhe_ctx* c, size_t B, const void* d_out, void* stream, F&& body) {
+    Device* dp = nullptr;
+    SCHECK(device_for(c, d_out, dp));
+    Device& d = *dp;
+    HCHECK(hipSetDevice(d.id));
+    SCHECK(ensure_scratch(c, d, B));
+    hipStream_t saved = d.stream;
+    if (stream) d.stream = (hipStream_t)stream;
+    tfhe_status st = sc_acquire(d, d.stream);
+    if (st == TFHE_OK) st = body(d);
+    const tfhe_status rel = sc_release(d, d.stream);  // even after a failed launch: later users wait on it
+    d.stream = saved;
+    return st != TFHE_OK ? st : rel;
+}
+}  // namespace
+}  // extern "C++"
+
 tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* c, int gate, size_t B, const uint64_t* d_ct1, const uint64_t* d_ct2,
                                       uint64_t q, uint64_t* d_out, void* stream) {
     return guarded([&]() -> tfhe_status {
@@ -1552,18 +1617,54 @@ tfhe_status tfhe_eval_bin_gate_device(tfhe_ctx* c, int gate, size_t B, const uin
         if (gate < TFHE_OR || gate > TFHE_XNOR) return fail(TFHE_ERR_INVALID_ARGUMENT, "unknown gate");
         if (B == 0) return TFHE_OK;
         if (!d_ct1 || !d_ct2 || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
-        Device* dp = nullptr;
-        SCHECK(device_for(c, d_out, dp));
-        Device& d = *dp;
-        HCHECK(hipSetDevice(d.id));
-        SCHECK(ensure_scratch(c, d, B));
-        hipStream_t saved = d.stream;
-        if (stream) d.stream = (hipStream_t)stream;
-        tfhe_status st = sc_acquire(d, d.stream);
-        if (st == TFHE_OK) st = dev_gate(c, d, gate, d_ct1, d_ct2, q, d_out, B);
-        const tfhe_status rel = sc_release(d, d.stream);  // even after a failed launch: later users wait on it
-        d.stream = saved;
-        return st != TFHE_OK ? st : rel;
+        return run_device_op(c, B, d_out, stream,
+                             [&](Device& d) { return dev_gate(c, d, gate, d_ct1, d_ct2, q, d_out, B); });
+    });
+}
+
+tfhe_status tfhe_eval_func_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct, uint64_t q, const uint64_t* d_lut,
+                                  int per_ct_lut, uint64_t* d_out, void* stream) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!d_ct || !d_lut || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        if (q < 4 || (2ull * c->p.N) % q) return fail(TFHE_ERR_INVALID_ARGUMENT, "q must divide 2N");
+        // the first LUT classifies the batch (binfhe-base-scheme.cpp:697-698): q words to the host
+        std::vector<uint64_t> lut0(q);
+        hipStream_t s = stream ? (hipStream_t)stream : nullptr;
+        {
+            Device* dp = nullptr;
+            SCHECK(device_for(c, d_out, dp));
+            HCHECK(hipSetDevice(dp->id));
+            if (!s) s = dp->stream;
+            HCHECK(hipMemcpyAsync(lut0.data(), d_lut, q * 8, hipMemcpyDeviceToHost, s));
+            HCHECK(hipStreamSynchronize(s));
+        }
+        const int prop = check_input_function(lut0.data(), q, q);
+        return run_device_op(c, B, d_out, stream, [&](Device& d) {
+            return dev_func(c, d, prop, d_ct, q, d_lut, per_ct_lut ? q : 0, d_out, B);
+        });
+    });
+}
+
+tfhe_status tfhe_eval_floor_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct, uint64_t mod, uint32_t roundbits,
+                                   uint64_t* d_out, void* stream) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!d_ct || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        return run_device_op(c, B, d_out, stream,
+                             [&](Device& d) { return dev_floor(c, d, d_ct, mod, roundbits, d_out, B); });
+    });
+}
+
+tfhe_status tfhe_eval_sign_device(tfhe_ctx* c, size_t B, const uint64_t* d_ct, uint64_t mod, uint64_t* d_out,
+                                  void* stream) {
+    return guarded([&]() -> tfhe_status {
+        SCHECK(check_ctx(c));
+        if (B == 0) return TFHE_OK;
+        if (!d_ct || !d_out) return fail(TFHE_ERR_INVALID_ARGUMENT, "null argument");
+        return run_device_op(c, B, d_out, stream, [&](Device& d) { return dev_sign(c, d, d_ct, mod, d_out, B); });
     });
 }
 

@@ -14,6 +14,24 @@ struct BRParams {
     uint64_t r1;  // floor(2^b / Q), b = word bits, for lazy-sum reduction
 };
 
+// Launch choices of one context: read from the environment once, at setup (engine.hip
+// knobs_from_env), changed afterwards only through tfhe_set_knobs (tests, A/B runs).  The C-ABI
+// mirror is tfhe_knobs (include/tfhe_hip.h); the launchers below take them by reference.
+struct Knobs {
+    int32_t ks_tiled_min = -1;  // smallest batch on the tiled key switch; -1: by key width, 0: never
+    int32_t ks_cts = 0;         // ciphertexts per thread of the tiled key switch; 0: by key width / batch
+    int32_t ks_split = 16;      // most block groups the key-switch steps split over at small batches; 1: none
+    int32_t ks_pk = 1;          // 0: no packed u16 column sums
+    int32_t host_parts = 1;     // sub-batches per device of the host-array runner
+    int32_t wire = 1;           // 0: u64 PCIe words (no narrow wire format)
+    int32_t acc_flags = 1;      // 0: no completion-flagged EvalAcc output
+    int32_t f64w = 1;           // 0: slot-layout FP64 kernel instead of the wave-local f64w
+    int32_t sf2 = 1;            // 0: gen3sf instead of the wave-local sf2
+    int32_t generic = 0;        // 0: gen3 / v2 by N; 1: v1 (all digits in LDS); 2: v2 also at N = 2048
+    int32_t trace = 0;          // host-array runner timeline on stderr
+    int32_t probe = 0;          // test library only (TFHE_TEST_PROBES): f64w fault probe / timing builds
+};
+
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
 struct DevTables {
     const void* psi;     // [N]  forward twiddles, bit-reversed order
@@ -39,7 +57,7 @@ struct BRDone {
 //   bsk/bsk_sh: [n][2][dG2][2][N] in W, NTT domain, scaled by N^-1.
 hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const DevTables& T, const void* bsk,
                                        const void* bsk_sh, const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B,
-                                       hipStream_t s);
+                                       hipStream_t s, const Knobs& kn);
 
 // Fast STD128-class blind rotation (W = u32, N = 1024, dG2 = 8): register-resident
 // transforms, one wavefront per ciphertext.  Returns hipErrorNotSupported when the
@@ -68,18 +86,22 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
                                      size_t B, hipStream_t s, BRDone* dn = nullptr);
 
-// Exact-FP64 blind rotation for 2^32 <= Q < 2^40 (STD192 class): keys/tables as centred
-// doubles derived on device from the generic (u64) arena.
+// Exact-FP64 blind rotation for 2^32 <= Q < 2^50, N = 2048 (STD192 / STD192Q / STD128Q classes):
+// keys/tables as centred doubles derived on device from the generic (u64) arena.
 bool f64_path_supported(const BRParams& P, int word_bits);
+// an instance exists for this context's (Q width, top-digit fold) combination (f64w or slot layout)
+bool f64_instance_available(const BRParams& P, bool fold);
 size_t bsk_f64_bytes(const BRParams& P);
 // fold: eliminate the top digit's transforms (keys packed accordingly); only when
 // f64_fold_enabled(P) (thr = 0; WRAP correction where the top digit is not always exact;
 // TFHE_F64_FOLD=1 folds only exact sets, 0 turns it off).
 bool f64_fold_enabled(const BRParams& P);
+// true only in the test library (blind_rotate_f64.hip built with -DTFHE_TEST_PROBES)
+bool f64_test_probes_compiled();
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
                                hipStream_t s);
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold, const uint64_t* a,
-                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, const Knobs& kn);
 
 // Special-form u64 blind rotation (gen3sf, blind_rotate_generic.hip) for N = 2048 and
 // Q = 2^54 - c, c < 2^20 (the logQ / arbFunc contexts): constants as (w, w 2^31 mod Q), five
@@ -88,7 +110,8 @@ bool sf_path_supported(const BRParams& P, int word_bits);
 size_t sf_bytes(const BRParams& P);
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
-                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s);
+                                  const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
+                                  const Knobs& kn);
 
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
 //   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.
@@ -106,7 +129,7 @@ hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const v
 size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B);
 bool ks_tiled_supported(const KSParams& P);
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
-                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s);
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn);
 
 // ---- test vectors, extraction and LWE glue (binfhe-base-scheme.cpp) ----
 enum TvMode : uint32_t {

@@ -308,21 +308,23 @@ __global__ void __launch_bounds__(256) k_ks_combine(KSParams P, const uint64_t* 
     }
 }
 
-// Splits for a batch: enough blocks for two per CU (512), at most kMaxSplit, dividing the stage pairs
-constexpr uint32_t kMaxSplit = 4, kSplitMaxB = 2048;
-uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B) {
-    const char* e = std::getenv("TFHE_KS_SPLIT");  // A/B runs (read per call): 1 = no split
-    const uint32_t cap = e ? (uint32_t)std::max(1, std::atoi(e)) : kMaxSplit;
+// Splits for a batch: enough blocks for two per CU (512), dividing the stage pairs; at most 4 up to
+// kSplitMaxB ciphertexts, at most kMaxSplit up to kWideSplitMaxB (round 4: a 128- or 256-ciphertext
+// batch has one ciphertext tile, 32 blocks for STD128Q -- the C5 shard of 1024 over 8 GPUs)
+constexpr uint32_t kMaxSplit = 16, kSplitMaxB = 2048, kWideSplitMaxB = 512;
+uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B, const Knobs& kn) {
+    const uint32_t cap = std::min<uint32_t>((uint32_t)std::max(1, kn.ks_split),  // knob (TFHE_KS_SPLIT): 1 = no split
+                                            B <= kWideSplitMaxB ? kMaxSplit : 4);
     const uint32_t pairs = P.N * P.dKS / (2 * GMAX);
     uint32_t z = 1;
-    while (2 * z <= std::min(cap, kMaxSplit) && B <= kSplitMaxB && blocks * z < 512 && pairs % (2 * z) == 0) z *= 2;
+    while (2 * z <= cap && B <= kSplitMaxB && blocks * z < 512 && pairs % (2 * z) == 0) z *= 2;
     return z;
 }
 
 template <typename KW, typename ACC, int CT, int CTS, int G = 4, bool PK = false>
 hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, const uint32_t* dig,
                         const uint64_t* bq, size_t B, size_t Bp, uint64_t fmod, uint64_t* out, uint64_t* part,
-                        hipStream_t s) {
+                        hipStream_t s, const Knobs& kn) {
     constexpr int STRIDE = CT * sizeof(KW) + 16;
     const size_t lds = 2 * (size_t)G * P.baseKS * STRIDE + 2 * (size_t)G * P.baseKS * sizeof(KW);
     // staging slots per thread and stage: G steps, ceil(pieces per step / KT) slots each (k_ks_tiled)
@@ -335,7 +337,7 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = (P.n_pad + CT - 1) / CT;
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
-    const uint32_t nsplit = ks_nsplit(P, blocks, B);
+    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn);
     hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp,
                        nct, ncol, fmod, out, nsplit, part);
     if (nsplit > 1) {
@@ -353,7 +355,8 @@ size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; 
 }  // namespace
 
 size_t ks_tiled_part_words(const KSParams& P, size_t B) {  // split partial sums (ks_nsplit)
-    return (size_t)kMaxSplit * std::min(B, (size_t)kSplitMaxB) * (P.n + 1);
+    return std::max((size_t)kMaxSplit * std::min(B, (size_t)kWideSplitMaxB), (size_t)4 * std::min(B, (size_t)kSplitMaxB)) *
+           (P.n + 1);
 }
 
 size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
@@ -368,7 +371,7 @@ bool ks_tiled_supported(const KSParams& P) {
 }
 
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
-                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s) {
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn) {
     if (B == 0) return hipSuccess;
     if (!ks_tiled_supported(P)) return hipErrorNotSupported;
     const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
@@ -388,26 +391,24 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     // ciphertexts per thread: two halve the KSK segments streamed per ciphertext; they pay for u64 keys
     // (ARB12 B = 4096 13.8 -> 12.5 ms, logQ = 23 B = 1024 4.06 -> 3.66) and for u32 keys at large
     // batches (STD192 8192 5.81 -> 5.24), not for STD128Q at 1024 (1.26 -> 1.40) or the packed u16
-    // form (profiles/r03ks, r03ks2, r03z).  TFHE_KS_CTS overrides (A/B runs and tests; read per call).
-    const char* ev = std::getenv("TFHE_KS_CTS");
-    const int cts = ev ? std::atoi(ev) : (ksk_bits == 64 || (ksk_bits == 32 && B >= 4096)) ? 2 : 1;
+    // form (profiles/r03ks, r03ks2, r03z).  The ks_cts knob (TFHE_KS_CTS) overrides (A/B runs and tests).
+    const int cts = kn.ks_cts ? kn.ks_cts : (ksk_bits == 64 || (ksk_bits == 32 && B >= 4096)) ? 2 : 1;
     switch (ksk_bits) {
         case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
-            // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (TFHE_KS_PK=0: u32 sums, A/B runs)
-            if ((P.qKS & (P.qKS - 1)) == 0 && P.qKS <= (1u << 16) && !(std::getenv("TFHE_KS_PK") &&
-                                                                        std::getenv("TFHE_KS_PK")[0] == '0'))
-                return launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
-            return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
+            // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (ks_pk knob 0: u32 sums, A/B runs)
+            if ((P.qKS & (P.qKS - 1)) == 0 && P.qKS <= (1u << 16) && kn.ks_pk)
+                return launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
+            return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
         case 32:
             // u32 sums also when they wrap mod 2^32 harmlessly: qKS a power of two (STD128Q: 2^25)
             if (acc32 || (P.qKS & (P.qKS - 1)) == 0)
-                return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
-                                : launch_tiled<uint32_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
-            return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
-                            : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
+                return cts == 2 ? launch_tiled<uint32_t, uint32_t, 32, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
+                                : launch_tiled<uint32_t, uint32_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
+            return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
+                            : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
         default:
-            return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s)
-                            : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s);
+            return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
+                            : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
     }
 }
 

@@ -12,7 +12,8 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
-ABI_VERSION = 4  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays)
+ABI_VERSION = 5  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays;
+                 # 5: device-resident EvalFunc / EvalFloor / EvalSign)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -46,6 +47,15 @@ class Info(C.Structure):
     _fields_ = [("num_devices", C.c_int), ("word_bits", C.c_int), ("bsk_device_bytes", C.c_uint64),
                 ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64),
                 ("br_kernel", C.c_int), ("replicate_method", C.c_int), ("replicate_ms", C.c_double)]
+
+
+class Knobs(C.Structure):
+    """tfhe_knobs: launch choices of a context (include/tfhe_hip.h), environment at setup, then tfhe_set_knobs."""
+    _fields_ = [(k, C.c_int32) for k in ("ks_tiled_min", "ks_cts", "ks_split", "ks_pk", "host_parts", "wire",
+                                         "acc_flags", "f64w", "sf2", "generic", "trace", "probe")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
@@ -85,12 +95,17 @@ _SIGS = {
     "tfhe_eval_bin_gate_device": ([VP, C.c_int, SZ, VP, VP, U64, VP, VP], C.c_int),
     "tfhe_eval_acc_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
     "tfhe_mkm_switch_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
+    "tfhe_eval_func_device": ([VP, SZ, VP, U64, VP, C.c_int, VP, VP], C.c_int),
+    "tfhe_eval_floor_device": ([VP, SZ, VP, U64, C.c_uint32, VP, VP], C.c_int),
+    "tfhe_eval_sign_device": ([VP, SZ, VP, U64, VP, VP], C.c_int),
     "tfhe_export_key_image": ([VP, VP, SZ, VP], C.c_int),
     "tfhe_setup_from_key_image": ([C.POINTER(VP), P, VP, SZ, C.c_int], C.c_int),
     "tfhe_save_key_image": ([VP, C.c_char_p], C.c_int),
     "tfhe_setup_from_key_file": ([C.POINTER(VP), P, C.c_char_p, C.c_int], C.c_int),
     "tfhe_get_info": ([VP, C.POINTER(Info)], C.c_int),
     "tfhe_host_selftest": ([P], C.c_int),
+    "tfhe_get_knobs": ([VP, C.POINTER(Knobs)], C.c_int),
+    "tfhe_set_knobs": ([VP, C.POINTER(Knobs)], C.c_int),
 }
 
 
@@ -110,14 +125,17 @@ def exported_symbols() -> list[str]:
     return sorted(set(re.findall(r"\b(tfhe_[a-z0-9_]+)\s*\(", txt)))
 
 
-_lib = None
+TEST_LIB = os.path.join(_PKG, "lib", "libtfhe_hip_test.so")  # + fault-probe / timing builds (tests only)
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB):
-            raise TfheError(-1, "load", f"{_LIB} missing: run tfhe_amd.build() (make -C tfhe-gpu_amd)")
+def lib(path: str | None = None):
+    """The product library (or `path`, e.g. TEST_LIB), loaded once per path."""
+    path = path or _LIB
+    L = _libs.get(path)
+    if L is None:
+        if not os.path.exists(path):
+            raise TfheError(-1, "load", f"{path} missing: run tfhe_amd.build() (make -C tfhe-gpu_amd)")
         # One HIP runtime per process: torch wheels bundle libamdhip64/libhsa-runtime64
         # with the same sonames as /opt/rocm's but are NEEDED under unversioned names,
         # so loading ours first would put two HSA runtimes on one GPU and torch would
@@ -126,7 +144,7 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        L = C.CDLL(_LIB)
+        L = C.CDLL(path)
         for name, (args, res) in _SIGS.items():
             fn = getattr(L, name, None)  # an older build (TFHE_LIB A/B runs) may lack a newer entry point
             if fn is None:
@@ -134,15 +152,15 @@ def lib():
             fn.argtypes = args
             fn.restype = res
         if L.tfhe_abi_version() != ABI_VERSION:  # the structs above mirror this ABI version
-            raise TfheError(-1, "load", f"{_LIB} has ABI {L.tfhe_abi_version()}, binding expects {ABI_VERSION}: "
+            raise TfheError(-1, "load", f"{path} has ABI {L.tfhe_abi_version()}, binding expects {ABI_VERSION}: "
                                         "rebuild (make -C tfhe-gpu_amd)")
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return L
 
 
-def check(status: int, where: str):
+def check(status: int, where: str, L=None):
     if status != 0:
-        msg = lib().tfhe_last_error().decode(errors="replace")
+        msg = (L or lib()).tfhe_last_error().decode(errors="replace")
         raise TfheError(status, where, msg)
 
 

@@ -72,6 +72,14 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(x: float, device) -> list[float]:
+    """Every rank's value of x, in rank order (per-rank kernel times in the bench line)."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def sum_over_ranks(x: int, device) -> int:
     t = torch.tensor([int(x)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)

@@ -2,7 +2,7 @@
 """Host-array entry point (the drop-in boundary: host buffers in and out, PCIe inside the
 timed call) against the device-resident entry point on the same box, STD128 NAND.
 Usage: python3 tools/host_path_bench.py [--batch 8192] [--reps 5]
-Env TFHE_HOST_PARTS (sub-batches per device) is read by the engine per call."""
+The host_parts knob (sub-batches per device) is set per variant through tfhe_set_knobs."""
 import argparse
 import json
 import os
@@ -59,7 +59,7 @@ def main():
     for rnd in range(2):  # alternate, so box drift hits every variant
         res.setdefault("device_ms", []).append(round(timeit(dev) * 1e3, 2))
         for parts in args.parts.split(","):
-            os.environ["TFHE_HOST_PARTS"] = parts
+            ctx.set_knobs(host_parts=int(parts))
             res.setdefault(f"host_parts{parts}_ms", []).append(round(timeit(host) * 1e3, 2))
     ref = ctx.EvalBinGate("NAND", c1[:64], c2[:64])
     res["host_equals_device"] = bool(np.array_equal(out[:64], ref)) and bool(

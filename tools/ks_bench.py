@@ -2,7 +2,10 @@
 """Key-switch (MKM) kernel A/B on one MI355X: the per-ciphertext gather (k_mkm) against
 the batch-tiled form (ks_tiled.hip), device-resident inputs, HIP events on the launch
 stream.  Both outputs must be equal.  One JSON line per configuration.
-Usage: python3 tools/ks_bench.py [STD128 STD192 STD128Q ARB12 LOGQ23] [--reps 3]
+Usage: python3 tools/ks_bench.py [STD128 STD192 STD128Q ARB12 LOGQ23] [--reps 3] [--batches 1,16,128]
+                                 [--splits 4,16]
+--batches sweeps the batch (one context per configuration); --splits times the tiled form at each
+ks_split cap (the knob; the engine caps it at 4 above 512 ciphertexts).
 """
 import argparse
 import json
@@ -28,6 +31,8 @@ def main():
     ap.add_argument("configs", nargs="*", default=list(CONFIGS))
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="override the batch")
+    ap.add_argument("--batches", default="", help="comma-separated batch sweep")
+    ap.add_argument("--splits", default="16", help="comma-separated ks_split caps for the tiled form")
     args = ap.parse_args()
     import torch
 
@@ -35,41 +40,41 @@ def main():
     from tfhe_amd import capi
 
     for name in args.configs:
-        mk, B = CONFIGS[name]
-        B = args.batch or B
+        mk, B0 = CONFIGS[name]
+        batches = [int(x) for x in args.batches.split(",")] if args.batches else [args.batch or B0]
         p = mk(capi)
         rs = np.random.default_rng(3)
         bsk = rs.integers(0, p.Q, p.bsk_words(), dtype=np.uint64)
         ksk = rs.integers(0, p.qKS, p.ksk_words(), dtype=np.uint64)
         ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
         del bsk, ksk
-        ext = torch.from_numpy(rs.integers(0, p.Q, (B, p.N + 1), dtype=np.uint64).view(np.int64)).cuda()
-        outs = {}
-        res = {"config": name, "batch": B, "N": p.N, "n": p.n, "qKS": p.qKS, "baseKS": p.baseKS, "dKS": p.dKS}
+        full = torch.from_numpy(rs.integers(0, p.Q, (max(batches), p.N + 1), dtype=np.uint64).view(np.int64)).cuda()
         s = torch.cuda.Stream()
-        for mode, tmin in (("gather", "0"), ("tiled", "1")):
-            os.environ["TFHE_KS_TILED_MIN"] = tmin
-            out = torch.empty((B, p.n + 1), dtype=torch.int64, device="cuda")
-            call = lambda: capi.check(capi.lib().tfhe_mkm_switch_device(ctx.handle, B, ext.data_ptr(), p.q,
-                                                                        out.data_ptr(), s.cuda_stream), "mkm")
-            call()
-            s.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(args.reps):
+        for B in batches:
+            ext = full[:B].contiguous()
+            outs = {}
+            res = {"config": name, "batch": B, "N": p.N, "n": p.n, "qKS": p.qKS, "baseKS": p.baseKS, "dKS": p.dKS}
+            modes = [("gather", 0, 16)] + [(f"tiled_split{z}", 1, int(z)) for z in args.splits.split(",")]
+            for mode, tmin, split in modes:
+                ctx.set_knobs(ks_tiled_min=tmin, ks_split=split)
+                out = torch.empty((B, p.n + 1), dtype=torch.int64, device="cuda")
+                call = lambda: capi.check(capi.lib().tfhe_mkm_switch_device(ctx.handle, B, ext.data_ptr(), p.q,
+                                                                            out.data_ptr(), s.cuda_stream), "mkm")
                 call()
-            e1.record(s)
-            s.synchronize()
-            ms = e0.elapsed_time(e1) / args.reps
-            outs[mode] = out.cpu().numpy()
-            res[f"{mode}_ms"] = round(ms, 3)
-        os.environ.pop("TFHE_KS_TILED_MIN", None)
-        res["equal"] = bool(np.array_equal(outs["gather"], outs["tiled"]))
-        res["speedup"] = round(res["gather_ms"] / res["tiled_ms"], 2)
-        print(json.dumps(res), flush=True)
+                s.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(args.reps):
+                    call()
+                e1.record(s)
+                s.synchronize()
+                outs[mode] = out.cpu().numpy()
+                res[f"{mode}_ms"] = round(e0.elapsed_time(e1) / args.reps, 3)
+            ctx.set_knobs(ks_tiled_min=-1, ks_split=16)
+            res["equal"] = all(np.array_equal(outs["gather"], v) for v in outs.values())
+            print(json.dumps(res), flush=True)
         ctx.GPUClean()
-        del ext
-
+        del full
 
 if __name__ == "__main__":
     main()

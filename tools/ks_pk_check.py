@@ -1,6 +1,6 @@
 """Tiled key switch (each packing form, split on / off) against the gather form at three batches;
 prints mismatching columns (the check that found the bit_cast miscompile)."""
-import os, sys, numpy as np
+import sys, numpy as np
 sys.path[:0] = ["tfhe-gpu_amd"]
 import tfhe_amd
 cp = tfhe_amd.params_from_set("STD128")
@@ -10,11 +10,11 @@ ksk = rs.integers(0, cp.qKS, cp.ksk_words(), dtype=np.uint64)
 ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
 for B in (300, 1029, 5000):
     ext = rs.integers(0, cp.Q, (B, cp.N + 1), dtype=np.uint64)
-    os.environ["TFHE_KS_TILED_MIN"] = "0"; g = ctx.MKMSwitch(ext, cp.q)
-    os.environ["TFHE_KS_TILED_MIN"] = "1"
+    ctx.set_knobs(ks_tiled_min=0); g = ctx.MKMSwitch(ext, cp.q)
+    ctx.set_knobs(ks_tiled_min=1)
     for pk in ("0", "1"):
         for sp in ("1", "4"):
-            os.environ["TFHE_KS_PK"] = pk; os.environ["TFHE_KS_SPLIT"] = sp
+            ctx.set_knobs(ks_pk=int(pk), ks_split=int(sp))
             t = ctx.MKMSwitch(ext, cp.q)
             bad = np.argwhere(t != g)
             print(B, "pk", pk, "split", sp, "mismatches", len(bad), "cols", sorted(set(bad[:, 1].tolist()))[:12], "cts", sorted(set(bad[:, 0].tolist()))[:8], flush=True)

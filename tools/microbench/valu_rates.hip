@@ -10,6 +10,8 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "../../tfhe-gpu_amd/csrc/device_math.hpp"
+
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
     fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
 
@@ -213,6 +215,55 @@ __global__ void k_modmul_f64(double* out, int iters, uint32_t seed) {
     out[t] = s;
 }
 
+// The products the N = 2048 kernels actually issue, from the kernels' own header (device_math.hpp):
+// fmodmul_f64 (blind_rotate_f64.hip: 6 FP64 instructions) at STD192's Q = 2^37 - 2^17 + 1 and
+// STD128Q's Q = 2^50 - 2^14 + 1 with full-width centred operands, and sf_mul (the sf kernels of
+// blind_rotate_generic.hip: five v_mad_u64_u32 + shifts) at Q = 2^54 - 77823 with lazy operands.
+// Each lane runs 8 independent chains x = x * w mod Q, w a per-chain constant (a key / twiddle).
+template <uint64_t QV>
+__global__ void k_modmul_fmod(double* out, int iters, uint32_t seed) {
+    uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
+    const double Q = (double)QV, Qinv = 1.0 / Q, half = (double)(QV >> 1);
+    double x[8], w[8];
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t h = (uint64_t)(seed + t * 8 + k) * 0x9E3779B97F4A7C15ull;
+        x[k] = (double)(int64_t)((h >> 7) % QV) - half;
+        w[k] = (double)(int64_t)(((h * 0xBF58476D1CE4E5B9ull) >> 9) % QV) - half;
+    }
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = tfhe::fmodmul_f64(x[k], w[k], Q, Qinv);
+    }
+    double s = 0;
+    for (int k = 0; k < 8; ++k) s += x[k];
+    out[t] = s;
+}
+__global__ void k_modmul_sf54(uint64_t* out, int iters, uint32_t seed) {
+    uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
+    constexpr uint64_t Q = (1ull << 54) - 77823;
+    constexpr uint32_t c = 77823;
+    uint64_t x[8], w0[8], w1[8];
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t h = (uint64_t)(seed + t * 8 + k) * 0x9E3779B97F4A7C15ull;
+        x[k] = (h >> 3) % Q;
+        w0[k] = ((h * 0xBF58476D1CE4E5B9ull) >> 9) % Q;
+        // W1 = w 2^31 mod Q, the form k_pack_sf stores
+        const uint64_t y = ((w0[k] & ((1ull << 23) - 1)) << 31) + (w0[k] >> 23) * c;
+        w1[k] = y >= Q ? y - Q : y;
+    }
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = tfhe::sf_mul(x[k], w0[k], w1[k], c);
+    }
+    uint64_t s = 0;
+    for (int k = 0; k < 8; ++k) s ^= x[k];
+    out[t] = s;
+}
+
 template <typename T, typename K>
 static void run(const char* name, K kern, int ops_per_iter_lane, double peak_lane_ops) {
     const int blocks = 256 * 8, threads = 256, iters = 2000;
@@ -269,5 +320,8 @@ int main() {
     run<uint32_t>("modmul_barrett_u32", k_modmul_barrett, ops, peak);
     run<int32_t>("modmul_smont_i32", k_modmul_smont, ops, peak);
     run<double>("modmul_f64_centred", k_modmul_f64, ops, peak);
+    run<double>("modmul_fmod_q37", k_modmul_fmod<(1ull << 37) - (1ull << 17) + 1>, ops, peak);
+    run<double>("modmul_fmod_q50", k_modmul_fmod<(1ull << 50) - (1ull << 14) + 1>, ops, peak);
+    run<uint64_t>("modmul_sf_q54", k_modmul_sf54, ops, peak);
     return 0;
 }
