@@ -245,7 +245,7 @@ tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, siz
  * TFHE_GENERIC, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no launch reads the
  * environment.  Every setting computes the same outputs (each is a parity-tested cross-check). ---- */
 typedef struct tfhe_knobs {
-    int32_t ks_tiled_min; /* smallest batch on the batch-tiled key switch; -1: by key width; 0: never */
+    int32_t ks_tiled_min; /* smallest batch on the batch-tiled key switch; -1: the default (1); 0: never */
     int32_t ks_cts;       /* ciphertexts per thread in the tiled key switch: 0 (by key width / batch), 1, 2 */
     int32_t ks_split;     /* most block groups the key-switch steps split over at small batches (1: none) */
     int32_t ks_pk;        /* 0: 32-bit column sums for u16 keys instead of packed u16 pairs */

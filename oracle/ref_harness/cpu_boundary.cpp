@@ -13,6 +13,7 @@
 //                    output NativeVector(n, fmod) (bootstrapping.cu:1898,1926);
 //   CiphertextMulMatrix_CUDA: exact sum mod `modulus` of the reference formula
 //                    (lwe-operation.cu:50-137, FP64 there: equal while sums < 2^53).
+#include <cmath>
 #include "binfhecontext.h"
 #include "bootstrapping.cuh"
 #include "lwe-operation.cuh"
@@ -73,28 +74,44 @@ void GPUFFTBootstrap::MKMSwitch_CUDA(const std::shared_ptr<LWECryptoParams> para
     }
 }
 
+// CiphertextMulMatrix_CUDA with the reference's own semantics (lwe-operation.cu:50-137) on the CPU:
+// A[K][n+1] and B[K][cols] converted to double (ConvertToDouble / static_cast<double>), C = A B^T as an
+// FP64 product, fmod(C, modulus) (applyFmod, :42-48), each entry static_cast<uint64_t> into a
+// NativeVector(n, modulus) and a NativeInteger without further reduction (:115-122).  The only freedom
+// taken: cuBLAS's DGEMM summation order is unspecified, so the sum runs k = 0 .. K-1 in order (this
+// file is compiled without FMA contraction); every sum below 2^53 is exact in any order.  Where the
+// reference's outputs leave [0, modulus) (negative sums: fmod keeps the sign and the cast wraps) or
+// round (|sums| >= 2^53), the HIP engine's exact integer product differs by design.
 std::shared_ptr<std::vector<LWECiphertext>> GPULWEOperation::CiphertextMulMatrix_CUDA(
     const std::shared_ptr<BinFHECryptoParams> params, const std::vector<LWECiphertext>& ct,
     const std::vector<std::vector<int64_t>>& matrix, uint64_t modulus) {
-    const uint32_t n = params->GetLWEParams()->Getn();
-    const size_t K = ct.size(), cols = matrix.empty() ? 0 : matrix[0].size();
+    if (ct.empty()) OPENFHE_THROW(openfhe_error, "Input ciphertexts are empty.");
+    if (matrix.empty()) OPENFHE_THROW(openfhe_error, "Input matrix is empty.");
+    if (ct.size() != matrix.size())
+        OPENFHE_THROW(openfhe_error, "The number of rows of the matrix must be equal to the number of input ciphertexts.");
+    const uint32_t n = params->GetLWEParams()->Getn(), M = n + 1;
+    const size_t K = ct.size(), cols = matrix[0].size();
+    std::vector<double> hA(M * K), hB(K * cols);
+    for (size_t i = 0; i < K; ++i) {
+        const NativeVector& a = ct[i]->GetA();
+        for (uint32_t j = 0; j < n; ++j) hA[M * i + j] = a[j].ConvertToDouble();
+        hA[M * i + n] = ct[i]->GetB().ConvertToDouble();
+    }
+    for (size_t i = 0; i < K; ++i)
+        for (size_t j = 0; j < cols; ++j) hB[cols * i + j] = static_cast<double>(matrix[i][j]);
+    const double dm = static_cast<double>(modulus);
     auto res = std::make_shared<std::vector<LWECiphertext>>(cols);
-    const unsigned __int128 m = modulus;
+#pragma omp parallel for schedule(static)
     for (size_t c = 0; c < cols; ++c) {
-        NativeVector av(n, modulus);
-        __int128 b = 0;
-        std::vector<__int128> acc(n, 0);
+        std::vector<double> C(M, 0.0);
         for (size_t k = 0; k < K; ++k) {
-            const __int128 w = matrix[k][c];
-            for (uint32_t l = 0; l < n; ++l) acc[l] += w * (__int128)ct[k]->GetA()[l].ConvertToInt();
-            b += w * (__int128)ct[k]->GetB().ConvertToInt();
+            const double w = hB[cols * k + c];
+            for (uint32_t j = 0; j < M; ++j) C[j] += hA[M * k + j] * w;
         }
-        for (uint32_t l = 0; l < n; ++l) {
-            __int128 r = acc[l] % (__int128)m;
-            av[l] = (uint64_t)(r < 0 ? r + (__int128)m : r);
-        }
-        __int128 rb = b % (__int128)m;
-        (*res)[c] = std::make_shared<LWECiphertextImpl>(std::move(av), NativeInteger((uint64_t)(rb < 0 ? rb + (__int128)m : rb)));
+        NativeVector av(n, modulus);
+        for (uint32_t j = 0; j < n; ++j) av[j] = static_cast<uint64_t>(std::fmod(C[j], dm));
+        NativeInteger b(static_cast<uint64_t>(std::fmod(C[n], dm)));
+        (*res)[c] = std::make_shared<LWECiphertextImpl>(LWECiphertextImpl(std::move(av), b));
     }
     return res;
 }

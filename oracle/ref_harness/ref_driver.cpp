@@ -15,7 +15,9 @@
 //   keys=synth:<seed>  SURVEY.md Appendix B: splitmix64 coefficients, SetFormat(EVALUATION),
 //                      BTKeyLoad (binfhecontext.h:208-210)
 //   keys=valid:<seed>  the C oracle's deterministic valid keys (or_keygen), same load path
-//   op=params | lut_cube | kat | bskeval | acc | mkm | <gate> | func | funcvec | floor | sign | decomp
+//   op=params | lut_cube | kat | bskeval | acc | mkm | <gate> | func | funcvec | floor | sign | decomp |
+//      mulmatrix (CiphertextMulMatrix, binfhecontext.cpp:319-321: in = ciphertexts mod `mod`, matrix =
+//      int64 [K][cols] file, cols=<cols>, modulus=<m>)
 //   api=vector (default; through the 7 boundary symbols) | single (CPU single-ciphertext API)
 //   in=<u64 file> in2=<u64 file> lut=<u64 file> acc=<u64 file> mod=<ct modulus> fmod=<m>
 //   roundbits=<r> out=<u64 file> gpus=<numGPUs for GPUSetup> reps=<timed repetitions>
@@ -436,6 +438,22 @@ int main(int argc, char** argv) {
             continue;
         }
 
+        if (op == "mulmatrix") {  // vector API only (no single-ciphertext counterpart)
+            auto ct = read_cts(arg("in"), s.n, arg_u64("mod", s.q.ConvertToInt()));
+            auto mw = read_u64(arg("matrix"));
+            const size_t cols = arg_u64("cols");
+            if (cols == 0 || mw.size() != ct.size() * cols) die("matrix file must hold [K][cols] int64");
+            std::vector<std::vector<int64_t>> m(ct.size(), std::vector<int64_t>(cols));
+            for (size_t k = 0; k < ct.size(); ++k)
+                for (size_t c = 0; c < cols; ++c) m[k][c] = (int64_t)mw[k * cols + c];
+            ts = now_s();
+            auto res = s.cc.CiphertextMulMatrix(ct, m, arg_u64("modulus"));
+            double dt = now_s() - ts;
+            best = std::min(best, dt);
+            total += dt;
+            for (auto& c : res) append_ct(out, c);
+            continue;
+        }
         const uint64_t mod = arg_u64("mod", s.q.ConvertToInt());
         auto ct = read_cts(arg("in"), s.n, mod);
         std::vector<LWECiphertext> res;

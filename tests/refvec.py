@@ -37,7 +37,12 @@ def gen(spec, fixtures):
         return np.asarray(fixtures[spec["golden"]], dtype=np.uint64)
     shape = spec["shape"]
     count = int(np.prod(shape))
-    return pyoracle.splitmix(pyoracle.Rng(spec["seed"]), count, spec["mod"]).reshape(shape)
+    v = pyoracle.splitmix(pyoracle.Rng(spec["seed"]), count, spec["mod"]).reshape(shape)
+    if "offset" in spec:  # signed entries (CiphertextMulMatrix's int64 matrix): value - offset
+        v = v.astype(np.int64) - np.int64(spec["offset"])
+    if "scale" in spec:   # large entries: value * scale (int64)
+        v = v.astype(np.int64) * np.int64(spec["scale"])
+    return v
 
 
 def inputs(c, fixtures):
@@ -48,7 +53,8 @@ def write_inputs(c, fixtures, tmpdir):
     files = {}
     for k, arr in inputs(c, fixtures).items():
         path = os.path.join(tmpdir, f"{k}.bin")
-        np.ascontiguousarray(arr, dtype=np.uint64).tofile(path)
+        arr = np.ascontiguousarray(arr)
+        (arr.view(np.uint64) if arr.dtype == np.int64 else arr.astype(np.uint64)).tofile(path)
         files[k] = path
     return files
 
@@ -159,3 +165,29 @@ def check(c, out, extra):
     for k in ("moduli", "digits"):
         if k in want:
             assert extra[k] == want[k], (c["name"], k, extra[k], want[k])
+
+
+def mulmatrix_reference(ct, mat, modulus):
+    """CiphertextMulMatrix as the reference computes it (lwe-operation.cu:79-125): ciphertext words and
+    matrix entries as doubles, out[c] = sum_k mat[k][c] ct[k] in FP64 (k = 0 .. K-1 in order: cuBLAS's
+    order is unspecified, every sum below 2^53 is exact in any order), fmod(., modulus), then
+    static_cast<uint64_t> -- a negative fmod result wraps as x86-64 converts it (cvttsd2si): 2^64 - |r|.
+    Returns [cols][n+1] u64."""
+    A = np.asarray(ct, dtype=np.uint64).astype(np.float64)          # [K][n+1]
+    W = np.asarray(mat, dtype=np.int64).astype(np.float64)          # [K][cols]
+    C = np.zeros((W.shape[1], A.shape[1]), dtype=np.float64)
+    for k in range(A.shape[0]):
+        C += W[k][:, None] * A[k][None, :]
+    return np.fmod(C, float(modulus)).astype(np.int64).view(np.uint64)
+
+
+def mulmatrix_exact(ct, mat, modulus):
+    """The exact product sum_k mat[k][c] ct[k] mod modulus in [0, modulus) (the HIP kernel's definition)."""
+    A = [[int(x) for x in row] for row in np.asarray(ct, dtype=np.uint64)]
+    W = np.asarray(mat, dtype=np.int64)
+    out = np.empty((W.shape[1], len(A[0])), dtype=np.uint64)
+    for c in range(W.shape[1]):
+        col = [int(w) for w in W[:, c]]
+        for j in range(len(A[0])):
+            out[c, j] = sum(col[k] * A[k][j] for k in range(len(A))) % modulus
+    return out

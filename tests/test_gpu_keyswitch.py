@@ -19,6 +19,11 @@ SETS = {
     "STD192": lambda m: m.params_from_set("STD192"),
     "STD128Q": lambda m: m.params_from_set("STD128Q"),
     "ARB12": lambda m: m.params_from_logq("STD128", True, 12, 0, 0, 1),
+    # round 4: the remaining tiled builds some parameter set reaches -- u16 keys with baseKS 32 (staging
+    # depth 2), u32 keys with baseKS 64 (depth 8), u32 keys with u64 sums (qKS not a power of two)
+    "STD128Q_OPT": lambda m: m.params_from_set("STD128Q_OPT"),
+    "STD192Q": lambda m: m.params_from_set("STD192Q"),
+    "SIGNED_MOD_TEST": lambda m: m.params_from_set("SIGNED_MOD_TEST"),
 }
 
 
@@ -98,3 +103,16 @@ def test_tiled_keyswitch_ciphertexts_per_thread(ks_ctx, cts):
         tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
     gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
     assert np.array_equal(tiled, gather)
+
+
+def test_u16_keys_without_packed_sums(ks_ctx):
+    """u16 keys with 32-bit column sums (the ks_pk knob 0) equal the packed-u16-sum form and the gather."""
+    name, op, ctx, orc = ks_ctx
+    if ctx.info().ksk_device_bytes == 0 or op.qKS > (1 << 16):
+        pytest.skip("u16 keys only")
+    ext = _ext(op, 700, 21)
+    packed = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+    with ctx.knobs_set(ks_pk=0):
+        plain = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+    gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
+    assert np.array_equal(packed, plain) and np.array_equal(plain, gather)

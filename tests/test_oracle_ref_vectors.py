@@ -28,7 +28,11 @@ def oracle_for(oracle, c):
     return _ctx_cache[key]
 
 
-@pytest.mark.parametrize("name", [c["name"] for c in DATA["cases"]])
+BOOTSTRAP_CASES = [c["name"] for c in DATA["cases"] if c["op"] != "mulmatrix"]
+MM_CASES = [c["name"] for c in DATA["cases"] if c["op"] == "mulmatrix"]
+
+
+@pytest.mark.parametrize("name", BOOTSTRAP_CASES)
 def test_oracle_matches_reference_vector_api(oracle, name):
     c = refvec.case(name, DATA)
     o = oracle_for(oracle, c)
@@ -39,7 +43,8 @@ def test_oracle_matches_reference_vector_api(oracle, name):
 def test_vector_equals_single_in_reference():
     """The generator ran every case through the reference's single-ciphertext API too."""
     for c in DATA["cases"]:
-        assert c["single_fnv"] == c["vector"]["fnv"], c["name"]
+        if c["op"] != "mulmatrix":  # (CiphertextMulMatrix has no single-ciphertext form)
+            assert c["single_fnv"] == c["vector"]["fnv"], c["name"]
 
 
 def test_cube_lut_is_the_reference_lut():
@@ -61,3 +66,17 @@ def test_openfhe_eval_format_matches_reference(oracle, name):
     ev = oracle.openfhe_ntt(p.Q, p.N, bsk)
     assert f"{oracle.fnv1a64(ev[:2 * p.N]):016x}" == fx["head_fnv"]
     assert f"{oracle.fnv1a64(ev):016x}" == fx["fnv"]
+
+
+@pytest.mark.parametrize("name", MM_CASES)
+def test_mulmatrix_model_is_the_reference(oracle, name):
+    """refvec.mulmatrix_reference (FP64 sum, fmod, static_cast<uint64_t>) reproduces the reference's own
+    CiphertextMulMatrix outputs (the FP64 DGEMM + fmod of lwe-operation.cu:79-125 on the CPU) bit for bit,
+    including the cases where they leave [0, modulus) (negative sums) or round (sums >= 2^53)."""
+    c = refvec.case(name, DATA)
+    x = refvec.inputs(c, DATA["fixtures"])
+    model = refvec.mulmatrix_reference(x["in"], x["matrix"], c["args"]["modulus"])
+    refvec.check(c, model.ravel(), {})
+    if name == "mm_gemm":  # GEMM.cpp's config: every sum exact, so model == exact product
+        small = refvec.mulmatrix_exact(x["in"][:, :4], x["matrix"][:, :3], c["args"]["modulus"])
+        assert np.array_equal(small, model[:3, :4])

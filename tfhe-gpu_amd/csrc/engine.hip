@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -181,6 +182,7 @@ struct tfhe_ctx {
     double replicate_ms = 0;
     size_t max_chunk = 65536;  // the reference's max_bootstapping_num, bootstrapping.cuh:140
     Knobs kn{};                // launch choices: environment at setup, tfhe_set_knobs afterwards
+    std::string rccl_lib;      // TFHE_RCCL_LIB at setup ("" = the system librccl)
     ~tfhe_ctx();  // frees every device's arena, scratch, streams (error paths included)
 };
 
@@ -496,14 +498,16 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     return TFHE_OK;
 }
 
-// Smallest batch that takes the tiled key switch (TFHE_KS_TILED_MIN overrides; 0 = never).
-// Below it the per-ciphertext gather (k_mkm, split over several waves) has the better
-// latency: the tiled kernel's workgroups each sweep all N dKS rows, ~1 ms for STD128 at any
-// batch up to 8192, while the u16 gather costs 1.87 ms per 8192 (crossover ~4400); for
-// u32/u64 keys the gather is 2-10x slower already at 1024 (profiles/r02_ks).
+// Smallest batch that takes the tiled key switch (knob ks_tiled_min / TFHE_KS_TILED_MIN; 0 = never).
+// Round 2 set it at 4096 (u16 keys) / 256 (wider keys): the tiled workgroups each swept all N dKS rows
+// (~1 ms for STD128 at any batch up to 8192).
 size_t ks_tiled_min(const tfhe_ctx* c) {
     if (c->kn.ks_tiled_min >= 0) return (size_t)c->kn.ks_tiled_min;  // knob (TFHE_KS_TILED_MIN)
-    return c->ksk_bits == 16 ? 4096 : 256;
+    // round 4 (profiles/r04b/ks_sweep.log): with the steps split up to 16 ways at small batches, the tiled
+    // form beats the gather at every batch from 1 to 1024 and every key width (STD128Q B = 128: 0.33 vs
+    // 6.3 ms; logQ = 23: 1.68 vs 9.3 ms; STD128 B = 1: 0.105 vs 0.64 ms); the gather stays for key
+    // shapes the tiled form does not support
+    return 1;
 }
 
 // the tiled form runs when d.sc.ks holds B ciphertexts (ensure_scratch / ensure_ks_scratch)
@@ -810,6 +814,10 @@ tfhe_status wait_flags(const uint32_t* flags, size_t lo, size_t hi, hipStream_t 
             ++i;
             continue;
         }
+        // a miss: pause (the spinning thread shares its core with the host pool draining other blocks,
+        // ADVICE r3), yield every 64 misses, check the stream every 1024
+        __builtin_ia32_pause();
+        if ((polls & 63) == 63) std::this_thread::yield();
         if ((polls & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(cs);
             if (q == hipSuccess) {
@@ -819,7 +827,6 @@ tfhe_status wait_flags(const uint32_t* flags, size_t lo, size_t hi, hipStream_t 
             }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
                 return fail(TFHE_ERR_DEVICE, "blind rotation: completion flags not set within 120 s");
-            std::this_thread::yield();
         }
     }
     return TFHE_OK;
@@ -1036,6 +1043,7 @@ tfhe_status create_ctx(const tfhe_params* p, int num_gpus, std::unique_ptr<tfhe_
     // with its own arena, streams, scratch and host thread -- the multi-device setup, replication
     // (peer copies: one RCCL communicator cannot hold a device twice), sharding and error paths
     // run on a one-GPU box (tests/test_gpu_multidevice.py).  Read per setup.
+    if (const char* rl = std::getenv("TFHE_RCCL_LIB")) c->rccl_lib = rl;
     const char* lg = std::getenv("TFHE_LOGICAL_DEVICES");
     const int logical = lg ? std::atoi(lg) : 0;
     if (logical > 1) count = logical;
@@ -1136,11 +1144,19 @@ struct RcclApi {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGetErrorString) err = nullptr;
 };
-const RcclApi& rccl() {
-    static const RcclApi api = [] {
+// path: "" = the system RCCL (librccl.so.1); otherwise TFHE_RCCL_LIB, read at setup -- a test build of the
+// same six entry points (tests/stub_rccl: broadcasts by device copies, so the group / sync / destroy
+// sequence below runs on a one-GPU box with logical devices).  Loaded once per path.
+const RcclApi& rccl(const std::string& path) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::string, std::unique_ptr<RcclApi>>> loaded;
+    std::lock_guard<std::mutex> lock(mu);
+    for (auto& e : loaded)
+        if (e.first == path) return *e.second;
+    loaded.emplace_back(path, std::make_unique<RcclApi>([&] {
         RcclApi a;
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        void* h = path.empty() ? dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL) : dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h && path.empty()) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
         if (!h) return a;
         a.init_all = (decltype(a.init_all))dlsym(h, "ncclCommInitAll");
         a.bcast = (decltype(a.bcast))dlsym(h, "ncclBroadcast");
@@ -1150,8 +1166,22 @@ const RcclApi& rccl() {
         a.err = (decltype(a.err))dlsym(h, "ncclGetErrorString");
         a.ok = a.init_all && a.bcast && a.group_start && a.group_end && a.destroy && a.err;
         return a;
-    }();
-    return api;
+    }()));
+    return *loaded.back().second;
+}
+
+// Sum of the checksum partials of `bytes` at p on device d (stream synchronised)
+tfhe_status arena_checksum(Device& d, size_t bytes, uint64_t& out) {
+    DevBuf part;
+    HCHECK(hipSetDevice(d.id));
+    HCHECK(hipMalloc(&part.p, kChecksumBlocks * sizeof(uint64_t)));
+    HCHECK(launch_checksum(d.arena, bytes, part.as<uint64_t>(), d.stream));
+    std::vector<uint64_t> h(kChecksumBlocks);
+    HCHECK(hipMemcpyAsync(h.data(), part.p, h.size() * 8, hipMemcpyDeviceToHost, d.stream));
+    HCHECK(hipStreamSynchronize(d.stream));
+    out = 0;
+    for (uint64_t v : h) out += v;
+    return TFHE_OK;
 }
 
 // Device 0's image -> devices 1..D-1.  GPUSetup(numGPUs) in the reference copies every key from the
@@ -1165,11 +1195,13 @@ tfhe_status replicate_arena(tfhe_ctx* c, size_t bytes) {
     const auto t0 = std::chrono::steady_clock::now();
     const char* env = std::getenv("TFHE_REPLICATE");
     bool want_rccl = !(env && std::strcmp(env, "peer") == 0);
-    for (size_t g = 1; g < D; ++g)  // logical devices sharing one GPU (TFHE_LOGICAL_DEVICES)
-        if (c->devs[g].id == c->devs[0].id) want_rccl = false;
+    // logical devices sharing one GPU (TFHE_LOGICAL_DEVICES): a real communicator cannot hold a device
+    // twice; a TFHE_RCCL_LIB test build can (tests/test_gpu_rccl_stub.py)
+    for (size_t g = 1; g < D; ++g)
+        if (c->devs[g].id == c->devs[0].id && c->rccl_lib.empty()) want_rccl = false;
     bool done = false;
-    if (want_rccl && rccl().ok) {
-        const RcclApi& R = rccl();
+    if (want_rccl && rccl(c->rccl_lib).ok) {
+        const RcclApi& R = rccl(c->rccl_lib);
         std::vector<ncclComm_t> comms(D);
         std::vector<int> ids(D);
         for (size_t g = 0; g < D; ++g) ids[g] = c->devs[g].id;
@@ -1204,6 +1236,15 @@ tfhe_status replicate_arena(tfhe_ctx* c, size_t bytes) {
     }
     c->replicate_method = done ? TFHE_REPLICATE_RCCL : TFHE_REPLICATE_PEER;
     c->replicate_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // every replica must equal device 0's image: a bad broadcast fails setup, not a later call
+    uint64_t want = 0, got = 0;
+    SCHECK(arena_checksum(c->devs[0], bytes, want));
+    for (size_t g = 1; g < D; ++g) {
+        SCHECK(arena_checksum(c->devs[g], bytes, got));
+        if (got != want)
+            return fail(TFHE_ERR_DEVICE, "key arena replica on device " + std::to_string(g) + " differs from device 0's (" +
+                                             (done ? "RCCL broadcast" : "peer copy") + ")");
+    }
     return TFHE_OK;
 }
 
@@ -1693,8 +1734,7 @@ tfhe_status tfhe_eval_func(tfhe_ctx* c, size_t B, const uint64_t* ct, uint64_t q
         if (st == TFHE_OK)
             st = run_lwe_batch(c, B, ct, w, nullptr, 0, out, w,
                                [&](Device& d, const uint64_t* i1, const uint64_t*, uint64_t* o, size_t b, size_t off) {
-                                   size_t g = 0;
-                                   while (c->devs[g].id != d.id) ++g;
+                                   const size_t g = (size_t)(&d - c->devs.data());  // the device's index (logical devices share an id)
                                    return dev_func(c, d, prop, i1, q, d_lut[g] + (per_ct_lut ? off * q : 0), stride, o, b);
                                },
                                WireLim{q, 0, 0, 0});

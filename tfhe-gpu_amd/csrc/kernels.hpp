@@ -18,7 +18,7 @@ struct BRParams {
 // knobs_from_env), changed afterwards only through tfhe_set_knobs (tests, A/B runs).  The C-ABI
 // mirror is tfhe_knobs (include/tfhe_hip.h); the launchers below take them by reference.
 struct Knobs {
-    int32_t ks_tiled_min = -1;  // smallest batch on the tiled key switch; -1: by key width, 0: never
+    int32_t ks_tiled_min = -1;  // smallest batch on the tiled key switch; -1: default (1), 0: never
     int32_t ks_cts = 0;         // ciphertexts per thread of the tiled key switch; 0: by key width / batch
     int32_t ks_split = 16;      // most block groups the key-switch steps split over at small batches; 1: none
     int32_t ks_pk = 1;          // 0: no packed u16 column sums
@@ -176,6 +176,11 @@ enum LweOp : uint32_t {
 // element-wise over B ciphertexts of n+1 words; y may be null for unary ops
 hipError_t launch_lwe_op(uint32_t op, uint32_t n, uint64_t m, uint64_t c, const uint64_t* x, const uint64_t* y,
                          uint64_t* out, size_t B, hipStream_t s);
+
+// Position-mixed checksum of `bytes` (a multiple of 8) of device memory: kChecksumBlocks u64 partials,
+// whose sum (mod 2^64) the host forms.  engine.hip compares every key-arena replica with device 0's.
+constexpr unsigned kChecksumBlocks = 1024;
+hipError_t launch_checksum(const void* p, size_t bytes, uint64_t* partial, hipStream_t s);
 
 // CiphertextMulMatrix: out[c][w] = sum_k matrix[k][c] * ct[k][w] mod modulus.
 // ct and matrix are device copies the launch reduces in place into [0, modulus).

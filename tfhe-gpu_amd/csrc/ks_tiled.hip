@@ -330,8 +330,22 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     // staging slots per thread and stage: G steps, ceil(pieces per step / KT) slots each (k_ks_tiled)
     const size_t lpt = (size_t)G * ((P.baseKS * (CT * sizeof(KW) / 16) + KT - 1) / KT);
     if (lds > 80 * 1024 || lpt > 8) return hipErrorNotSupported;
-    auto k = lpt <= 2 ? k_ks_tiled<KW, ACC, CT, CTS, 2, G, PK> : lpt <= 4 ? k_ks_tiled<KW, ACC, CT, CTS, 4, G, PK>
-                                                                         : k_ks_tiled<KW, ACC, CT, CTS, 8, G, PK>;
+    // staging depth MAXL: only the depths some parameter set reaches are built (round 4; each is in a parity
+    // test, tests/test_gpu_keyswitch.py): u16 keys 2 (baseKS 32: the *_OPT / STD256Q sets) or 4 (baseKS
+    // 128), u32 keys with u32 sums 4 or 8 (baseKS 28 / 32 / 64: STD192, STD128Q / STD192Q), the others 4.
+    // Any other shape takes the gather form.
+    constexpr bool D2 = sizeof(KW) == 2, D8 = sizeof(KW) == 4 && sizeof(ACC) == 4;
+    void (*k)(KSParams, const KW*, const KW*, const uint32_t*, const uint64_t*, size_t, size_t, uint32_t, uint32_t,
+              uint64_t, uint64_t*, uint32_t, uint64_t*) = nullptr;
+    if (lpt <= 2) {
+        if constexpr (D2) k = k_ks_tiled<KW, ACC, CT, CTS, 2, G, PK>;
+        else k = k_ks_tiled<KW, ACC, CT, CTS, 4, G, PK>;  // (a shallower need fits the depth-4 build)
+    } else if (lpt <= 4) {
+        k = k_ks_tiled<KW, ACC, CT, CTS, 4, G, PK>;
+    } else {
+        if constexpr (D8) k = k_ks_tiled<KW, ACC, CT, CTS, 8, G, PK>;
+    }
+    if (!k) return hipErrorNotSupported;
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));

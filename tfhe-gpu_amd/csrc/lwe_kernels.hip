@@ -128,15 +128,12 @@ hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const v
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, grid, block, lds, s, P, (const KW*)kska, (const KW*)kskb, ext, fmod, out, B, split);
     };
-    auto pick = [&](auto tag) {
-        using KW = decltype(tag);
-        if (one) go(k_mkm<KW, 1>, tag);
-        else go(k_mkm<KW>, tag);
-    };
+    // one wavefront per workgroup: only the N = 8192 contexts need it, and their keys are u64 (qKS = 2^35)
+    if (one && ksk_bits != 64) return hipErrorNotSupported;
     switch (ksk_bits) {
-        case 16: pick(uint16_t{}); break;
-        case 32: pick(uint32_t{}); break;
-        default: pick(uint64_t{}); break;
+        case 16: go(k_mkm<uint16_t>, uint16_t{}); break;
+        case 32: go(k_mkm<uint32_t>, uint32_t{}); break;
+        default: one ? go(k_mkm<uint64_t, 1>, uint64_t{}) : go(k_mkm<uint64_t>, uint64_t{}); break;
     }
     return hipGetLastError();
 }
@@ -268,6 +265,32 @@ hipError_t launch_narrow(const uint64_t* src, int wb, void* dst, size_t n, hipSt
     if (wb == 2) hipLaunchKernelGGL(k_narrow<uint16_t>, dim3(g), dim3(256), 0, s, src, (uint16_t*)dst, n);
     else if (wb == 4) hipLaunchKernelGGL(k_narrow<uint32_t>, dim3(g), dim3(256), 0, s, src, (uint32_t*)dst, n);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// Arena checksum (engine.hip replicate_arena: every replica must equal device 0's image).  Each block
+// sums a position-mixed hash of its strided words into partial[blockIdx.x]; the host adds the partials.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(256) k_checksum(const uint64_t* __restrict__ p, size_t words,
+                                                  uint64_t* __restrict__ partial) {
+    __shared__ uint64_t red[256];
+    uint64_t h = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x)
+        h += mix64(p[i] ^ (i * 0x9E3779B97F4A7C15ull));
+    red[threadIdx.x] = h;
+    __syncthreads();
+    for (uint32_t w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+hipError_t launch_checksum(const void* p, size_t bytes, uint64_t* partial, hipStream_t s) {
+    hipLaunchKernelGGL(k_checksum, dim3(kChecksumBlocks), dim3(256), 0, s, (const uint64_t*)p, bytes / 8, partial);
     return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@
 namespace lbcrypto {
 namespace {
 tfhe_ctx* g_ctx = nullptr;  // process-global, like the reference's static device state (bootstrapping.cuh:142-159)
+uint32_t g_n = 0;           // LWE dimension n of the set-up context (EvalAcc_CUDA checks every a row against it)
 
 void check(tfhe_status s, const char* where) {
     if (s != TFHE_OK)
@@ -69,16 +70,31 @@ uint64_t* words(const NativeVector& v, int) { return const_cast<uint64_t*>(words
 // batch) are released by one background thread, after the call has returned: freeing them on the
 // caller's thread took 1.6-1.9 ms per 8192 (profiles/r03o), and from the OpenMP workers the frees
 // of blocks another thread allocated serialise on the allocator.  One heap object, intentionally
-// never destroyed (its thread is detached), so process exit does not race it.
+// never destroyed (its thread is detached).  flush() waits until every queued batch is freed: GPUClean
+// and an atexit handler call it, so no destructor of an OpenFHE object runs after exit() has begun
+// tearing down OpenFHE's static parameter and allocator state.
 class Reaper {
    public:
+    static Reaper& get() {
+        static Reaper* r = [] {
+            auto* x = new Reaper();
+            std::atexit([] { Reaper::get().flush(); });
+            return x;
+        }();
+        return *r;
+    }
     static void drop(std::vector<std::shared_ptr<void>>&& batch) {
-        static Reaper* r = new Reaper();
+        Reaper& r = get();
         {
-            std::lock_guard<std::mutex> lk(r->m_);
-            r->q_.push_back(std::move(batch));
+            std::lock_guard<std::mutex> lk(r.m_);
+            r.q_.push_back(std::move(batch));
+            ++r.queued_;
         }
-        r->cv_.notify_one();
+        r.cv_.notify_one();
+    }
+    void flush() {
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return freed_ == queued_; });
     }
 
    private:
@@ -93,11 +109,17 @@ class Reaper {
                 q_.pop_front();
             }
             b.clear();
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                ++freed_;
+            }
+            done_cv_.notify_all();
         }
     }
     std::mutex m_;
-    std::condition_variable cv_;
+    std::condition_variable cv_, done_cv_;
     std::deque<std::vector<std::shared_ptr<void>>> q_;
+    uint64_t queued_ = 0, freed_ = 0;
 };
 
 template <typename T>
@@ -174,12 +196,15 @@ void GPUFFTBootstrap::GPUSetup(const std::shared_ptr<BinFHECryptoParams> params,
     GPUClean();  // the reference grows its device list on a second GPUSetup (bootstrapping.cu:762); here it re-creates
     // numGPUs <= 0 or more than visible: every visible device, as the reference (bootstrapping.cu:736-739)
     check(tfhe_setup_eval(&g_ctx, &p, bsk.data(), ksk.data(), numGPUs), "tfhe_setup_eval");
+    g_n = p.n;
     tm.lap("tfhe_setup_eval", 0);
 }
 
 void GPUFFTBootstrap::GPUClean() {
+    Reaper::get().flush();  // objects replaced by earlier calls are freed before the caller moves on
     if (g_ctx) tfhe_clean(g_ctx);
     g_ctx = nullptr;
+    g_n = 0;
 }
 
 void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> params,
@@ -224,7 +249,10 @@ void GPUFFTBootstrap::EvalAcc_CUDA(const std::shared_ptr<RingGSWCryptoParams> pa
         }
         sparse = sparse && nz == 0;
     }
-    if (!lens_ok) OPENFHE_THROW(openfhe_error, "EvalAcc_CUDA: the a vectors differ in length");
+    // the engine reads n words per row (the n of GPUSetup): shorter rows would be read past their end
+    if (!lens_ok || n != g_n)
+        OPENFHE_THROW(openfhe_error, "EvalAcc_CUDA: every a vector must have the LWE dimension n of GPUSetup (" +
+                                         std::to_string(g_n) + ")");
     tm.lap(sparse ? "marshal in (test vectors)" : "marshal in", Bn);
     if (sparse) {
         // Results go into the accumulators' own coefficient vectors when this vector holds the only
