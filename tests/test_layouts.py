@@ -34,8 +34,9 @@ def test_fast4_exchange_layouts():
 
 
 def test_special_form_kernel_bounds():
-    """gen3sf (blind_rotate_generic.hip): product inputs < 2^61, no 64-bit overflow in the
-    partial products, non-negative offset subtractions, one-subtraction accumulator update."""
+    """gen3sf / sf2 (blind_rotate_generic.hip): the register-level sf_mul sequence is exact, its
+    quotient fits 32 bits, no value reaches 2^64, offset subtractions stay non-negative, and the
+    accumulator update needs one subtraction -- for c = 77823 and the largest admitted c."""
     out = run_tool("bounds_sf.py")
     assert out.strip().endswith("OK"), out
 

@@ -663,20 +663,21 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
 
 // ---------------------------------------------------------------------------
 // gen3sf: gen3 for Q = 2^54 - c, c < 2^20 (the logQ / arbFunc contexts, Q = 2^54 - 77823: C3,
-// C5b).  Every constant w (twiddle, key, monomial) is held as W0 = w and W1 = w 2^31 mod Q (the
-// same 16 bytes as a word and its Shoup companion), and a product of a lazily reduced
-// a < 2^61 with w is
-//     a w = a0 W0 + a1 W1 (mod Q),  a0 = a mod 2^31, a1 = a >> 31:   S = H 2^32 + P.lo < 2^86
-//     r = (S mod 2^54) + (S >> 54) c  < 2^54 + 2^32 c
+// C5b).  Every constant w (twiddle, key, monomial) is held as W0 = w and W1 = w 2^32 mod Q (the
+// same 16 bytes as a word and its Shoup companion), and a product of any a < 2^64 with w is
+//     a w = a0 W0 + a1 W1 (mod Q),  a0 = a mod 2^32, a1 = a >> 32:   S < 2^87
+//     r = (S mod 2^55) + (S >> 55) 2c  < 2^55 + 2^33 c
 // -- five v_mad_u64_u32 and no quotient estimate, against ten multiplies for the u64 Shoup
-// product.  Values stay unsigned and lazy: the forward transform needs no reduction at all
-// (y' = x + 2Q - v, 11 stages < 23 Q), the inverse folds its pure sums once per pass
-// (x -> (x mod 2^54) + (x >> 54) c, one mad), the accumulator update folds once and subtracts
-// Q at most once.  tools/bounds_sf.py checks every bound of this schedule.
+// product (round 4: nine VALU, device_math.hpp sf_mul).  Values stay unsigned and lazy: the
+// forward transform needs no reduction at all (y' = x + 3Q - v, 11 stages < 35 Q), the inverse
+// folds its pure sums once per pass (x -> (x mod 2^54) + (x >> 54) c, one mad), the accumulator
+// update folds once and subtracts Q at most once.  tools/bounds_sf.py checks every bound of
+// this schedule.
 // (SF_K and sf_mul live in device_math.hpp, shared with the VALU microbenchmark)
 
 struct SfC {
-    uint64_t Q, Q2, Q9;  // Q, 2Q (forward offset), 9Q (inverse offset)
+    uint64_t Q, Q3, Q10;  // Q, 3Q (forward offset), 10Q (inverse and monomial offsets; tools/bounds_sf.py)
+    uint32_t c2;          // 2c: sf_mul folds at 2^55
     uint32_t c;
 };
 __device__ __forceinline__ uint64_t sf_fold(uint64_t x, uint32_t c) {
@@ -706,13 +707,13 @@ __device__ __forceinline__ uint64_t tw1(const SfTwB& T, uint32_t i) {
 // Monomial factors from two 64-entry LDS tables instead of gathers from the 2N-entry table in
 // memory (those missed the cache and stalled every round, profiles/r02z): T[j] = psi^(64 j),
 // T[64 + j] = psi^j as (W0, W1) pairs, built from mono = psi^k - 1 at kernel start, and
-//     A (psi^e - 1) = sf(sf(A, T[e >> 6]), T[64 + (e & 63)]) + (9Q - A)      (A < 9Q)
+//     A (psi^e - 1) = sf(sf(A, T[e >> 6]), T[64 + (e & 63)]) + (10Q - fold(A))
 constexpr uint32_t SF_MT = 256;  // u64 words of the two tables
 __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __restrict__ mono,
                                                const uint64_t* __restrict__ mono1, uint64_t Q) {
     for (uint32_t k = threadIdx.x; k < 128; k += blockDim.x) {
         const uint32_t e = k < 64 ? 64 * k : k - 64;
-        const uint64_t w0 = mono[e] + 1, w1 = mono1[e] + (1ull << 31);  // psi^e, psi^e 2^31
+        const uint64_t w0 = mono[e] + 1, w1 = mono1[e] + (1ull << 32);  // psi^e, psi^e 2^32
         T[2 * k] = w0 >= Q ? w0 - Q : w0;
         T[2 * k + 1] = w1 >= Q ? w1 - Q : w1;
     }
@@ -720,20 +721,21 @@ __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __re
 __device__ __forceinline__ uint64_t sf_mono_mul(uint64_t A, uint32_t e, const uint64_t* T, const SfC& K) {
     const uint64_t* th = T + 2 * (e >> 6);
     const uint64_t* tl = T + 2 * (64 + (e & 63));
-    return sf_mul(sf_mul(A, th[0], th[1], K.c), tl[0], tl[1], K.c) + (K.Q9 - A);
+    // the offset subtracts A folded below 1.01 Q: gen3sf's A sums 2 products per digit (up to 8 digits)
+    return sf_mul(sf_mul(A, th[0], th[1], K.c2), tl[0], tl[1], K.c2) + (K.Q10 - sf_fold(A, K.c));
 }
 
 template <class TW>
 __device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const TW& T, uint32_t i, const SfC& K) {
-    const uint64_t v = sf_mul(y, tw0(T, i), tw1(T, i), K.c);
-    y = x + (K.Q2 - v);
+    const uint64_t v = sf_mul(y, tw0(T, i), tw1(T, i), K.c2);
+    y = x + (K.Q3 - v);
     x = x + v;
 }
 template <bool FOLD = false, class TW>
 __device__ __forceinline__ void sf_gs(uint64_t& x, uint64_t& y, const TW& T, uint32_t i, const SfC& K) {
-    const uint64_t d = x + (K.Q9 - y), s = x + y;
+    const uint64_t d = x + (K.Q10 - y), s = x + y;
     x = FOLD ? sf_fold(s, K.c) : s;
-    y = sf_mul(d, tw0(T, i), tw1(T, i), K.c);
+    y = sf_mul(d, tw0(T, i), tw1(T, i), K.c2);
 }
 
 template <class TW>
@@ -822,7 +824,7 @@ __device__ __forceinline__ void sf_ntt_inv(uint64_t* buf, uint64_t (&v)[8], cons
     g3_ad(0, tau, ad);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
-    sf_inv_core<false>(v, 4, 0, T, K);  // outputs < 8.2 Q: the accumulator update folds
+    sf_inv_core<false>(v, 4, 0, T, K);  // outputs < 18.1 Q: the accumulator update folds
 }
 
 // keys / monomials / inverse twiddles: W0 = the generic arena's words, W1 from sf1 (the same
@@ -868,7 +870,7 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
 
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
-        uint64_t A[2][2][CN];  // A_kj per owned slot (< 2.1 Q per digit)
+        uint64_t A[2][2][CN];  // A_kj per owned slot (< 2.3 Q per digit)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -919,8 +921,8 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
                 const uint64_t(&c)[8] = kv[g & 1];
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    A[kk][j][k] += sf_mul(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], K.c) +
-                                   sf_mul(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], K.c);
+                    A[kk][j][k] += sf_mul(d0, c[(j * 2) * 2], c[(j * 2) * 2 + 1], K.c2) +
+                                   sf_mul(d1, c[(j * 2 + 1) * 2], c[(j * 2 + 1) * 2 + 1], K.c2);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();  // the next pass A rewrites entries other threads' products read
@@ -935,7 +937,7 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
         }
         __syncthreads();
         uint64_t v[8];
-        sf_ntt_inv(buf, v, TI, K);  // outputs < 8.2 Q
+        sf_ntt_inv(buf, v, TI, K);  // outputs < 18.1 Q
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -1027,7 +1029,7 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
 }
 
 // inverse: units of slots 4u .. 4u+3 from registers (second stage's sums folded), C and B
-// wave-local (last stage's sums folded), barrier, pass A into v (polynomial t >> 8, < 8.2 Q)
+// wave-local (last stage's sums folded), barrier, pass A into v (polynomial t >> 8, < 18.1 Q)
 // the units of polynomial q (this lane's own slots of the buffer)
 template <class TW>
 __device__ __forceinline__ void sf2_inv_unit(uint64_t* buf, int q, const uint64_t (&sq)[4], const TW& T,
@@ -1078,10 +1080,24 @@ __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], 
     sf_inv_core<false>(v, 4, 0, T, K);
 }
 
+// SF2_MONO_ROWS: the factors from the row tables (1) or the two-level LDS tables (0); SF_ROW_AUX: cache
+// policy of the row loads (2 = nt)
+#ifndef SF2_MONO_ROWS
+#define SF2_MONO_ROWS 1
+#endif
+#ifndef SF_ROW_AUX
+#define SF_ROW_AUX 0
+#endif
+// Monomial factors (round 4): row m of the [2N][N] tables holds psi^e - 1, e = (2 bitrev(x) + 1) m mod 2N,
+// for every slot x in the transform's output order (W0 in mrow, W1 in mrow1; k_pack_mono_rows), so
+// a round reads two rows -- m = a'_i for the + key, 2N - a'_i for the - key -- as 64 contiguous bytes
+// per lane, like a key row, and A (X^(+-a') - 1) is ONE sf product (round 3: two products by the
+// two-level LDS tables plus an offset subtraction, and the slot exponents computed every round).
 template <int DIG>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                   const uint64_t* __restrict__ mrow, const uint64_t* __restrict__ mrow1,
                    const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
                    const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -1095,8 +1111,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
-    uint64_t* mt = psi1_l + N;  // monomial tables
-    sf_mono_tables(mt, mono, mono1, Q);
+    uint64_t* mt = psi1_l + N;  // monomial tables (SF2_MONO_ROWS = 0)
+    if constexpr (!SF2_MONO_ROWS) sf_mono_tables(mt, mono, mono1, Q);
     const SfTw TF{psi_l, psi1_l};
     const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
@@ -1121,6 +1137,18 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
 
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow1), 0, -1, 0x00020000);
+    // the decomposition's offsets: digit l of x is that of c + Kd_l, c = x or x - Q (centred), i.e. of
+    // x + (x < Q/2 ? Kd_l : Kd_l - Q); the digit r in [-B/2, B/2) enters the transform as r + Q (< 2Q,
+    // congruent, no sign test; tools/bounds_sf.py starts the forward transform at 2Q)
+    int64_t Kdl[DIG];
+#pragma unroll
+    for (int l = 0; l < DIG; ++l) {
+        int64_t Kd = 0;
+        for (uint32_t z = 0; z < l + P.thr; ++z) Kd = (Kd << logG) + Bh;
+        Kdl[l] = Kd;
+    }
     for (uint32_t i = 0; i < P.n; ++i) {
         // a_i mod amod (rgsw-acc-cggi.cpp:153) by a division, not a mask: with the mask, the
         // consumer of this round's scalar load moved past the forward transform and results came
@@ -1130,20 +1158,17 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
-            const uint32_t lt = l + P.thr, shift = lt * logG;
-            int64_t Kd = 0;
-            for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
+            const uint32_t shift = (l + P.thr) * logG;
+            const int64_t Klo = Kdl[l], Khi = Kdl[l] - Qs;
             uint64_t v[8];
 #pragma unroll
             for (int p = 0; p < 2; ++p)
 #pragma unroll
                 for (int k = 0; k < CN; ++k) {
                     const uint64_t x = acc[p][k];
-                    const int64_t c = x < Qhalf ? (int64_t)x : (int64_t)x - Qs;
-                    const int64_t d = (c + Kd) >> shift;
-                    int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
-                    if (r < 0) r += Qs;
-                    v[p * CN + k] = (uint64_t)r;
+                    const int64_t d = ((int64_t)x + (x < Qhalf ? Klo : Khi)) >> shift;
+                    const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    v[p * CN + k] = (uint64_t)(r + Qs);
                 }
             if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
             // one digit: its outputs stay in LDS (frees 16 VGPRs; C3 18.8K -> 20.0K); two digits:
@@ -1151,28 +1176,36 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             if (DIG == 1) sf2_ntt_fwd<true>(buf, v, D[l], TF, K);
             else sf2_ntt_fwd(buf, v, D[l], TF, K);
         }
-        // products: group g = (column j, key kk, row r = 2l + polynomial), 4 slots x (W0, W1) of key
-        // words each, the next group's loaded before this group's arithmetic; A_kj of slots u4 + s
-        // (< 2.1 Q per digit); once both keys of column j are summed, its monomial factors
-        constexpr int RW = 2 * DIG, NG = 4 * RW;
-        // key words through buffer resources: uniform round + row offset, 32-bit lane offset
+        // products: per column j, groups (key kk, row r = 2l + polynomial) of 4 slots x (W0, W1) of key
+        // words, then two monomial groups (rows a'_i and 2N - a'_i of the factor tables); the next
+        // group's words are loaded before this group's arithmetic.  A_kj of slots u4 + s (< 2.3 Q per
+        // digit); the + key's factor product is kept in A[0] until the - key's is added.
+        constexpr int RW = 2 * DIG, GJ = 2 * RW + (SF2_MONO_ROWS ? 2 : 0), NG = 2 * GJ;
+        const uint32_t mplus = __builtin_amdgcn_readfirstlane(ai), mminus = (twoN - mplus) & (twoN - 1);  // uniform
+        // key words and factor rows through buffer resources: uniform row offset, 32-bit lane offset
         auto kload = [&](int g, uint64_t (&kw)[8]) {
-            const uint32_t j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
-            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
-            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
-            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
-            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
-            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
+            const uint32_t j = g / GJ, q = g % GJ, kk = q / RW, r = q % RW;
+            const bool mono_g = q >= 2 * RW;
+            const uint32_t o = mono_g ? (q == 2 * RW ? mplus : mminus) * N * 8
+                                      : round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const __amdgpu_buffer_rsrc_t r0 = mono_g ? rm0 : rk0, r1 = mono_g ? rm1 : rk1;
+            v4u a0, a1, b0, b1;
+#define SF2_LOAD4(AUX)                                                                                              \
+    a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8), (int)o, AUX));          \
+    a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8 + 16), (int)o, AUX));     \
+    b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8), (int)o, AUX));          \
+    b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8 + 16), (int)o, AUX));
+            if (mono_g) {
+                SF2_LOAD4(SF_ROW_AUX)
+            } else {
+                SF2_LOAD4(0)
+            }
+#undef SF2_LOAD4
             kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
             kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
             kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
             kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
         };
-        uint32_t ip[4];  // slot x evaluates at psi^(2 bitrev(x) + 1) (recomputed each round, the
-        uint32_t uo = u4;  // opaque copy keeps the compiler from hoisting four live values)
-        asm volatile("" : "+v"(uo));
-#pragma unroll
-        for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
         uint64_t S[2][4], A[2][4];
         uint64_t kw[2][8];
         kload(0, kw[0]);
@@ -1180,20 +1213,32 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         for (int g = 0; g < NG; ++g) {
             if (g + 1 < NG) kload(g + 1, kw[(g + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            const int j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
+            const int j = g / GJ, q = g % GJ, kk = q / RW, r = q % RW;
             const uint64_t(&c)[8] = kw[g & 1];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const uint64_t dv = (DIG > 1 || r < RW - 2) ? D[r >> 1][r & 1][s] : buf[(r & 1) * N + (g3_swz(u4) ^ s)];
-                const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c);
-                A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
-            }
-            if (kk == 1 && r == RW - 1) {
+            if (q < 2 * RW) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const uint32_t in = (twoN - ip[s]) & (twoN - 1);
-                    S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip[s], mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
+                    const uint64_t dv = (DIG > 1 || r < RW - 2) ? D[r >> 1][r & 1][s] : buf[(r & 1) * N + (g3_swz(u4) ^ s)];
+                    const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
+                    A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
                 }
+                if (!SF2_MONO_ROWS && kk == 1 && r == RW - 1) {  // two-level LDS factor tables
+                    uint32_t uo = u4;
+                    asm volatile("" : "+v"(uo));
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+                        const uint32_t in = (twoN - ip) & (twoN - 1);
+                        S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip, mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
+                    }
+                    if constexpr (DIG > 1) sf2_inv_unit(buf, j, S[j], TI, K);
+                }
+            } else if (q == 2 * RW) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) A[0][s] = sf_mul(A[0][s], c[s], c[4 + s], K.c2);  // A_0j (X^a' - 1)
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) S[j][s] = sf_fold(A[0][s] + sf_mul(A[1][s], c[s], c[4 + s], K.c2), K.c);
                 // two digits: the buffer is dead after the last forward units (its outputs are in
                 // registers), so column j's inverse units run now and S[j] dies here (fewer live
                 // registers through column 1's products).  One digit: the buffer still holds that
@@ -1203,7 +1248,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             __builtin_amdgcn_sched_barrier(0);
         }
         uint64_t v[8];
-        sf2_ntt_inv<DIG == 1>(buf, S, v, TI, K);  // outputs < 8.2 Q
+        sf2_ntt_inv<DIG == 1>(buf, S, v, TI, K);  // outputs < 18.1 Q
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -1225,14 +1270,27 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     }
 }
 
-// W1 = w 2^31 mod Q for w < Q: w 2^31 = (w >> 23) 2^54 + (w mod 2^23) 2^31
+// W1 = w 2^32 mod Q for w < Q: w 2^32 = (w >> 22) 2^54 + (w mod 2^22) 2^32  (< 2^54 + 2^32 c < 2Q)
 __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ in, size_t words,
                           uint64_t* __restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= words) return;
     const uint64_t w = in[i] % Q;
-    const uint64_t x = ((w & ((1ull << (SF_K - 31)) - 1)) << 31) + (w >> (SF_K - 31)) * c;
+    const uint64_t x = ((w & ((1ull << (SF_K - 32)) - 1)) << 32) + (w >> (SF_K - 32)) * c;
     out[i] = x >= Q ? x - Q : x;
+}
+
+// the [2N][N] monomial factor rows of k_blind_rotate_sf2: row m, slot x = psi^e - 1 for
+// e = (2 bitrev(x) + 1) m mod 2N, taken from the arena's table mono[e] = psi^e - 1 (W0) and its packed
+// companion mono1[e] (W1 = W0 2^32 mod Q, k_pack_sf)
+__global__ void k_pack_mono_rows(uint64_t Q, const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                                 uint32_t N, uint32_t logN, uint64_t* __restrict__ row0, uint64_t* __restrict__ row1) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)2 * N * N) return;
+    const uint32_t m = (uint32_t)(i / N), x = (uint32_t)(i % N);
+    const uint32_t e = (uint32_t)(((2ull * (__builtin_bitreverse32(x) >> (32 - logN)) + 1) * m) & (2 * N - 1));
+    row0[i] = mono[e] % Q;
+    row1[i] = mono1[e];
 }
 
 }  // namespace
@@ -1312,8 +1370,10 @@ bool sf_path_supported(const BRParams& P, int word_bits) {
            P.logG < 64 && P.n > 0;
 }
 
-// W1 arrays behind the arena's W0 ones: psi [N], ipsi [N], mono [2N], bsk [n][2][dG2][2][N]
-size_t sf_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
+// W1 arrays behind the arena's W0 ones: psi [N], ipsi [N], mono [2N], bsk [n][2][dG2][2][N]; then sf2's
+// monomial factor rows W0 [2N][N] and W1 [2N][N] (128 MiB at N = 2048)
+static size_t sf_w1_words(const BRParams& P) { return (size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N; }
+size_t sf_bytes(const BRParams& P) { return (sf_w1_words(P) + (size_t)4 * P.N * P.N) * 8; }
 
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s) {
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
@@ -1325,6 +1385,12 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
     for (const Part& q : parts)
         hipLaunchKernelGGL(k_pack_sf, dim3((unsigned)((q.n + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, c,
                            (const uint64_t*)q.src, q.n, o + q.off);
+    uint64_t* rows = o + sf_w1_words(P);
+    const size_t row_words = (size_t)2 * P.N * P.N;
+    uint32_t logN = 0;
+    while ((1u << logN) < P.N) ++logN;
+    hipLaunchKernelGGL(k_pack_mono_rows, dim3((unsigned)((row_words + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q,
+                       (const uint64_t*)T.mono, (const uint64_t*)(o + 2 * P.N), P.N, logN, rows, rows + row_words);
     return hipGetLastError();
 }
 
@@ -1334,8 +1400,9 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     if (B == 0) return hipSuccess;
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
     SfC K;
-    K.Q = P.Q, K.Q2 = 2 * P.Q, K.Q9 = 9 * P.Q;
+    K.Q = P.Q, K.Q3 = 3 * P.Q, K.Q10 = 10 * P.Q;
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
+    K.c2 = 2 * K.c;
     const uint64_t* w1 = (const uint64_t*)sf;
     const size_t lds = ((size_t)4 * G3_N + SF_MT) * 8 + rot_exponent_bytes(P.n);  // two polynomials, forward twiddles, monomial tables, a'_i
     const bool no_sf2 = !kn.sf2;  // gen3sf (cross-check)
@@ -1344,9 +1411,10 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     if (!no_sf2 && fits32 && (P.digits == 1 || P.digits == 2)) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            const uint64_t* rows = w1 + sf_w1_words(P);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
-                               (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
-                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
+                               (const uint64_t*)T.ipsi, w1 + P.N, rows, rows + (size_t)2 * P.N * P.N,
+                               (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
         if (P.digits == 2) go(k_blind_rotate_sf2<2>);
         else go(k_blind_rotate_sf2<1>);

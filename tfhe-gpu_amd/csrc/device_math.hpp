@@ -69,18 +69,34 @@ __device__ __forceinline__ double fmodmul_f64(double a, double b, double Q, doub
 
 // Special-form product for Q = 2^54 - c, c < 2^20 (the sf kernels of blind_rotate_generic.hip;
 // also timed alone by tools/microbench/valu_rates.hip).  The constant w is held as (W0, W1) =
-// (w, w 2^31 mod Q); for a lazily reduced a < 2^61, a0 = a mod 2^31, a1 = a >> 31:
-//     S = a0 W0 + a1 W1 < 2^86,   r = (S mod 2^54) + (S >> 54) c  <  2^54 + 2^32 c,   r = a w mod Q
+// (w, w 2^32 mod Q), both < Q; for ANY a < 2^64, a0 = a mod 2^32, a1 = a >> 32 (register halves):
+//     S = a0 W0 + a1 W1 < 2^87
+//     P = a0 W0lo + a1 W1lo < 2^65       (one carry out of 64 bits)
+//     H = a0 W0hi + a1 W1hi + P.hi + carry 2^32 = S >> 32 < 2^55
+//     r = (S mod 2^55) + (S >> 55) c2 < 2^55 + 2^32 c2,   c2 = 2c (2^55 = 2c mod Q),   r = a w mod Q
+// Nine VALU: five v_mad_u64_u32, the mov that zero-extends P.hi into an aligned pair, one
+// v_addc_co_u32 (the carry, kept in the SGPR lane mask v_mad_u64_u32 writes), alignbit, and.
+// Round 3's form (31/31 split of a < 2^61, W1 = w 2^31, fold at 2^54) took eleven: the split
+// cost an and + alignbit and the P.hi addend an extra 64-bit add.  The carry mad and the
+// H mads are written out so the addends stay fused; the addc reads the carry at least three
+// VALU after the mad that wrote it (it depends on both H mads), which covers gfx950's
+// SGPR-write -> carry-read hazard (two wait states) without an s_nop.
+// tools/bounds_sf.py checks S, H and every lazily reduced input of the sf kernels.
 constexpr uint32_t SF_K = 54;
-__device__ __forceinline__ uint64_t sf_mul(uint64_t a, uint64_t w0, uint64_t w1, uint32_t c) {
-    const uint32_t a0 = (uint32_t)a & 0x7fffffffu, a1 = (uint32_t)(a >> 31);  // a1 < 2^30
-    uint64_t P = (uint64_t)a0 * (uint32_t)w0;
-    P += (uint64_t)a1 * (uint32_t)w1;                                        // < 2^64
-    uint64_t H = (uint64_t)a0 * (uint32_t)(w0 >> 32) + (P >> 32);
-    H += (uint64_t)a1 * (uint32_t)(w1 >> 32);                                // < 2^54
-    const uint32_t hs = (uint32_t)(H >> (SF_K - 32));
-    const uint64_t L = ((H & ((1ull << (SF_K - 32)) - 1)) << 32) | (uint32_t)P;
-    return L + (uint64_t)hs * c;
+__device__ __forceinline__ uint64_t sf_mul(uint64_t a, uint64_t w0, uint64_t w1, uint32_t c2) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint64_t P1 = (uint64_t)a0 * (uint32_t)w0;
+    uint64_t P, H, cy, junk0, junk1, junk2;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(P), "=s"(cy) : "v"(a1), "v"((uint32_t)w1), "v"(P1));
+    const uint64_t X = P >> 32;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(H), "=s"(junk0) : "v"(a0), "v"((uint32_t)(w0 >> 32)), "v"(X));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(H), "=s"(junk1) : "v"(a1), "v"((uint32_t)(w1 >> 32)));
+    uint32_t hh;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(hh), "=s"(junk2) : "v"((uint32_t)(H >> 32)), "s"(cy));
+    const uint32_t hl = (uint32_t)H;
+    const uint32_t hs = __builtin_amdgcn_alignbit(hh, hl, 23);  // S >> 55 < 2^32
+    const uint64_t L = ((uint64_t)(hl & 0x7fffffu) << 32) | (uint32_t)P;  // S mod 2^55
+    return L + (uint64_t)hs * c2;
 }
 
 // lwe-pke.cpp:41-46 RoundqQ: floor(0.5 + (double)v * (double)q / (double)Q) % q,

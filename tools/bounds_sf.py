@@ -1,16 +1,18 @@
-"""Worst-case magnitude model of the special-form u64 blind rotation (gen3sf in
-blind_rotate_generic.hip) for Q = 2^k - c (k = 54, c = 77823: the logQ / arbFunc contexts).
+"""Worst-case magnitude model of the special-form u64 blind rotations (gen3sf, sf2 in
+blind_rotate_generic.hip) for Q = 2^k - c (k = 54; c = 77823, the logQ / arbFunc contexts, and
+c = 2^20 - 1, the largest c sf_path_supported admits).
 
-Arithmetic: every constant w (twiddle, key, monomial) is stored as W0 = w and W1 = w 2^31 mod Q
-(both < Q); a product of an unsigned 64-bit a < 2^61 with w is
-    a w = a0 W0 + a1 W1  (mod Q),   a0 = a mod 2^31,  a1 = a >> 31 < 2^30
-    S   = a0 W0 + a1 W1 < 2^86      (four v_mad_u64_u32, no overflow: checked below)
-    r   = (S mod 2^k) + (S >> k) c  < 2^k + 2^32 c   (one more v_mad_u64_u32)
+Arithmetic (round 4, device_math.hpp sf_mul): every constant w (twiddle, key, monomial) is stored
+as W0 = w and W1 = w 2^32 mod Q (both < Q); a product of ANY unsigned 64-bit a with w is
+    a w = a0 W0 + a1 W1  (mod Q),   a0 = a mod 2^32,  a1 = a >> 32
+    P   = a0 W0lo + a1 W1lo < 2^65       (the carry out of 64 bits is kept)
+    H   = a0 W0hi + a1 W1hi + (P >> 32) + carry 2^32 = S >> 32   (must stay < 2^55)
+    r   = (S mod 2^55) + (S >> 55) 2c  < 2^55 + 2^32 2c          (2^55 = 2c mod Q)
 All values are unsigned, lazily reduced; a "fold" x -> (x mod 2^k) + (x >> k) c (one mad)
 brings any x < 2^64 below 2^k + 2^(64-k) c.  This script walks the kernel's schedule with
 the worst-case bound of every element and checks
-  * every product input is below 2^61 (so a1 < 2^30) and every value below 2^64,
-  * the partial sums of the product never overflow 64 bits,
+  * every value (product inputs included) is below 2^64,
+  * H < 2^55, so the folded quotient S >> 55 fits the mad's 32-bit multiplier,
   * the offsets kQ of the subtractions keep every difference non-negative,
   * the accumulator update lands in [0, Q) after one fold and one conditional subtraction.
 Usage: python3 tools/bounds_sf.py   (exit 1 on a violation; run by tests/test_layouts.py)
@@ -18,10 +20,6 @@ Usage: python3 tools/bounds_sf.py   (exit 1 on a violation; run by tests/test_la
 import sys
 
 K = 54
-C = 77823
-Q = (1 << K) - C
-IN_MAX = 1 << 61          # product input limit
-R_MAX = (1 << K) + (1 << 32) * C  # product output bound
 ok = True
 
 
@@ -31,41 +29,48 @@ def fail(msg):
     ok = False
 
 
+class Arith:
+    def __init__(self, c):
+        self.C = c
+        self.Q = (1 << K) - c
+
+
+A = Arith(77823)
+
+
 def mulw(a):
-    if a >= IN_MAX:
-        fail(f"product input 2^{a.bit_length()} >= 2^61")
-    a0, a1 = (1 << 31) - 1, (a >> 31)
-    w_lo, w_hi = (1 << 32) - 1, (Q >> 32)
+    """bound of sf_mul(a, W0, W1, 2c) for an input bound a"""
+    if a >= 1 << 64:
+        fail(f"product input 2^{a.bit_length()} >= 2^64")
+    Q = A.Q
+    a0, a1 = min(a, (1 << 32) - 1), a >> 32
+    w_lo, w_hi = (1 << 32) - 1, (Q - 1) >> 32
     P = a0 * w_lo + a1 * w_lo
-    if P >= 1 << 64:
-        fail("P overflows 64 bits")
+    if P >= 1 << 65:
+        fail("P needs more than one carry")
     H = a0 * w_hi + a1 * w_hi + (P >> 32)
-    if H >= 1 << K:
-        fail("H >= 2^k: the folded quotient would not fit 32 bits")
-    return R_MAX
+    if H >= 1 << 55:
+        fail("H >= 2^55: the folded quotient would not fit 32 bits")
+    return (1 << 55) - 1 + (H >> 23) * 2 * A.C
 
 
 def fold(x):
     if x >= 1 << 64:
         fail("value >= 2^64")
-    return (1 << K) + (x >> K) * C
-
-
-OFF_CT = 2 * Q   # forward: y' = x + 2Q - v
-OFF_GS = 9 * Q   # inverse: d = x + 9Q - y
+    return (1 << K) - 1 + (x >> K) * A.C
 
 
 def ct(x, y):
     v = mulw(y)
-    if v > OFF_CT:
-        fail("forward offset below the product bound")
-    return x + v, x + OFF_CT
+    if v > 3 * A.Q:
+        fail("forward offset 3Q below the product bound")
+    return x + v, x + 3 * A.Q          # y' = x + 3Q - v
 
 
 def gs(x, y, fold_sum):
-    if y > OFF_GS:
-        fail(f"inverse offset below the subtrahend bound {y / Q:.2f} Q")
-    d = x + OFF_GS                     # x + 9Q - y
+    if y > 10 * A.Q:
+        fail(f"inverse offset below the subtrahend bound {y / A.Q:.2f} Q")
+    d = x + 10 * A.Q                   # x + 10Q - y
     s = x + y
     return (fold(s) if fold_sum else s), mulw(d)
 
@@ -119,24 +124,28 @@ INV_FOLD_PASS = (False, False, True)   # inverse radix-8 passes C, B: fold the l
 INV_FOLD_LAST = (False, False, False)  # pass A: none (the accumulator update folds)
 
 
-def model(rows):
-    x = Q                       # digits are canonical (r mod Q)
+def model(rows, sf2=True):
+    Q = A.Q
+    x = 2 * Q if sf2 else Q     # sf2: digits r + Q, r in [-B/2, B/2); gen3sf: canonical digits
     for _ in range(3):
         x = max(fwd_r8(x))
     D = max(fwd_r4(x))
-    print(f"  forward outputs < {D / Q:.1f} Q")
-    A = rows * 2 * mulw(D)      # rows digits x 2 polynomials per (key, column)
-    # A0j (X^a' - 1) + A1j (X^-a' - 1) with two LDS table factors per monomial:
-    # sf(sf(A, T_hi), T_lo) + (9Q - A) per term, the sum folded
-    if A > OFF_GS:
-        fail("monomial offset 9Q below the product sum bound")
-    S = fold(2 * (mulw(mulw(A)) + OFF_GS))
-    print(f"  products < {A / Q:.2f} Q, S < {S / Q:.2f} Q")
+    R = mulw(D)
+    Ap = rows * 2 * R           # rows digits x 2 polynomials per (key, column)
+    # A0j (X^a' - 1) + A1j (X^-a' - 1), the sum folded: sf2 multiplies by the factor rows (one product
+    # per term); gen3sf by two LDS table factors per term, sf(sf(A, T_hi), T_lo) + (10Q - fold(A))
+    if sf2:
+        S = fold(2 * mulw(Ap))
+    else:
+        if fold(Ap) > 10 * Q:
+            fail("monomial offset 10Q below the folded product sum")
+        S = fold(2 * (mulw(mulw(Ap)) + 10 * Q))
     x = max(inv_r4(S, INV_FOLD_UNITS))
     x = max(inv_r8(x, INV_FOLD_PASS))
     x = max(inv_r8(x, INV_FOLD_PASS))
     out = max(inv_r8(x, INV_FOLD_LAST))
-    print(f"  inverse outputs < {out / Q:.2f} Q")
+    print(f"  forward outputs < {D / Q:.1f} Q, products < {R / Q:.3f} Q, sums < {Ap / Q:.2f} Q, "
+          f"S < {S / Q:.2f} Q, inverse outputs < {out / Q:.2f} Q")
     acc = (Q - 1) + out
     f = fold(acc)
     if f >= 2 * Q:
@@ -144,11 +153,55 @@ def model(rows):
     return ok
 
 
+def sf_mul_model(a, w0, w1, c2):
+    """the register-level sequence of device_math.hpp sf_mul (32-bit halves, one carry)"""
+    M32, M64 = (1 << 32) - 1, (1 << 64) - 1
+    a0, a1 = a & M32, a >> 32
+    P1 = a0 * (w0 & M32)
+    t = a1 * (w1 & M32) + P1
+    P, cy = t & M64, t >> 64
+    H = a0 * (w0 >> 32) + (P >> 32)
+    H = a1 * (w1 >> 32) + H
+    if H >= 1 << 64:
+        fail("H overflows its register")
+    hh = ((H >> 32) + cy) & M32
+    hl = H & M32
+    hs = ((hh << 32 | hl) >> 23) & M32          # v_alignbit_b32 hh, hl, 23
+    L = ((hl & 0x7FFFFF) << 32) | (P & M32)
+    return (L + hs * c2) & M64
+
+
+def exactness(c, trials=20000):
+    """sf_mul_model(a, w, w 2^32 mod Q) = a w mod Q for corner and random a < 2^64, w < Q"""
+    import random
+    Q = (1 << K) - c
+    rng = random.Random(c)
+    ws = [0, 1, Q - 1, Q - 2, (1 << 32) - 1, 1 << 32, Q >> 1] + [rng.randrange(Q) for _ in range(64)]
+    As = [0, 1, (1 << 64) - 1, (1 << 64) - 2, (1 << 32) - 1, 1 << 32, (1 << 63), Q, 3 * Q]
+    bad = 0
+    for i in range(trials):
+        w = ws[i % len(ws)]
+        a = As[i % len(As)] if i < 4 * len(As) * len(ws) else rng.getrandbits(64)
+        r = sf_mul_model(a, w, (w << 32) % Q, 2 * c)
+        if r % Q != a * w % Q or r >= (1 << 55) + (1 << 32) * 2 * c:
+            bad += 1
+    if bad:
+        fail(f"sf_mul model inexact on {bad} of {trials} products (c = {c})")
+    print(f"c = {c}: sf_mul model exact on {trials} products")
+
+
 def main():
+    global A
     good = True
-    for name, digits in (("C3 (one digit per polynomial)", 1), ("C5b (two digits)", 2)):
-        print(name)
-        good &= model(digits)
+    for c in (77823, (1 << 20) - 1):
+        exactness(c)
+    for c in (77823, (1 << 20) - 1):
+        A = Arith(c)
+        for name, digits, sf2 in (("sf2, C3 (one digit per polynomial)", 1, True), ("sf2, C5b (two digits)", 2, True),
+                                  ("gen3sf, 3 digits (TOY logQ 23)", 3, False),
+                                  ("gen3sf, 8 digits (the most any context has)", 8, False)):
+            print(f"c = {c}, {name}")
+            good &= model(digits, sf2)
     print("OK" if good and ok else "FAILED")
     return 0 if good and ok else 1
 

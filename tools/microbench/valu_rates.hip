@@ -218,7 +218,7 @@ __global__ void k_modmul_f64(double* out, int iters, uint32_t seed) {
 // The products the N = 2048 kernels actually issue, from the kernels' own header (device_math.hpp):
 // fmodmul_f64 (blind_rotate_f64.hip: 6 FP64 instructions) at STD192's Q = 2^37 - 2^17 + 1 and
 // STD128Q's Q = 2^50 - 2^14 + 1 with full-width centred operands, and sf_mul (the sf kernels of
-// blind_rotate_generic.hip: five v_mad_u64_u32 + shifts) at Q = 2^54 - 77823 with lazy operands.
+// blind_rotate_generic.hip: five v_mad_u64_u32 + four more VALU) at Q = 2^54 - 77823 with lazy operands.
 // Each lane runs 8 independent chains x = x * w mod Q, w a per-chain constant (a key / twiddle).
 template <uint64_t QV>
 __global__ void k_modmul_fmod(double* out, int iters, uint32_t seed) {
@@ -249,15 +249,15 @@ __global__ void k_modmul_sf54(uint64_t* out, int iters, uint32_t seed) {
         const uint64_t h = (uint64_t)(seed + t * 8 + k) * 0x9E3779B97F4A7C15ull;
         x[k] = (h >> 3) % Q;
         w0[k] = ((h * 0xBF58476D1CE4E5B9ull) >> 9) % Q;
-        // W1 = w 2^31 mod Q, the form k_pack_sf stores
-        const uint64_t y = ((w0[k] & ((1ull << 23) - 1)) << 31) + (w0[k] >> 23) * c;
+        // W1 = w 2^32 mod Q, the form k_pack_sf stores
+        const uint64_t y = ((w0[k] & ((1ull << 22) - 1)) << 32) + (w0[k] >> 22) * c;
         w1[k] = y >= Q ? y - Q : y;
     }
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = tfhe::sf_mul(x[k], w0[k], w1[k], c);
+            for (int k = 0; k < 8; ++k) x[k] = tfhe::sf_mul(x[k], w0[k], w1[k], 2 * c);
     }
     uint64_t s = 0;
     for (int k = 0; k < 8; ++k) s ^= x[k];
