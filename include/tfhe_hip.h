@@ -53,9 +53,10 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 5  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
+#define TFHE_HIP_ABI_VERSION 6  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
                                    4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows);
-                                   5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs */
+                                   5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs;
+                                   6: tfhe_knobs.duo, tfhe_info.duo_timeouts (two-workgroup sf2 form) */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -105,6 +106,8 @@ typedef struct tfhe_info {
     int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
     int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
     double replicate_ms;       /* wall time of that replication (0 for one device) */
+    uint32_t duo_timeouts;     /* two-workgroup blind rotations whose partner never arrived (reads the
+                                  devices' error words: synchronises them); 0 in every correct run */
 } tfhe_info;
 
 /* tfhe_info.replicate_method */
@@ -257,6 +260,8 @@ typedef struct tfhe_knobs {
     int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
     int32_t trace;        /* host-array runner timeline on stderr */
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
+    int32_t duo;          /* two-digit special-form contexts: batches up to this size (default 128, at most 256) run
+                             each ciphertext on two workgroups (sf2duo); 0: never */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
 tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);

@@ -1270,6 +1270,214 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     }
 }
 
+// ---------------------------------------------------------------------------
+// sf2duo: the two-digit sf2 round split over TWO workgroups per ciphertext, for batches too small
+// to fill the chip (round 4: C5b's 128-ciphertext shard of an 8-GPU node ran one workgroup per CU
+// on half the CUs).  Workgroup x of a pair owns accumulator polynomial x: it decomposes acc_x into
+// its two digits (threads 0-255 digit 0, 256-511 digit 1: the forward transform of sf2 with the
+// digits in place of the polynomials), multiplies them by key rows 2l + x of both keys and both
+// columns, applies the monomial factors to its partial sums of both columns and inverts both
+// (sf2's inverse).  INTT is linear, so acc_x += INTT(S_x) = its own column-x output plus the
+// partner's; each round the workgroup publishes its column-(1-x) output (16 KiB) to the partner:
+// sc1 (write-through) stores, every wave's vmcnt(0), barrier, one sc1 flag store; it polls the
+// partner's flag with sc1 loads, barrier, sc1 loads of the partner's 16 KiB
+// (MI355X_MICROARCH.md hand-off table, first row; tools/microbench/pair_handoff.hip measured
+// 1.1-1.3 us per round with b, b + 8 pairing).  Per workgroup and round: half the forward
+// transforms and half the products of sf2<2>, the same monomial and inverse work.
+// Pairs are blocks b and b + 8 (one XCD under round-robin dispatch; correctness does not depend
+// on it).  Every poll is bounded: a partner that never arrives sets X.err and both leave the
+// round loop (the launcher admits at most 256 pairs, all resident at two workgroups per CU).
+struct SfDuo {
+    uint64_t* xbuf;   // [pairs][2 members][2 round parities][N]
+    uint32_t* flags;  // [pairs][2] one 128-B line each (32 words), zero at launch
+    uint32_t* err;
+};
+constexpr uint32_t kDuoMaxPairs = 256;
+constexpr uint32_t kDuoMaxPolls = 1u << 24;
+__device__ __forceinline__ void duo_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(G3_TH, 4)
+k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
+                      const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                      const uint64_t* __restrict__ mrow, const uint64_t* __restrict__ mrow1,
+                      const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                      const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
+                      const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, SfDuo X,
+                      uint32_t pairs) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = G3_N, TH = G3_TH;
+    const uint32_t b = blockIdx.x, pair = (b >> 4) * 8 + (b & 7), x = (b >> 3) & 1;
+    if (pair >= pairs) return;  // both members of a pair take this branch together
+    __shared__ uint32_t duo_ok;
+    uint64_t* buf = reinterpret_cast<uint64_t*>(smem);  // [2][N], swizzled
+    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
+    const uint32_t half = __builtin_amdgcn_readfirstlane(t >> 8);  // digit (forward), column (inverse)
+    const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    uint64_t* psi_l = buf + 2 * N;
+    uint64_t* psi1_l = psi_l + N;
+    for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
+    uint64_t* mt = psi1_l + N;
+    if constexpr (!SF2_MONO_ROWS) sf_mono_tables(mt, mono, mono1, Q);
+    const SfTw TF{psi_l, psi1_l};
+    const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
+    uint64_t* g = acc_io + (size_t)pair * twoN;
+    const uint64_t* ap = a + (size_t)pair * P.n;
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * G3_N + SF_MT) * 8);  // rotation exponents [n]
+    stage_rot_exponents<G3_TH>(ex, ap, P.n, amod, twoN);
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
+    const uint32_t c0 = t & 255;                            // coefficients c0 + 256 k of acc_x
+
+    uint64_t acc[8];  // acc_x, canonical [0, Q); both halves hold the same values
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t v = g[x * N + c0 + 256 * k];
+        acc[k] = v >= Q ? v % Q : v;
+    }
+    __syncthreads();  // forward twiddles, exponents in LDS
+
+    const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow1), 0, -1, 0x00020000);
+    int64_t Kd = 0;  // digit `half` of acc_x (sf2's closed-form offsets)
+    for (uint32_t z = 0; z < half + P.thr; ++z) Kd = (Kd << logG) + Bh;
+    const int64_t Klo = Kd, Khi = Kd - Qs;
+    const uint32_t shift = (half + P.thr) * logG;
+    uint32_t* myflag = X.flags + (pair * 2 + x) * 32;
+    const uint32_t* peerflag = X.flags + (pair * 2 + (1 - x)) * 32;
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint32_t ai = ex[i];
+        const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint64_t xv = acc[k];
+            const int64_t d = ((int64_t)xv + (xv < Qhalf ? Klo : Khi)) >> shift;
+            const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+            v[k] = (uint64_t)(r + Qs);
+        }
+        uint64_t D[2][4];  // D[l][s]: digit l of acc_x at slots u4 + s
+        if (i > 0) __syncthreads();  // every thread has read the previous round's exchange from the buffer
+        sf2_ntt_fwd(buf, v, D, TF, K);
+        // products: per column j, groups (key kk, digit l: row 2l + x), then the two factor rows
+        constexpr int RW = 2, GJ = 2 * RW + (SF2_MONO_ROWS ? 2 : 0), NG = 2 * GJ;
+        const uint32_t mplus = __builtin_amdgcn_readfirstlane(ai), mminus = (twoN - mplus) & (twoN - 1);
+        auto kload = [&](int gi, uint64_t (&kw)[8]) {
+            const uint32_t j = gi / GJ, q = gi % GJ, kk = q / RW, l = q % RW;
+            const bool mono_g = q >= 2 * RW;
+            const uint32_t o = mono_g ? (q == 2 * RW ? mplus : mminus) * N * 8
+                                      : round_off + ((kk * P.dG2 + 2 * l + x) * 2 + j) * N * 8;
+            const __amdgpu_buffer_rsrc_t r0 = mono_g ? rm0 : rk0, r1 = mono_g ? rm1 : rk1;
+            v4u a0, a1, b0, b1;
+#define SF2_LOAD4(AUX)                                                                                              \
+    a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8), (int)o, AUX));          \
+    a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8 + 16), (int)o, AUX));     \
+    b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8), (int)o, AUX));          \
+    b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8 + 16), (int)o, AUX));
+            if (mono_g) {
+                SF2_LOAD4(SF_ROW_AUX)
+            } else {
+                SF2_LOAD4(0)
+            }
+#undef SF2_LOAD4
+            kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
+            kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
+            kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
+            kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
+        };
+        uint64_t S[2][4], A[2][4];
+        uint64_t kw[2][8];
+        kload(0, kw[0]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gi + 1 < NG) kload(gi + 1, kw[(gi + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j = gi / GJ, q = gi % GJ, kk = q / RW, l = q % RW;
+            const uint64_t(&c)[8] = kw[gi & 1];
+            if (q < 2 * RW) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const uint64_t prod = sf_mul(D[l][s], c[s], c[4 + s], K.c2);
+                    A[kk][s] = l == 0 ? prod : A[kk][s] + prod;
+                }
+                if (!SF2_MONO_ROWS && kk == 1 && l == RW - 1) {
+                    uint32_t uo = u4;
+                    asm volatile("" : "+v"(uo));
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+                        const uint32_t in = (twoN - ip) & (twoN - 1);
+                        S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip, mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
+                    }
+                    sf2_inv_unit(buf, j, S[j], TI, K);
+                }
+            } else if (q == 2 * RW) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) A[0][s] = sf_mul(A[0][s], c[s], c[4 + s], K.c2);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) S[j][s] = sf_fold(A[0][s] + sf_mul(A[1][s], c[s], c[4 + s], K.c2), K.c);
+                sf2_inv_unit(buf, j, S[j], TI, K);  // the buffer is dead after the forward units
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        sf2_ntt_inv<false>(buf, S, v, TI, K);  // v: this workgroup's INTT(S_half) at c0 + 256 k, < 18.1 Q
+        // exchange: column 1 - x goes to the partner, column x stays (through the buffer)
+        uint64_t* mine = X.xbuf + (((size_t)pair * 2 + x) * 2 + (i & 1)) * N;
+        const uint64_t* theirs = X.xbuf + (((size_t)pair * 2 + (1 - x)) * 2 + (i & 1)) * N;
+        if (half != x) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) duo_store(mine + c0 + 256 * k, v[k]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's stores drained; every read of the inverse's pass A done
+        if (half == x) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) buf[c0 + 256 * k] = v[k];
+        }
+        if (t == 0) {
+            __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t polls = 0;
+            while (__hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
+                   ++polls < kDuoMaxPolls)
+                __builtin_amdgcn_s_sleep(1);
+            duo_ok = polls < kDuoMaxPolls;
+            if (polls >= kDuoMaxPolls) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!duo_ok) break;  // uniform: the partner never arrived (the launcher reports X.err)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint64_t s = acc[k] + buf[c0 + 256 * k] + duo_load(theirs + c0 + 256 * k);  // < 37.2 Q
+            const uint64_t y = sf_fold(s, K.c);
+            acc[k] = y >= Q ? y - Q : y;
+        }
+    }
+    __syncthreads();  // every thread has read the last exchange
+    if (half == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) buf[c0 + 256 * k] = acc[k];
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {
+        if (x == 0) {  // acc0 transposed (poly.cpp:762-770)
+            const uint64_t v = buf[k == 0 ? 0 : N - k];
+            g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+        } else {
+            g[N + k] = buf[k];
+        }
+    }
+}
+
 // W1 = w 2^32 mod Q for w < Q: w 2^32 = (w >> 22) 2^54 + (w mod 2^22) 2^32  (< 2^54 + 2^32 c < 2Q)
 __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ in, size_t words,
                           uint64_t* __restrict__ out) {
@@ -1394,9 +1602,12 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
     return hipGetLastError();
 }
 
+size_t sf_duo_bytes() { return (size_t)kDuoMaxPairs * (4 * G3_N * 8 + 2 * 128) + 128; }
+uint32_t sf_duo_err_offset_words() { return (uint32_t)((size_t)kDuoMaxPairs * 4 * G3_N * 2 + kDuoMaxPairs * 2 * 32); }
+
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                  const Knobs& kn) {
+                                  const Knobs& kn, void* duo) {
     if (B == 0) return hipSuccess;
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
     SfC K;
@@ -1416,6 +1627,21 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)T.ipsi, w1 + P.N, rows, rows + (size_t)2 * P.N * P.N,
                                (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
+        if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
+            SfDuo X;
+            X.xbuf = (uint64_t*)duo;
+            X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * G3_N);
+            X.err = X.flags + kDuoMaxPairs * 2 * 32;
+            if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
+            const uint64_t* rows = w1 + sf_w1_words(P);
+            (void)hipFuncSetAttribute((const void*)k_blind_rotate_sf2duo, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            hipLaunchKernelGGL(k_blind_rotate_sf2duo, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), lds, s, P, K,
+                               (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, rows,
+                               rows + (size_t)2 * P.N * P.N, (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk,
+                               w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
+            return hipGetLastError();
+        }
         if (P.digits == 2) go(k_blind_rotate_sf2<2>);
         else go(k_blind_rotate_sf2<1>);
         return hipGetLastError();

@@ -120,7 +120,8 @@ struct Device {
     unsigned char* arena = nullptr;
     void* bsk_fast = nullptr;
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
-    void* keys_sf = nullptr;   // special-form path: W1 = w 2^31 mod Q of the arena's tables and BSK
+    void* keys_sf = nullptr;   // special-form path: W1 = w 2^32 mod Q of the arena's tables and BSK, factor rows
+    void* sf_duo = nullptr;    // two-digit special-form path: exchange buffers of the two-workgroup form
     Scratch sc;
     DevTables tables{};
     hipStream_t stream2 = nullptr;  // copy stream of the host-array runner
@@ -208,6 +209,7 @@ Knobs knobs_from_env() {
     num("TFHE_ACC_FLAGS", k.acc_flags);
     num("TFHE_F64W", k.f64w);
     num("TFHE_SF2", k.sf2);
+    num("TFHE_DUO", k.duo);
     num("TFHE_GENERIC", k.generic);
     if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
     if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;
@@ -361,6 +363,10 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
     if (c->use_sf) {
         HCHECK(hipMalloc(&d.keys_sf, sf_bytes(c->br)));
         HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
+        if (c->br.digits == 2) {
+            HCHECK(hipMalloc(&d.sf_duo, sf_duo_bytes()));
+            HCHECK(hipMemsetAsync(d.sf_duo, 0, sf_duo_bytes(), d.stream));
+        }
         HCHECK(hipStreamSynchronize(d.stream));
     }
     return TFHE_OK;
@@ -375,6 +381,7 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     hipFree(d.keys_sf);
+    hipFree(d.sf_duo);
     if (d.stream2) hipStreamSynchronize(d.stream2);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
@@ -489,7 +496,8 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     } else if (c->use_f64) {
         HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream, c->kn));
     } else if (c->use_sf) {
-        HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream, c->kn));
+        HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream, c->kn,
+                                      d.sf_duo));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
                                            amod, acc, B, d.stream, c->kn));
@@ -1431,6 +1439,15 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
                                       : TFHE_BR_GENERIC;
         out->replicate_method = c->replicate_method;
         out->replicate_ms = c->replicate_ms;
+        out->duo_timeouts = 0;
+        for (Device& d : c->devs) {
+            if (!d.sf_duo) continue;
+            uint32_t e = 0;
+            HCHECK(hipSetDevice(d.id));
+            HCHECK(hipStreamSynchronize(d.stream));
+            HCHECK(hipMemcpy(&e, (const uint32_t*)d.sf_duo + sf_duo_err_offset_words(), 4, hipMemcpyDeviceToHost));
+            out->duo_timeouts += e;
+        }
         return TFHE_OK;
     });
 }
@@ -1452,7 +1469,8 @@ tfhe_status tfhe_set_knobs(tfhe_ctx* c, const tfhe_knobs* in) {
         if (!in) return fail(TFHE_ERR_INVALID_ARGUMENT, "null knobs");
         Knobs k;
         std::memcpy(&k, in, sizeof(Knobs));
-        if (k.generic < 0 || k.generic > 2 || k.ks_cts < 0 || k.ks_cts > 2 || k.ks_split < 1 || k.host_parts < 1)
+        if (k.generic < 0 || k.generic > 2 || k.ks_cts < 0 || k.ks_cts > 2 || k.ks_split < 1 || k.host_parts < 1 ||
+            k.duo < 0 || k.duo > 256)
             return fail(TFHE_ERR_INVALID_ARGUMENT, "knob out of range");
         if (k.probe != 0 && !f64_test_probes_compiled())
             return fail(TFHE_ERR_UNSUPPORTED, "probe builds exist only in the test library (libtfhe_hip_test.so)");

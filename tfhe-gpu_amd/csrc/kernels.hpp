@@ -30,6 +30,7 @@ struct Knobs {
     int32_t generic = 0;        // 0: gen3 / v2 by N; 1: v1 (all digits in LDS); 2: v2 also at N = 2048
     int32_t trace = 0;          // host-array runner timeline on stderr
     int32_t probe = 0;          // test library only (TFHE_TEST_PROBES): f64w fault probe / timing builds
+    int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup sf2 form (two digits, <= 256); 0: never
 };
 
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
@@ -109,9 +110,11 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
 bool sf_path_supported(const BRParams& P, int word_bits);
 size_t sf_bytes(const BRParams& P);
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
+size_t sf_duo_bytes();  // exchange buffers of the two-workgroup sf2 form (k_blind_rotate_sf2duo)
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                  const Knobs& kn);
+                                  const Knobs& kn, void* duo);
+uint32_t sf_duo_err_offset_words();  // the error word's u32 index in the duo buffer
 
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
 //   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.

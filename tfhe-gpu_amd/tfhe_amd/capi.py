@@ -12,8 +12,8 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
-ABI_VERSION = 5  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays;
-                 # 5: device-resident EvalFunc / EvalFloor / EvalSign)
+ABI_VERSION = 6  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays;
+                 # 5: device-resident EvalFunc / EvalFloor / EvalSign; 6: knobs.duo, info.duo_timeouts)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -46,13 +46,14 @@ class Params(C.Structure):
 class Info(C.Structure):
     _fields_ = [("num_devices", C.c_int), ("word_bits", C.c_int), ("bsk_device_bytes", C.c_uint64),
                 ("ksk_device_bytes", C.c_uint64), ("bootstraps", C.c_uint64), ("key_image_bytes", C.c_uint64),
-                ("br_kernel", C.c_int), ("replicate_method", C.c_int), ("replicate_ms", C.c_double)]
+                ("br_kernel", C.c_int), ("replicate_method", C.c_int), ("replicate_ms", C.c_double),
+                ("duo_timeouts", C.c_uint32)]
 
 
 class Knobs(C.Structure):
     """tfhe_knobs: launch choices of a context (include/tfhe_hip.h), environment at setup, then tfhe_set_knobs."""
     _fields_ = [(k, C.c_int32) for k in ("ks_tiled_min", "ks_cts", "ks_split", "ks_pk", "host_parts", "wire",
-                                         "acc_flags", "f64w", "sf2", "generic", "trace", "probe")]
+                                         "acc_flags", "f64w", "sf2", "generic", "trace", "probe", "duo")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
