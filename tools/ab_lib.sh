@@ -13,7 +13,7 @@ for CFG in $CFGS; do
     for L in $LIBS; do
       i=$((i + 1))
       echo "[$(date +%T)] $CFG lib$i round $r ($L)"
-      TFHE_LIB=$L timeout -k 10 300 python3 bench.py --config $CFG --no-cpu-baseline --no-host-array --no-dropin \
+      TFHE_ABI_PREV=1 TFHE_LIB=$L timeout -k 10 300 python3 bench.py --config $CFG --no-cpu-baseline --no-host-array --no-dropin \
         --steps 3 --warmup 1 > $O/ab_${CFG}_${i}_$r.log 2>&1 || { echo "ab rc=$?"; exit 1; }
       tail -1 $O/ab_${CFG}_${i}_$r.log | python3 -c "import json,sys; l=json.loads(sys.stdin.read()); r=l['roofline']; print('   ', l['value'], 'kernel_ms', r['kernel_ms'])"
     done
