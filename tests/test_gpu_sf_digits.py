@@ -1,0 +1,58 @@
+"""GPU: the special-form kernels at every digit count a Q = 2^54 - c context reaches.
+
+sf2 is built for 1, 2 and 3 transformed digits (3: the CHES-experiments.cpp EvalFunc context,
+GenerateBinFHEContext(STD128, true, 12, 0, GINX, false, 1 << 18) -- baseG 2^18, no thrown digit),
+gen3sf takes more (TOY logQ 29: 4, tests/test_gpu_unittest_func.py) and is the cross-check of all
+(knob sf2 = 0).  Per context: EvalAcc on 5 ciphertexts bit-exact against the oracle, and 64
+ciphertexts equal on sf2 and gen3sf.  Keys: Appendix B splitmix64 keys.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CONTEXTS = {  # name: params_from_logq args, transformed digits
+    "C3_arb_logQ12_thr1": (("STD128", True, 12, 0, 0, 1), 1),
+    "C5b_logQ23_thr1": (("STD128", False, 23, 0, 0, 1), 2),
+    "CHES_func_baseG18": (("STD128", True, 12, 0, 1 << 18, 0), 3),
+}
+
+
+@pytest.fixture(scope="module", params=list(CONTEXTS))
+def sfctx(request, oracle):
+    import tfhe_amd
+
+    spec, digits = CONTEXTS[request.param]
+    op, cp = oracle.params_from_logq(*spec), tfhe_amd.params_from_logq(*spec)
+    assert cp.digitsG - cp.numDigitsToThrow == digits and cp.Q == (1 << 54) - 77823
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(91))
+    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    assert ctx.info().br_kernel == 5  # TFHE_BR_SF
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    yield op, ctx, orc
+    ctx.GPUClean()
+    orc.close()
+
+
+def _inputs(op, B, seed):
+    rs = np.random.default_rng(seed)
+    return (rs.integers(0, 2 * op.N, (B, op.n), dtype=np.uint64),
+            rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64))
+
+
+def test_sf2_eval_acc_matches_oracle(sfctx):
+    op, ctx, orc = sfctx
+    a, acc = _inputs(op, 5, 11)
+    out = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(out.reshape(5, -1), orc.eval_acc(a, 2 * op.N, acc).reshape(5, -1))
+
+
+def test_sf2_equals_gen3sf(sfctx):
+    op, ctx, _ = sfctx
+    a, acc = _inputs(op, 64, 12)
+    with ctx.knobs_set(duo=0):
+        one = ctx.EvalAcc(a, 2 * op.N, acc)
+    with ctx.knobs_set(sf2=0):
+        ref = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(one, ref)

@@ -1155,7 +1155,10 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         // out wrong intermittently on the STD128Q sets (profiles/r02ax: bisected to this line)
         const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
-        uint64_t D[DIG][2][4];  // forward outputs (one digit: in LDS instead)
+        // forward outputs in registers; with an odd digit count the last digit's stay in LDS (one
+        // digit: frees 16 VGPRs; three: the register budget of two)
+        constexpr bool LAST_LDS = (DIG & 1) != 0;
+        uint64_t D[DIG][2][4];
 #pragma unroll
         for (int l = 0; l < DIG; ++l) {
             const uint32_t shift = (l + P.thr) * logG;
@@ -1173,7 +1176,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
             // one digit: its outputs stay in LDS (frees 16 VGPRs; C3 18.8K -> 20.0K); two digits:
             // registers (LDS for the second measured 11.4K -> 10.0K on C5b, profiles/r02ah)
-            if (DIG == 1) sf2_ntt_fwd<true>(buf, v, D[l], TF, K);
+            if (LAST_LDS && l == DIG - 1) sf2_ntt_fwd<true>(buf, v, D[l], TF, K);
             else sf2_ntt_fwd(buf, v, D[l], TF, K);
         }
         // products: per column j, groups (key kk, row r = 2l + polynomial) of 4 slots x (W0, W1) of key
@@ -1218,7 +1221,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             if (q < 2 * RW) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const uint64_t dv = (DIG > 1 || r < RW - 2) ? D[r >> 1][r & 1][s] : buf[(r & 1) * N + (g3_swz(u4) ^ s)];
+                    const uint64_t dv = (LAST_LDS && r >= RW - 2) ? buf[(r & 1) * N + (g3_swz(u4) ^ s)] : D[r >> 1][r & 1][s];
                     const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
                     A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
                 }
@@ -1231,7 +1234,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                         const uint32_t in = (twoN - ip) & (twoN - 1);
                         S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip, mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
                     }
-                    if constexpr (DIG > 1) sf2_inv_unit(buf, j, S[j], TI, K);
+                    if constexpr (!LAST_LDS) sf2_inv_unit(buf, j, S[j], TI, K);
                 }
             } else if (q == 2 * RW) {
 #pragma unroll
@@ -1241,14 +1244,14 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                 for (int s = 0; s < 4; ++s) S[j][s] = sf_fold(A[0][s] + sf_mul(A[1][s], c[s], c[4 + s], K.c2), K.c);
                 // two digits: the buffer is dead after the last forward units (its outputs are in
                 // registers), so column j's inverse units run now and S[j] dies here (fewer live
-                // registers through column 1's products).  One digit: the buffer still holds that
-                // digit's outputs for column 1.
-                if constexpr (DIG > 1) sf2_inv_unit(buf, j, S[j], TI, K);
+                // registers through column 1's products).  One or three digits: the buffer still holds
+                // the last digit's outputs for column 1.
+                if constexpr (!LAST_LDS) sf2_inv_unit(buf, j, S[j], TI, K);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
         uint64_t v[8];
-        sf2_ntt_inv<DIG == 1>(buf, S, v, TI, K);  // outputs < 18.1 Q
+        sf2_ntt_inv<LAST_LDS>(buf, S, v, TI, K);  // outputs < 18.1 Q
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -1619,7 +1622,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     const bool no_sf2 = !kn.sf2;  // gen3sf (cross-check)
     // sf2 addresses the keys with 32-bit byte offsets (buffer resources)
     const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
-    if (!no_sf2 && fits32 && (P.digits == 1 || P.digits == 2)) {
+    if (!no_sf2 && fits32 && P.digits >= 1 && P.digits <= 3) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             const uint64_t* rows = w1 + sf_w1_words(P);
@@ -1642,7 +1645,8 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
             return hipGetLastError();
         }
-        if (P.digits == 2) go(k_blind_rotate_sf2<2>);
+        if (P.digits == 3) go(k_blind_rotate_sf2<3>);  // (CHES-experiments.cpp's EvalFunc context, baseG 2^18)
+        else if (P.digits == 2) go(k_blind_rotate_sf2<2>);
         else go(k_blind_rotate_sf2<1>);
         return hipGetLastError();
     }

@@ -198,6 +198,7 @@ def main():
     for c in (77823, (1 << 20) - 1):
         A = Arith(c)
         for name, digits, sf2 in (("sf2, C3 (one digit per polynomial)", 1, True), ("sf2, C5b (two digits)", 2, True),
+                                  ("sf2, CHES EvalFunc context (three digits)", 3, True),
                                   ("gen3sf, 3 digits (TOY logQ 23)", 3, False),
                                   ("gen3sf, 8 digits (the most any context has)", 8, False)):
             print(f"c = {c}, {name}")
