@@ -705,22 +705,14 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 }
 
 // FOLD (thr = 0) only; LD = transformed digits (digits - 1), WRAP as in k_blind_rotate_f64.
-// Monomial factors psi^(+-e) - 1 of the lane's 4 slots (round 4): rows a'_i and 2N - a'_i of the
-// [2N][N] factor table behind the BSK, 32 contiguous bytes per lane each, loaded with the first key
-// group.  Round 3's form took two LDS table products per factor once per round (8 per lane-round,
-// and the slot exponents); its measured alternatives -- per-slot gathers from the 2N-entry table at
-// each use (STD192 474 ms), table products at each use (385 ms), the 8 gathers once per round
-// (357 ms), against 315-323 ms (profiles/r02ae, r03i) -- were all per-slot gathers, not rows.
+// Monomial factors psi^(+-e) - 1 of the lane's 4 slots: two LDS table products once per round
+// (then one product per use).  Round 3 measured the alternatives and removed them (round 4): gathers
+// from the 2N-entry memory table at each use (STD192 474 ms), table products at each use (385 ms),
+// the 8 gathers once per round (357 ms), against 315-323 ms (profiles/r02ae, r03i).
 // PROBE (test library only, TFHE_TEST_PROBES; tests/test_gpu_f64w_race.py): bit 1 delays waves 1..
 // inside the prologue's C' transform (between passes B and C), bit 0 omits the barrier after it --
 // together they reproduce the round-0 race of the round-2 kernel; bit 2 (timing only) drops the
 // barrier before each further digit's pass A
-#ifndef F64W_MONO_ROWS
-#define F64W_MONO_ROWS 1
-#endif
-#ifndef F64_ROW_AUX
-#define F64_ROW_AUX 0
-#endif
 template <bool RED, bool WRAP, int LD, int PROBE = 0>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
@@ -730,19 +722,17 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     double* psi = lds_d;
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
-    double* mt = lds_d + 4 * N;   // (k_blind_rotate_f64's monomial tables; here only the exponents behind them)
+    double* mt = lds_d + 4 * N;   // monomial tables (k_blind_rotate_f64)
     __shared__ int wflag[2];
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
     for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
-    if constexpr (!F64W_MONO_ROWS) {
-        const double* mono = tabs + twoN;
-        for (uint32_t k = t; k < 128; k += TH) {
-            const uint32_t e = k < 64 ? 64 * k : k - 64;
-            const double v = __dadd_rn(mono[e], 1.0);
-            mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
-        }
+    const double* mono = tabs + twoN;
+    for (uint32_t k = t; k < 128; k += TH) {
+        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        const double v = __dadd_rn(mono[e], 1.0);
+        mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
     }
     const double* bsk = tabs + 2 * twoN;
     const uint64_t Qhalf = P.Q >> 1;
@@ -756,9 +746,6 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     const size_t round_words = (size_t)4 * P.dG2 * N;
     // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
-    // monomial factor rows [2N][N] behind the BSK (k_pack_f64_rows): row m, the lane's 4 slots = psi^(+-e) - 1
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk + (size_t)P.n * round_words), 0, -1, 0x00020000);
 
     double acc[2][CN];  // centred [Qhalf - Q, Qhalf), pass A's layout
 #pragma unroll
@@ -877,28 +864,14 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
             kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
         };
+        uint32_t ip[4];  // slot x evaluates at psi^(2 bitrev(x) + 1) (recomputed each round, the
+        uint32_t uo = u4;  // opaque copy keeps the compiler from hoisting four live values)
+        asm volatile("" : "+v"(uo));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ip[q] = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
         double S[2][4], A[2][4];
         double kv[2][4];
-        double Wp[4], Wm[4];  // psi^e - 1, psi^-e - 1 at the 4 slots: rows a'_i and 2N - a'_i
-        if constexpr (F64W_MONO_ROWS) {
-            const uint32_t mp = __builtin_amdgcn_readfirstlane(ai), mm = (twoN - mp) & (twoN - 1);
-            const v2d p0 = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(u4 * 8), (int)(mp * N * 8), F64_ROW_AUX));
-            const v2d p1 = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(u4 * 8 + 16), (int)(mp * N * 8), F64_ROW_AUX));
-            const v2d m0 = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(u4 * 8), (int)(mm * N * 8), F64_ROW_AUX));
-            const v2d m1 = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(u4 * 8 + 16), (int)(mm * N * 8), F64_ROW_AUX));
-            Wp[0] = p0.x, Wp[1] = p0.y, Wp[2] = p1.x, Wp[3] = p1.y;
-            Wm[0] = m0.x, Wm[1] = m0.y, Wm[2] = m1.x, Wm[3] = m1.y;
-        } else {  // two LDS table products per factor, once per round (round 3)
-            uint32_t uo = u4;
-            asm volatile("" : "+v"(uo));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
-                const uint32_t in = (twoN - ip) & (twoN - 1);
-                Wp[q] = __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
-                Wm[q] = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
-            }
-        }
+        double Wp[4], Wm[4];  // psi^e - 1, psi^-e - 1 at the 4 slots (built at j = 0)
         kload(0, kv[0]);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
@@ -916,6 +889,11 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
             if (kk == 1 && r == RW - 1) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    const uint32_t in = (twoN - ip[q]) & (twoN - 1);
+                    if (j == 0) {
+                        Wp[q] = __dsub_rn(fmodmul(mt[ip[q] >> 6], mt[64 + (ip[q] & 63)], K), 1.0);
+                        Wm[q] = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
+                    }
                     const double sv = fred(__dadd_rn(fmodmul(A[0][q], Wp[q], K), fmodmul(A[1][q], Wm[q], K)), K);
                     S[j][q] = sv;
                     Cn[j][q] = fred(__dadd_rn(Cn[j][q], sv), K);
@@ -981,15 +959,6 @@ __global__ void k_pack_f64(uint64_t Q, uint32_t N, uint32_t dG2, F64Fold F, cons
     }
 }
 
-// f64w's [2N][N] monomial factor rows behind the BSK: row m, slot x = psi^e - 1 (centred) for
-// e = (2 bitrev(x) + 1) m mod 2N, from the packed table mono (out + 2N); 64 MiB at N = 2048
-__global__ void k_pack_f64_rows(uint32_t N, uint32_t logN, const double* __restrict__ mono, double* __restrict__ rows) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)2 * N * N) return;
-    const uint32_t m = (uint32_t)(i / N), x = (uint32_t)(i % N);
-    rows[i] = mono[((2ull * (__builtin_bitreverse32(x) >> (32 - logN)) + 1) * m) & (2 * N - 1)];
-}
-
 uint64_t pow_mod(uint64_t b, uint64_t e, uint64_t Q) {
     unsigned __int128 r = 1, x = b % Q;
     for (; e; e >>= 1, x = x * x % Q)
@@ -1035,10 +1004,7 @@ bool f64_path_supported(const BRParams& P, int word_bits) {
     return word_bits == 64 && P.Q >= (1ull << 32) && P.Q < (1ull << 50) && P.N == 2048 && P.logG <= 32 && P.n > 0;
 }
 
-// tables psi [N], ipsi [N], mono [2N], the BSK [n][2][dG2][2][N], then f64w's factor rows [2N][N]
-size_t bsk_f64_bytes(const BRParams& P) {
-    return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N + (size_t)2 * P.N * P.N) * 8;
-}
+size_t bsk_f64_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
 
 // TFHE_F64_FOLD (read at setup): unset/2 = fold whenever thr = 0, with the WRAP correction where the top
 // digit is not always exact (STD128Q: 16.2K vs 15.2K bootstraps/s unfolded on C5a); 1 = only where it is
@@ -1079,11 +1045,6 @@ hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void
     hipLaunchKernelGGL(k_pack_f64, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, P.N, P.dG2,
                        make_fold(P, fold), (const uint64_t*)T.psi, (const uint64_t*)T.ipsi, (const uint64_t*)T.mono, (const uint64_t*)bsk,
                        words, (double*)out);
-    const size_t rows = (size_t)2 * P.N * P.N;
-    uint32_t logN = 0;
-    while ((1u << logN) < P.N) ++logN;
-    hipLaunchKernelGGL(k_pack_f64_rows, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, P.N, logN,
-                       (const double*)out + 2 * P.N, (double*)out + 4 * (size_t)P.N + words);
     return hipGetLastError();
 }
 

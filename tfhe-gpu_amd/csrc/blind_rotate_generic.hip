@@ -707,7 +707,8 @@ __device__ __forceinline__ uint64_t tw1(const SfTwB& T, uint32_t i) {
 // Monomial factors from two 64-entry LDS tables instead of gathers from the 2N-entry table in
 // memory (those missed the cache and stalled every round, profiles/r02z): T[j] = psi^(64 j),
 // T[64 + j] = psi^j as (W0, W1) pairs, built from mono = psi^k - 1 at kernel start, and
-//     A (psi^e - 1) = sf(sf(A, T[e >> 6]), T[64 + (e & 63)]) + (10Q - fold(A))
+//     A0 (psi^e0 - 1) + A1 (psi^e1 - 1) = sf(sf(A0, T[e0 >> 6]), T[64 + (e0 & 63)]) + (the same for A1)
+//                                       + (10Q - fold(A0 + A1))
 constexpr uint32_t SF_MT = 256;  // u64 words of the two tables
 __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __restrict__ mono,
                                                const uint64_t* __restrict__ mono1, uint64_t Q) {
@@ -718,11 +719,17 @@ __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __re
         T[2 * k + 1] = w1 >= Q ? w1 - Q : w1;
     }
 }
-__device__ __forceinline__ uint64_t sf_mono_mul(uint64_t A, uint32_t e, const uint64_t* T, const SfC& K) {
-    const uint64_t* th = T + 2 * (e >> 6);
-    const uint64_t* tl = T + 2 * (64 + (e & 63));
-    // the offset subtracts A folded below 1.01 Q: gen3sf's A sums 2 products per digit (up to 8 digits)
-    return sf_mul(sf_mul(A, th[0], th[1], K.c2), tl[0], tl[1], K.c2) + (K.Q10 - sf_fold(A, K.c));
+// both keys' factors of one column: A0 (psi^e0 - 1) + A1 (psi^e1 - 1), the two offsets merged into one
+// subtraction of fold(A0 + A1), the sum folded (< 1.01 Q)
+__device__ __forceinline__ uint64_t sf_mono_pair(uint64_t A0, uint32_t e0, uint64_t A1, uint32_t e1, const uint64_t* T,
+                                                 const SfC& K) {
+    const uint64_t* h0 = T + 2 * (e0 >> 6);
+    const uint64_t* l0 = T + 2 * (64 + (e0 & 63));
+    const uint64_t* h1 = T + 2 * (e1 >> 6);
+    const uint64_t* l1 = T + 2 * (64 + (e1 & 63));
+    const uint64_t p0 = sf_mul(sf_mul(A0, h0[0], h0[1], K.c2), l0[0], l0[1], K.c2);
+    const uint64_t p1 = sf_mul(sf_mul(A1, h1[0], h1[1], K.c2), l1[0], l1[1], K.c2);
+    return sf_fold(p0 + p1 + (K.Q10 - sf_fold(A0 + A1, K.c)), K.c);
 }
 
 template <class TW>
@@ -931,9 +938,8 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
         for (int k = 0; k < CN; ++k) {
             const uint32_t x = t + TH * k;
             const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            buf[ts + TH * k] = sf_fold(sf_mono_mul(A[0][0][k], ip, mt, K) + sf_mono_mul(A[1][0][k], in, mt, K), K.c);
-            buf[N + ts + TH * k] =
-                sf_fold(sf_mono_mul(A[0][1][k], ip, mt, K) + sf_mono_mul(A[1][1][k], in, mt, K), K.c);
+            buf[ts + TH * k] = sf_mono_pair(A[0][0][k], ip, A[1][0][k], in, mt, K);
+            buf[N + ts + TH * k] = sf_mono_pair(A[0][1][k], ip, A[1][1][k], in, mt, K);
         }
         __syncthreads();
         uint64_t v[8];
@@ -1080,24 +1086,10 @@ __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], 
     sf_inv_core<false>(v, 4, 0, T, K);
 }
 
-// SF2_MONO_ROWS: the factors from the row tables (1) or the two-level LDS tables (0); SF_ROW_AUX: cache
-// policy of the row loads (2 = nt)
-#ifndef SF2_MONO_ROWS
-#define SF2_MONO_ROWS 1
-#endif
-#ifndef SF_ROW_AUX
-#define SF_ROW_AUX 0
-#endif
-// Monomial factors (round 4): row m of the [2N][N] tables holds psi^e - 1, e = (2 bitrev(x) + 1) m mod 2N,
-// for every slot x in the transform's output order (W0 in mrow, W1 in mrow1; k_pack_mono_rows), so
-// a round reads two rows -- m = a'_i for the + key, 2N - a'_i for the - key -- as 64 contiguous bytes
-// per lane, like a key row, and A (X^(+-a') - 1) is ONE sf product (round 3: two products by the
-// two-level LDS tables plus an offset subtraction, and the slot exponents computed every round).
 template <int DIG>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
-                   const uint64_t* __restrict__ mrow, const uint64_t* __restrict__ mrow1,
                    const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
                    const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
@@ -1111,8 +1103,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
-    uint64_t* mt = psi1_l + N;  // monomial tables (SF2_MONO_ROWS = 0)
-    if constexpr (!SF2_MONO_ROWS) sf_mono_tables(mt, mono, mono1, Q);
+    uint64_t* mt = psi1_l + N;  // monomial tables
+    sf_mono_tables(mt, mono, mono1, Q);
     const SfTw TF{psi_l, psi1_l};
     const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
@@ -1137,8 +1129,6 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
 
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rm0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow), 0, -1, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rm1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow1), 0, -1, 0x00020000);
     // the decomposition's offsets: digit l of x is that of c + Kd_l, c = x or x - Q (centred), i.e. of
     // x + (x < Q/2 ? Kd_l : Kd_l - Q); the digit r in [-B/2, B/2) enters the transform as r + Q (< 2Q,
     // congruent, no sign test; tools/bounds_sf.py starts the forward transform at 2Q)
@@ -1179,36 +1169,39 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
             if (LAST_LDS && l == DIG - 1) sf2_ntt_fwd<true>(buf, v, D[l], TF, K);
             else sf2_ntt_fwd(buf, v, D[l], TF, K);
         }
-        // products: per column j, groups (key kk, row r = 2l + polynomial) of 4 slots x (W0, W1) of key
-        // words, then two monomial groups (rows a'_i and 2N - a'_i of the factor tables); the next
-        // group's words are loaded before this group's arithmetic.  A_kj of slots u4 + s (< 2.3 Q per
-        // digit); the + key's factor product is kept in A[0] until the - key's is added.
-        constexpr int RW = 2 * DIG, GJ = 2 * RW + (SF2_MONO_ROWS ? 2 : 0), NG = 2 * GJ;
-        const uint32_t mplus = __builtin_amdgcn_readfirstlane(ai), mminus = (twoN - mplus) & (twoN - 1);  // uniform
-        // key words and factor rows through buffer resources: uniform row offset, 32-bit lane offset
+        // products: group g = (column j, key kk, row r = 2l + polynomial), 4 slots x (W0, W1) of key
+        // words each, the next group's loaded before this group's arithmetic; A_kj of slots u4 + s
+        // (< 2.3 Q per digit); once both keys of column j are summed, its monomial factors from the
+        // two-level LDS tables (sf_mono_pair).  (Round 4 measured [2N][N] factor rows read from memory
+        // instead, one product per factor: 24 % fewer VALU, but 17x the L2 fetches and slower on C3;
+        // DESIGN.md 3.2c.)
+        constexpr int RW = 2 * DIG, NG = 4 * RW;
+        // key words through buffer resources: uniform round + row offset, 32-bit lane offset
         auto kload = [&](int g, uint64_t (&kw)[8]) {
-            const uint32_t j = g / GJ, q = g % GJ, kk = q / RW, r = q % RW;
-            const bool mono_g = q >= 2 * RW;
-            const uint32_t o = mono_g ? (q == 2 * RW ? mplus : mminus) * N * 8
-                                      : round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
-            const __amdgpu_buffer_rsrc_t r0 = mono_g ? rm0 : rk0, r1 = mono_g ? rm1 : rk1;
-            v4u a0, a1, b0, b1;
-#define SF2_LOAD4(AUX)                                                                                              \
-    a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8), (int)o, AUX));          \
-    a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8 + 16), (int)o, AUX));     \
-    b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8), (int)o, AUX));          \
-    b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8 + 16), (int)o, AUX));
-            if (mono_g) {
-                SF2_LOAD4(SF_ROW_AUX)
-            } else {
-                SF2_LOAD4(0)
-            }
-#undef SF2_LOAD4
+            const uint32_t j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
+            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
+            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
+            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
             kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
             kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
             kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
             kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
         };
+        // slot x evaluates at psi^(2 bitrev(x) + 1): the exponents of the lane's 4 slots, computed once per
+        // round (one digit) or at each column's factors (more digits: 4 fewer live VGPRs through the
+        // products, 45 -> 16 scratch operations per round for two); the opaque copy keeps the compiler
+        // from hoisting them out of the round loop
+        constexpr bool IP_ONCE = DIG == 1;
+        uint32_t ip[4];
+        auto slot_exponents = [&]() {
+            uint32_t uo = u4;
+            asm volatile("" : "+v"(uo));
+#pragma unroll
+            for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+        };
+        if constexpr (IP_ONCE) slot_exponents();
         uint64_t S[2][4], A[2][4];
         uint64_t kw[2][8];
         kload(0, kw[0]);
@@ -1216,32 +1209,18 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         for (int g = 0; g < NG; ++g) {
             if (g + 1 < NG) kload(g + 1, kw[(g + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            const int j = g / GJ, q = g % GJ, kk = q / RW, r = q % RW;
+            const int j = g / (2 * RW), kk = (g / RW) & 1, r = g % RW;
             const uint64_t(&c)[8] = kw[g & 1];
-            if (q < 2 * RW) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const uint64_t dv = (LAST_LDS && r >= RW - 2) ? buf[(r & 1) * N + (g3_swz(u4) ^ s)] : D[r >> 1][r & 1][s];
-                    const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
-                    A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
-                }
-                if (!SF2_MONO_ROWS && kk == 1 && r == RW - 1) {  // two-level LDS factor tables
-                    uint32_t uo = u4;
-                    asm volatile("" : "+v"(uo));
+            for (int s = 0; s < 4; ++s) {
+                const uint64_t dv = (LAST_LDS && r >= RW - 2) ? buf[(r & 1) * N + (g3_swz(u4) ^ s)] : D[r >> 1][r & 1][s];
+                const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
+                A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
+            }
+            if (kk == 1 && r == RW - 1) {
+                if constexpr (!IP_ONCE) slot_exponents();
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
-                        const uint32_t in = (twoN - ip) & (twoN - 1);
-                        S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip, mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
-                    }
-                    if constexpr (!LAST_LDS) sf2_inv_unit(buf, j, S[j], TI, K);
-                }
-            } else if (q == 2 * RW) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) A[0][s] = sf_mul(A[0][s], c[s], c[4 + s], K.c2);  // A_0j (X^a' - 1)
-            } else {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) S[j][s] = sf_fold(A[0][s] + sf_mul(A[1][s], c[s], c[4 + s], K.c2), K.c);
+                for (int s = 0; s < 4; ++s) S[j][s] = sf_mono_pair(A[0][s], ip[s], A[1][s], (twoN - ip[s]) & (twoN - 1), mt, K);
                 // two digits: the buffer is dead after the last forward units (its outputs are in
                 // registers), so column j's inverse units run now and S[j] dies here (fewer live
                 // registers through column 1's products).  One or three digits: the buffer still holds
@@ -1307,7 +1286,6 @@ __device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                       const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
-                      const uint64_t* __restrict__ mrow, const uint64_t* __restrict__ mrow1,
                       const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
                       const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
                       const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, SfDuo X,
@@ -1326,8 +1304,8 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
-    uint64_t* mt = psi1_l + N;
-    if constexpr (!SF2_MONO_ROWS) sf_mono_tables(mt, mono, mono1, Q);
+    uint64_t* mt = psi1_l + N;  // monomial tables
+    sf_mono_tables(mt, mono, mono1, Q);
     const SfTw TF{psi_l, psi1_l};
     const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
@@ -1349,8 +1327,6 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
 
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rm0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow), 0, -1, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rm1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(mrow1), 0, -1, 0x00020000);
     int64_t Kd = 0;  // digit `half` of acc_x (sf2's closed-form offsets)
     for (uint32_t z = 0; z < half + P.thr; ++z) Kd = (Kd << logG) + Bh;
     const int64_t Klo = Kd, Khi = Kd - Qs;
@@ -1371,32 +1347,25 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
         uint64_t D[2][4];  // D[l][s]: digit l of acc_x at slots u4 + s
         if (i > 0) __syncthreads();  // every thread has read the previous round's exchange from the buffer
         sf2_ntt_fwd(buf, v, D, TF, K);
-        // products: per column j, groups (key kk, digit l: row 2l + x), then the two factor rows
-        constexpr int RW = 2, GJ = 2 * RW + (SF2_MONO_ROWS ? 2 : 0), NG = 2 * GJ;
-        const uint32_t mplus = __builtin_amdgcn_readfirstlane(ai), mminus = (twoN - mplus) & (twoN - 1);
+        // products: group g = (column j, key kk, digit l: key row 2l + x), then column j's factors
+        constexpr int RW = 2, NG = 4 * RW;
         auto kload = [&](int gi, uint64_t (&kw)[8]) {
-            const uint32_t j = gi / GJ, q = gi % GJ, kk = q / RW, l = q % RW;
-            const bool mono_g = q >= 2 * RW;
-            const uint32_t o = mono_g ? (q == 2 * RW ? mplus : mminus) * N * 8
-                                      : round_off + ((kk * P.dG2 + 2 * l + x) * 2 + j) * N * 8;
-            const __amdgpu_buffer_rsrc_t r0 = mono_g ? rm0 : rk0, r1 = mono_g ? rm1 : rk1;
-            v4u a0, a1, b0, b1;
-#define SF2_LOAD4(AUX)                                                                                              \
-    a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8), (int)o, AUX));          \
-    a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r0, (int)(u4 * 8 + 16), (int)o, AUX));     \
-    b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8), (int)o, AUX));          \
-    b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r1, (int)(u4 * 8 + 16), (int)o, AUX));
-            if (mono_g) {
-                SF2_LOAD4(SF_ROW_AUX)
-            } else {
-                SF2_LOAD4(0)
-            }
-#undef SF2_LOAD4
+            const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, l = gi % RW;
+            const uint32_t o = round_off + ((kk * P.dG2 + 2 * l + x) * 2 + j) * N * 8;
+            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
+            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
+            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
+            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
             kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
             kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
             kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
             kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
         };
+        uint32_t ip[4];
+        uint32_t uo = u4;
+        asm volatile("" : "+v"(uo));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
         uint64_t S[2][4], A[2][4];
         uint64_t kw[2][8];
         kload(0, kw[0]);
@@ -1404,31 +1373,16 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
         for (int gi = 0; gi < NG; ++gi) {
             if (gi + 1 < NG) kload(gi + 1, kw[(gi + 1) & 1]);
             __builtin_amdgcn_sched_barrier(0);
-            const int j = gi / GJ, q = gi % GJ, kk = q / RW, l = q % RW;
+            const int j = gi / (2 * RW), kk = (gi / RW) & 1, l = gi % RW;
             const uint64_t(&c)[8] = kw[gi & 1];
-            if (q < 2 * RW) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const uint64_t prod = sf_mul(D[l][s], c[s], c[4 + s], K.c2);
-                    A[kk][s] = l == 0 ? prod : A[kk][s] + prod;
-                }
-                if (!SF2_MONO_ROWS && kk == 1 && l == RW - 1) {
-                    uint32_t uo = u4;
-                    asm volatile("" : "+v"(uo));
+            for (int s = 0; s < 4; ++s) {
+                const uint64_t prod = sf_mul(D[l][s], c[s], c[4 + s], K.c2);
+                A[kk][s] = l == 0 ? prod : A[kk][s] + prod;
+            }
+            if (kk == 1 && l == RW - 1) {
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
-                        const uint32_t in = (twoN - ip) & (twoN - 1);
-                        S[j][s] = sf_fold(sf_mono_mul(A[0][s], ip, mt, K) + sf_mono_mul(A[1][s], in, mt, K), K.c);
-                    }
-                    sf2_inv_unit(buf, j, S[j], TI, K);
-                }
-            } else if (q == 2 * RW) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) A[0][s] = sf_mul(A[0][s], c[s], c[4 + s], K.c2);
-            } else {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) S[j][s] = sf_fold(A[0][s] + sf_mul(A[1][s], c[s], c[4 + s], K.c2), K.c);
+                for (int s = 0; s < 4; ++s) S[j][s] = sf_mono_pair(A[0][s], ip[s], A[1][s], (twoN - ip[s]) & (twoN - 1), mt, K);
                 sf2_inv_unit(buf, j, S[j], TI, K);  // the buffer is dead after the forward units
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -1489,19 +1443,6 @@ __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ i
     const uint64_t w = in[i] % Q;
     const uint64_t x = ((w & ((1ull << (SF_K - 32)) - 1)) << 32) + (w >> (SF_K - 32)) * c;
     out[i] = x >= Q ? x - Q : x;
-}
-
-// the [2N][N] monomial factor rows of k_blind_rotate_sf2: row m, slot x = psi^e - 1 for
-// e = (2 bitrev(x) + 1) m mod 2N, taken from the arena's table mono[e] = psi^e - 1 (W0) and its packed
-// companion mono1[e] (W1 = W0 2^32 mod Q, k_pack_sf)
-__global__ void k_pack_mono_rows(uint64_t Q, const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
-                                 uint32_t N, uint32_t logN, uint64_t* __restrict__ row0, uint64_t* __restrict__ row1) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)2 * N * N) return;
-    const uint32_t m = (uint32_t)(i / N), x = (uint32_t)(i % N);
-    const uint32_t e = (uint32_t)(((2ull * (__builtin_bitreverse32(x) >> (32 - logN)) + 1) * m) & (2 * N - 1));
-    row0[i] = mono[e] % Q;
-    row1[i] = mono1[e];
 }
 
 }  // namespace
@@ -1581,10 +1522,8 @@ bool sf_path_supported(const BRParams& P, int word_bits) {
            P.logG < 64 && P.n > 0;
 }
 
-// W1 arrays behind the arena's W0 ones: psi [N], ipsi [N], mono [2N], bsk [n][2][dG2][2][N]; then sf2's
-// monomial factor rows W0 [2N][N] and W1 [2N][N] (128 MiB at N = 2048)
-static size_t sf_w1_words(const BRParams& P) { return (size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N; }
-size_t sf_bytes(const BRParams& P) { return (sf_w1_words(P) + (size_t)4 * P.N * P.N) * 8; }
+// W1 arrays behind the arena's W0 ones: psi [N], ipsi [N], mono [2N], bsk [n][2][dG2][2][N]
+size_t sf_bytes(const BRParams& P) { return ((size_t)4 * P.N + (size_t)P.n * 4 * P.dG2 * P.N) * 8; }
 
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s) {
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
@@ -1596,12 +1535,6 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
     for (const Part& q : parts)
         hipLaunchKernelGGL(k_pack_sf, dim3((unsigned)((q.n + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q, c,
                            (const uint64_t*)q.src, q.n, o + q.off);
-    uint64_t* rows = o + sf_w1_words(P);
-    const size_t row_words = (size_t)2 * P.N * P.N;
-    uint32_t logN = 0;
-    while ((1u << logN) < P.N) ++logN;
-    hipLaunchKernelGGL(k_pack_mono_rows, dim3((unsigned)((row_words + 255) / 256)), dim3(256), 0, s, (uint64_t)P.Q,
-                       (const uint64_t*)T.mono, (const uint64_t*)(o + 2 * P.N), P.N, logN, rows, rows + row_words);
     return hipGetLastError();
 }
 
@@ -1625,10 +1558,9 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     if (!no_sf2 && fits32 && P.digits >= 1 && P.digits <= 3) {
         auto go = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            const uint64_t* rows = w1 + sf_w1_words(P);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
-                               (const uint64_t*)T.ipsi, w1 + P.N, rows, rows + (size_t)2 * P.N * P.N,
-                               (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
+                               (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
+                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
         };
         if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
             SfDuo X;
@@ -1636,12 +1568,11 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
             X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * G3_N);
             X.err = X.flags + kDuoMaxPairs * 2 * 32;
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
-            const uint64_t* rows = w1 + sf_w1_words(P);
             (void)hipFuncSetAttribute((const void*)k_blind_rotate_sf2duo, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
             hipLaunchKernelGGL(k_blind_rotate_sf2duo, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), lds, s, P, K,
-                               (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, rows,
-                               rows + (size_t)2 * P.N * P.N, (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk,
+                               (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono,
+                               w1 + 2 * P.N, (const uint64_t*)bsk,
                                w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
             return hipGetLastError();
         }

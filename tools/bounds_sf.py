@@ -132,14 +132,11 @@ def model(rows, sf2=True):
     D = max(fwd_r4(x))
     R = mulw(D)
     Ap = rows * 2 * R           # rows digits x 2 polynomials per (key, column)
-    # A0j (X^a' - 1) + A1j (X^-a' - 1), the sum folded: sf2 multiplies by the factor rows (one product
-    # per term); gen3sf by two LDS table factors per term, sf(sf(A, T_hi), T_lo) + (10Q - fold(A))
-    if sf2:
-        S = fold(2 * mulw(Ap))
-    else:
-        if fold(Ap) > 10 * Q:
-            fail("monomial offset 10Q below the folded product sum")
-        S = fold(2 * (mulw(mulw(Ap)) + 10 * Q))
+    # A0j (X^a' - 1) + A1j (X^-a' - 1) by two LDS table factors per term (sf_mono_pair):
+    # sf(sf(A0, T_hi), T_lo) + sf(sf(A1, T_hi'), T_lo') + (10Q - fold(A0 + A1)), the sum folded
+    if fold(2 * Ap) > 10 * Q:
+        fail("monomial offset 10Q below the folded product sum")
+    S = fold(2 * mulw(mulw(Ap)) + 10 * Q)
     x = max(inv_r4(S, INV_FOLD_UNITS))
     x = max(inv_r8(x, INV_FOLD_PASS))
     x = max(inv_r8(x, INV_FOLD_PASS))
