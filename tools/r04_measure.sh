@@ -29,7 +29,7 @@ for s in $STEPS; do
     suite)
       # the whole GPU suite under a kernel trace: which kernel instances the parity tests run
       timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/suite_prof -o run --output-format csv -- \
-        python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || rc=$? ;;
+        python3 -u -m pytest -x -v --timeout 170 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || rc=$? ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || rc=$? ;;
     *)
