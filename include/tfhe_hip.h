@@ -56,7 +56,8 @@ extern "C" {
 #define TFHE_HIP_ABI_VERSION 6  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
                                    4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows);
                                    5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs;
-                                   6: tfhe_knobs.duo, tfhe_info.duo_timeouts (two-workgroup sf2 form) */
+                                   6: tfhe_knobs.duo / .sf2p, tfhe_info.duo_timeouts (two-workgroup and
+                                      two-ciphertext sf2 forms) */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -262,6 +263,8 @@ typedef struct tfhe_knobs {
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
     int32_t duo;          /* two-digit special-form contexts: batches up to this size (default 128, at most 256) run
                              each ciphertext on two workgroups (sf2duo); 0: never */
+    int32_t sf2p;         /* 0: one ciphertext per workgroup in the special-form kernel instead of two (sf2p, whose
+                             shared LDS holds the whole monomial factor table) */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
 tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);

@@ -1,6 +1,7 @@
 """GPU: the special-form kernels at every digit count a Q = 2^54 - c context reaches.
 
-sf2 is built for 1, 2 and 3 transformed digits (3: the CHES-experiments.cpp EvalFunc context,
+sf2 is built for 1, 2 and 3 transformed digits (2 also as sf2p, two ciphertexts per 1024-thread
+workgroup with the whole monomial table in their shared LDS -- the default above the duo batches) (3: the CHES-experiments.cpp EvalFunc context,
 GenerateBinFHEContext(STD128, true, 12, 0, GINX, false, 1 << 18) -- baseG 2^18, no thrown digit),
 gen3sf takes more (TOY logQ 29: 4, tests/test_gpu_unittest_func.py) and is the cross-check of all
 (knob sf2 = 0).  Per context: EvalAcc on 5 ciphertexts bit-exact against the oracle, and 64
@@ -56,3 +57,17 @@ def test_sf2_equals_gen3sf(sfctx):
     with ctx.knobs_set(sf2=0):
         ref = ctx.EvalAcc(a, 2 * op.N, acc)
     assert np.array_equal(one, ref)
+
+
+@pytest.mark.parametrize("B", [1, 63, 64])
+def test_sf2_pair_form_equals_one_ciphertext_form(sfctx, B):
+    """sf2p (default) = sf2 with one ciphertext per workgroup (knob sf2p = 0), odd batches included
+    (the last workgroup's second half repeats its neighbour and does not store)."""
+    op, ctx, orc = sfctx
+    a, acc = _inputs(op, B, 13 + B)
+    with ctx.knobs_set(duo=0):
+        two = ctx.EvalAcc(a, 2 * op.N, acc)
+        with ctx.knobs_set(sf2p=0):
+            one = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(two, one)
+    assert np.array_equal(two[-1:].reshape(1, -1), orc.eval_acc(a[-1:], 2 * op.N, acc[-1:]).reshape(1, -1))

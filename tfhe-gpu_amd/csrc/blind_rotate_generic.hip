@@ -986,11 +986,13 @@ __device__ __forceinline__ void wl_sync() {  // order this wave's LDS accesses (
 // forward: pass A from registers (polynomial t >> 8), barrier, B and C wave-local; then the units
 // of u = 64w + l for both polynomials into d[p][j] = slot 4u + j
 // TO_LDS: the units' outputs stay in the buffer (read back by this wave's products)
-template <bool TO_LDS = false>
-__device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uint64_t (&d)[2][4], const SfTw& T,
+// PAIR: two ciphertexts per 1024-thread workgroup (k_blind_rotate_sf2p): the thread's index within its
+// ciphertext's 512 threads
+template <bool TO_LDS = false, class TW = SfTw, bool PAIR = false>
+__device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uint64_t (&d)[2][4], const TW& T,
                                             const SfC& K) {
     constexpr uint32_t N = G3_N;
-    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t t = PAIR ? threadIdx.x & 511 : threadIdx.x, l = t & 63, w = t >> 6;
     {
         const uint32_t tau = g3_tau();
         uint64_t* p = buf + (t >> 8) * N;
@@ -1037,11 +1039,11 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
 // inverse: units of slots 4u .. 4u+3 from registers (second stage's sums folded), C and B
 // wave-local (last stage's sums folded), barrier, pass A into v (polynomial t >> 8, < 18.1 Q)
 // the units of polynomial q (this lane's own slots of the buffer)
-template <class TW>
+template <class TW, bool PAIR = false>
 __device__ __forceinline__ void sf2_inv_unit(uint64_t* buf, int q, const uint64_t (&sq)[4], const TW& T,
                                              const SfC& K) {
     constexpr uint32_t N = G3_N;
-    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t t = PAIR ? threadIdx.x & 511 : threadIdx.x, l = t & 63, w = t >> 6;
     const uint32_t u = (w << 6) | l, u0 = g3_swz(4 * u);
     uint64_t* pq = buf + q * N;
     uint64_t v0 = sq[0], v1 = sq[1], v2 = sq[2], v3 = sq[3];
@@ -1050,14 +1052,14 @@ __device__ __forceinline__ void sf2_inv_unit(uint64_t* buf, int q, const uint64_
     pq[u0] = v0, pq[u0 ^ 1] = v1, pq[u0 ^ 2] = v2, pq[u0 ^ 3] = v3;
 }
 // UNITS = false: the caller has already run both polynomials' units (sf2_inv_unit)
-template <bool UNITS = true, class TW>
+template <bool UNITS = true, class TW, bool PAIR = false>
 __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], uint64_t (&v)[8], const TW& T,
                                             const SfC& K) {
     constexpr uint32_t N = G3_N;
-    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t t = PAIR ? threadIdx.x & 511 : threadIdx.x, l = t & 63, w = t >> 6;
     if constexpr (UNITS) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) sf2_inv_unit(buf, q, s[q], T, K);
+        for (int q = 0; q < 2; ++q) sf2_inv_unit<TW, PAIR>(buf, q, s[q], T, K);
     }
     wl_sync();
     uint32_t tw = (w << 5) | (l & 31);
@@ -1249,6 +1251,170 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
         const uint64_t v = buf[k == 0 ? 0 : N - k];
         g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
         g[N + k] = buf[N + k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// sf2p: sf2 with TWO ciphertexts per 1024-thread workgroup (one per CU, 4 waves per SIMD as before),
+// so the LDS the two share can hold the whole 2N-entry monomial factor table -- row e = (psi^e - 1,
+// its W1), 64 KiB -- and A (X^(+-a') - 1) is ONE product per factor instead of two table products
+// and an offset (sf_mono_pair).  The forward twiddles move from LDS to memory (buffer loads, like the
+// inverse ones) to make room: per workgroup 2 x (32 KiB polynomial buffer + the exponents) + 64 KiB.
+// Threads 512 h .. 512 h + 511 run ciphertext 2 b + h with sf2's code (the transform helpers take the
+// thread's index within its ciphertext); every barrier is reached by both halves in the same order.
+template <int DIG>
+__global__ void __launch_bounds__(2 * G3_TH, 4)
+k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
+                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                    const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                    const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
+                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, uint32_t B) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = G3_N, TH = G3_TH, CN = G3_CN;
+    const uint32_t half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 9);
+    const uint32_t t = threadIdx.x & 511, twoN = 2 * N, logG = P.logG;
+    const uint32_t ct = min(2 * blockIdx.x + half, B - 1);  // an odd batch: the last half repeats its neighbour
+    const bool owner = 2 * blockIdx.x + half < B;
+    uint64_t* buf = reinterpret_cast<uint64_t*>(smem) + (size_t)half * 2 * N;  // [2][N] of this ciphertext
+    uint64_t* mtab = reinterpret_cast<uint64_t*>(smem) + (size_t)4 * N;        // [2N] (W0, W1), shared
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * N + 4 * N) * 8 + half * rot_exponent_bytes(P.n));
+    const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    for (uint32_t k = threadIdx.x; k < twoN; k += 2 * TH) {
+        mtab[2 * k] = mono[k] % Q;  // psi^k - 1
+        mtab[2 * k + 1] = mono1[k];
+    }
+    const SfTwB TF{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(psi), 0, (int)(N * 8), 0x00020000),
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(psi1), 0, (int)(N * 8), 0x00020000)};
+    const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
+    uint64_t* g = acc_io + (size_t)ct * twoN;
+    const uint64_t* ap = a + (size_t)ct * P.n;
+    {
+        const uint64_t scale = (uint64_t)twoN / amod;  // stage_rot_exponents for this half's 512 threads
+        for (uint32_t k = t; k < P.n; k += TH) {
+            const uint64_t ar = ap[k] % amod;
+            ex[k] = (uint32_t)((ar == 0 ? 0 : amod - ar) * scale);
+        }
+    }
+    __syncthreads();
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
+    auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
+
+    uint64_t acc[2][CN];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) {
+            const uint64_t v = g[lpos(p, k)];
+            acc[p][k] = v >= Q ? v % Q : v;
+        }
+
+    const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
+    int64_t Kdl[DIG];
+#pragma unroll
+    for (int l = 0; l < DIG; ++l) {
+        int64_t Kd = 0;
+        for (uint32_t z = 0; z < l + P.thr; ++z) Kd = (Kd << logG) + Bh;
+        Kdl[l] = Kd;
+    }
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint32_t ai = ex[i];
+        const uint32_t round_off = i * (uint32_t)round_words * 8;
+        constexpr bool LAST_LDS = (DIG & 1) != 0;
+        uint64_t D[DIG][2][4];
+#pragma unroll
+        for (int l = 0; l < DIG; ++l) {
+            const uint32_t shift = (l + P.thr) * logG;
+            const int64_t Klo = Kdl[l], Khi = Kdl[l] - Qs;
+            uint64_t v[8];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int k = 0; k < CN; ++k) {
+                    const uint64_t x = acc[p][k];
+                    const int64_t d = ((int64_t)x + (x < Qhalf ? Klo : Khi)) >> shift;
+                    const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    v[p * CN + k] = (uint64_t)(r + Qs);
+                }
+            if (l > 0) __syncthreads();
+            if (LAST_LDS && l == DIG - 1) sf2_ntt_fwd<true, SfTwB, true>(buf, v, D[l], TF, K);
+            else sf2_ntt_fwd<false, SfTwB, true>(buf, v, D[l], TF, K);
+        }
+        constexpr int RW = 2 * DIG, NG = 4 * RW;
+        auto kload = [&](int gi, uint64_t (&kw)[8]) {
+            const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
+            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
+            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
+            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
+            kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
+            kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
+            kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
+            kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
+        };
+        constexpr bool IP_ONCE = DIG == 1;
+        uint32_t ip[4];
+        auto slot_exponents = [&]() {
+            uint32_t uo = u4;
+            asm volatile("" : "+v"(uo));
+#pragma unroll
+            for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+        };
+        if constexpr (IP_ONCE) slot_exponents();
+        uint64_t S[2][4], A[2][4];
+        uint64_t kw[2][8];
+        kload(0, kw[0]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gi + 1 < NG) kload(gi + 1, kw[(gi + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
+            const uint64_t(&c)[8] = kw[gi & 1];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint64_t dv = (LAST_LDS && r >= RW - 2) ? buf[(r & 1) * N + (g3_swz(u4) ^ s)] : D[r >> 1][r & 1][s];
+                const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
+                A[kk][s] = r == 0 ? prod : A[kk][s] + prod;
+            }
+            if (kk == 1 && r == RW - 1) {
+                if constexpr (!IP_ONCE) slot_exponents();
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {  // one table product per factor (row e holds psi^e - 1)
+                    const uint64_t* fp = mtab + 2 * ip[s];
+                    const uint64_t* fm = mtab + 2 * ((twoN - ip[s]) & (twoN - 1));
+                    S[j][s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
+                }
+                if constexpr (!LAST_LDS) sf2_inv_unit<SfTwB, true>(buf, j, S[j], TI, K);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint64_t v[8];
+        sf2_ntt_inv<LAST_LDS, SfTwB, true>(buf, S, v, TI, K);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < CN; ++k) {
+                const uint64_t x = sf_fold(acc[p][k] + v[p * CN + k], K.c);
+                acc[p][k] = x >= Q ? x - Q : x;
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = acc[p][k];
+    __syncthreads();
+    if (owner) {
+        for (uint32_t k = t; k < N; k += TH) {  // acc0 transposed (poly.cpp:762-770)
+            const uint64_t v = buf[k == 0 ? 0 : N - k];
+            g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+            g[N + k] = buf[N + k];
+        }
     }
 }
 
@@ -1575,6 +1741,21 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                w1 + 2 * P.N, (const uint64_t*)bsk,
                                w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
             return hipGetLastError();
+        }
+        // two ciphertexts per workgroup, the monomial table in LDS: two digits only (same box, three reps,
+        // profiles/r04m: C5b 70.8 -> 67.7 ms per launch; one digit went the other way, 172.3 -> 178.0 ms,
+        // the forward twiddles now read from memory costing more than the table saves)
+        if (P.digits == 2 && kn.sf2p) {
+            const size_t ldsp = (size_t)8 * G3_N * 8 + 2 * rot_exponent_bytes(P.n);
+            if (ldsp <= 160 * 1024) {
+                auto kern = k_blind_rotate_sf2p<2>;
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp);
+                hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(2 * G3_TH), ldsp, s, P, K,
+                                   (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N,
+                                   (const uint64_t*)T.mono, w1 + 2 * P.N, (const uint64_t*)bsk, w1 + 4 * P.N, a, amod,
+                                   acc, (uint32_t)B);
+                return hipGetLastError();
+            }
         }
         if (P.digits == 3) go(k_blind_rotate_sf2<3>);  // (CHES-experiments.cpp's EvalFunc context, baseG 2^18)
         else if (P.digits == 2) go(k_blind_rotate_sf2<2>);

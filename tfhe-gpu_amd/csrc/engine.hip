@@ -210,6 +210,7 @@ Knobs knobs_from_env() {
     num("TFHE_F64W", k.f64w);
     num("TFHE_SF2", k.sf2);
     num("TFHE_DUO", k.duo);
+    num("TFHE_SF2P", k.sf2p);
     num("TFHE_GENERIC", k.generic);
     if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
     if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;

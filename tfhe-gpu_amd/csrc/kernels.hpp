@@ -31,6 +31,7 @@ struct Knobs {
     int32_t trace = 0;          // host-array runner timeline on stderr
     int32_t probe = 0;          // test library only (TFHE_TEST_PROBES): f64w fault probe / timing builds
     int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup sf2 form (two digits, <= 256); 0: never
+    int32_t sf2p = 1;           // 0: sf2 with one ciphertext per workgroup instead of two (sf2p) above the duo batches
 };
 
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).

@@ -53,7 +53,8 @@ class Info(C.Structure):
 class Knobs(C.Structure):
     """tfhe_knobs: launch choices of a context (include/tfhe_hip.h), environment at setup, then tfhe_set_knobs."""
     _fields_ = [(k, C.c_int32) for k in ("ks_tiled_min", "ks_cts", "ks_split", "ks_pk", "host_parts", "wire",
-                                         "acc_flags", "f64w", "sf2", "generic", "trace", "probe", "duo")]
+                                         "acc_flags", "f64w", "sf2", "generic", "trace", "probe", "duo",
+                                         "sf2p")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
