@@ -59,10 +59,10 @@ def test_sf2_equals_gen3sf(sfctx):
     assert np.array_equal(one, ref)
 
 
-@pytest.mark.parametrize("B", [1, 63, 64])
+@pytest.mark.parametrize("B", [511, 512, 513])
 def test_sf2_pair_form_equals_one_ciphertext_form(sfctx, B):
-    """sf2p (default) = sf2 with one ciphertext per workgroup (knob sf2p = 0), odd batches included
-    (the last workgroup's second half repeats its neighbour and does not store)."""
+    """sf2p (default from 512 ciphertexts) = sf2 with one ciphertext per workgroup (knob sf2p = 0), odd
+    batches included (the last workgroup's second half repeats its neighbour and does not store)."""
     op, ctx, orc = sfctx
     a, acc = _inputs(op, B, 13 + B)
     with ctx.knobs_set(duo=0):

@@ -1745,7 +1745,9 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
         // two ciphertexts per workgroup, the monomial table in LDS: two digits only (same box, three reps,
         // profiles/r04m: C5b 70.8 -> 67.7 ms per launch; one digit went the other way, 172.3 -> 178.0 ms,
         // the forward twiddles now read from memory costing more than the table saves)
-        if (P.digits == 2 && kn.sf2p) {
+        // (from 512 ciphertexts: 256 pair workgroups fill the 256 CUs; below, sf2's one-ciphertext
+        // workgroups spread over twice the CUs)
+        if (P.digits == 2 && kn.sf2p && B >= 512) {
             const size_t ldsp = (size_t)8 * G3_N * 8 + 2 * rot_exponent_bytes(P.n);
             if (ldsp <= 160 * 1024) {
                 auto kern = k_blind_rotate_sf2p<2>;
