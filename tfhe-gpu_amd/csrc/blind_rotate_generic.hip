@@ -709,14 +709,17 @@ __device__ __forceinline__ uint64_t tw1(const SfTwB& T, uint32_t i) {
 // T[64 + j] = psi^j as (W0, W1) pairs, built from mono = psi^k - 1 at kernel start, and
 //     A0 (psi^e0 - 1) + A1 (psi^e1 - 1) = sf(sf(A0, T[e0 >> 6]), T[64 + (e0 & 63)]) + (the same for A1)
 //                                       + (10Q - fold(A0 + A1))
+// The low table's row is swizzled: a wave's exponents share their low four bits (sf_mrow below), so
+// unswizzled its lanes hit 2-4 rows in one 16-byte bank group; bits 4-5 XOR-ed into 0-1 spread them.
 constexpr uint32_t SF_MT = 256;  // u64 words of the two tables
+__device__ __forceinline__ uint32_t sf_lrow(uint32_t x) { return 64 + (x ^ ((x >> 4) & 3)); }
 __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __restrict__ mono,
                                                const uint64_t* __restrict__ mono1, uint64_t Q) {
     for (uint32_t k = threadIdx.x; k < 128; k += blockDim.x) {
-        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        const uint32_t e = k < 64 ? 64 * k : k - 64, row = k < 64 ? k : sf_lrow(e);
         const uint64_t w0 = mono[e] + 1, w1 = mono1[e] + (1ull << 32);  // psi^e, psi^e 2^32
-        T[2 * k] = w0 >= Q ? w0 - Q : w0;
-        T[2 * k + 1] = w1 >= Q ? w1 - Q : w1;
+        T[2 * row] = w0 >= Q ? w0 - Q : w0;
+        T[2 * row + 1] = w1 >= Q ? w1 - Q : w1;
     }
 }
 // both keys' factors of one column: A0 (psi^e0 - 1) + A1 (psi^e1 - 1), the two offsets merged into one
@@ -724,9 +727,9 @@ __device__ __forceinline__ void sf_mono_tables(uint64_t* T, const uint64_t* __re
 __device__ __forceinline__ uint64_t sf_mono_pair(uint64_t A0, uint32_t e0, uint64_t A1, uint32_t e1, const uint64_t* T,
                                                  const SfC& K) {
     const uint64_t* h0 = T + 2 * (e0 >> 6);
-    const uint64_t* l0 = T + 2 * (64 + (e0 & 63));
+    const uint64_t* l0 = T + 2 * sf_lrow(e0 & 63);
     const uint64_t* h1 = T + 2 * (e1 >> 6);
-    const uint64_t* l1 = T + 2 * (64 + (e1 & 63));
+    const uint64_t* l1 = T + 2 * sf_lrow(e1 & 63);
     const uint64_t p0 = sf_mul(sf_mul(A0, h0[0], h0[1], K.c2), l0[0], l0[1], K.c2);
     const uint64_t p1 = sf_mul(sf_mul(A1, h1[0], h1[1], K.c2), l1[0], l1[1], K.c2);
     return sf_fold(p0 + p1 + (K.Q10 - sf_fold(A0 + A1, K.c)), K.c);
@@ -1262,6 +1265,12 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
 // inverse ones) to make room: per workgroup 2 x (32 KiB polynomial buffer + the exponents) + 64 KiB.
 // Threads 512 h .. 512 h + 511 run ciphertext 2 b + h with sf2's code (the transform helpers take the
 // thread's index within its ciphertext); every barrier is reached by both halves in the same order.
+// Row of factor e in the shared table.  A wave's 64 lanes look up e = (2 br(slot) + 1) a' mod 2N with
+// slots 4 lane + s: br(slot) keeps its low three bits (the wave's), so every lane's e has the same
+// low four bits -- one 16-byte bank group, a 64-way conflict with rows stored in order (25 % of the
+// kernel's cycles, profiles/r04p).  XOR-ing bits 4-7 and 8-11 into the low four spreads them.
+__device__ __forceinline__ uint32_t sf_mrow(uint32_t e) { return e ^ (((e >> 4) ^ (e >> 8)) & 15); }
+
 template <int DIG>
 __global__ void __launch_bounds__(2 * G3_TH, 4)
 k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
@@ -1282,8 +1291,8 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
     const uint32_t sh = 64 - logG;
     for (uint32_t k = threadIdx.x; k < twoN; k += 2 * TH) {
-        mtab[2 * k] = mono[k] % Q;  // psi^k - 1
-        mtab[2 * k + 1] = mono1[k];
+        mtab[2 * sf_mrow(k)] = mono[k] % Q;  // psi^k - 1
+        mtab[2 * sf_mrow(k) + 1] = mono1[k];
     }
     const SfTwB TF{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(psi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(psi1), 0, (int)(N * 8), 0x00020000)};
@@ -1385,8 +1394,8 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
                 if constexpr (!IP_ONCE) slot_exponents();
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {  // one table product per factor (row e holds psi^e - 1)
-                    const uint64_t* fp = mtab + 2 * ip[s];
-                    const uint64_t* fm = mtab + 2 * ((twoN - ip[s]) & (twoN - 1));
+                    const uint64_t* fp = mtab + 2 * sf_mrow(ip[s]);
+                    const uint64_t* fm = mtab + 2 * sf_mrow((twoN - ip[s]) & (twoN - 1));
                     S[j][s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
                 }
                 if constexpr (!LAST_LDS) sf2_inv_unit<SfTwB, true>(buf, j, S[j], TI, K);
