@@ -24,6 +24,9 @@ SETS = {
     "STD128Q_OPT": lambda m: m.params_from_set("STD128Q_OPT"),
     "STD192Q": lambda m: m.params_from_set("STD192Q"),
     "SIGNED_MOD_TEST": lambda m: m.params_from_set("SIGNED_MOD_TEST"),
+    # N = 8192 with u64 keys and dKS = 7: four waves' digit arrays exceed the LDS, so the gather runs
+    # its one-wavefront form (k_mkm<uint64_t, 1>, lwe_kernels.hip)
+    "TOY_N8192": lambda m: m.params_from_logq("TOY", False, 23, 8192, 0, 1),
 }
 
 
