@@ -263,8 +263,9 @@ typedef struct tfhe_knobs {
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
     int32_t duo;          /* two-digit special-form contexts: batches up to this size (default 128, at most 256) run
                              each ciphertext on two workgroups (sf2duo); 0: never */
-    int32_t sf2p;         /* 0: one ciphertext per workgroup in the special-form kernel instead of two (sf2p, whose
-                             shared LDS holds the whole monomial factor table) */
+    int32_t sf2p;         /* two-digit special-form contexts, batches of 512 or more: 1 (default) runs two
+                             ciphertexts per workgroup (sf2p, whose shared LDS holds the whole monomial factor
+                             table); 0: one per workgroup (sf2) */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
 tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);
