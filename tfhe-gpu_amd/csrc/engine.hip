@@ -1142,6 +1142,7 @@ tfhe_status tfhe_params_finish(tfhe_params* p) {
     });
 }
 
+extern "C++" {  // (a C++ return type: no C linkage inside the extern "C" block)
 namespace {
 // RCCL, loaded when a context spans several devices (no link-time dependency for one-GPU use)
 struct RcclApi {
@@ -1288,6 +1289,7 @@ tfhe_status setup_common(tfhe_ctx** out, const tfhe_params* p, const uint64_t* b
     return TFHE_OK;
 }
 }  // namespace
+}  // extern "C++"
 
 tfhe_status tfhe_setup(tfhe_ctx** out, const tfhe_params* p, const uint64_t* bsk_coeff, const uint64_t* ksk,
                        int num_gpus) {
