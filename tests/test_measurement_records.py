@@ -46,7 +46,7 @@ def test_roofline_fraction_from_records_is_at_most_one():
     assert 0.5 < achieved / peak["modmul_per_s"] <= 1.0
 
 
-# ---- round 4: one record per configuration (profiles/r04_*, profiles/r04k/bench_*.json) ----
+# ---- round 4: one record per configuration (profiles/r04_*, profiles/r04ab/bench_*.json) ----
 R04_CONFIGS = {  # config: (units per launch, n, N, dG2 of the transformed digits, peak family)
     "C2": (8192, 512, 1024, 8, "smont_i32"),
     "C3": (4096, 1305, 2048, 2, "sf_q54"),
@@ -93,7 +93,7 @@ def test_r04_pmc_records_are_consistent():
 def test_r04_bench_lines_reproduce_their_roofline():
     peaks = json.load(open(os.path.join(ROOT, "profiles", "r04_valu_peak.json")))["peaks"]
     for cfg, (units, n, N, dG2, fam) in R04_CONFIGS.items():
-        line = json.load(open(os.path.join(ROOT, "profiles", "r04k", f"bench_{cfg}.json")))
+        line = json.load(open(os.path.join(ROOT, "profiles", "r04ab", f"bench_{cfg}.json")))
         r = line["roofline"]
         assert r["units_per_launch"] == units and r["peak_family"] == fam, cfg
         assert r["alg_modmul_per_unit"] == _alg_modmul(n, N, dG2), cfg
