@@ -265,30 +265,30 @@ def cpu_baseline_reference(name, cfg, p, seconds, gpu_sample, bs_per_unit):
     mod = SIGN_MOD if cfg["op"] == "sign" else p.q
     arrs = {k: np.concatenate([v, rs.integers(0, mod, (K - len(v), width), dtype=np.uint64)]) for k, v in ins.items()}
 
-    def run(nunits, nthreads):
-        with tempfile.TemporaryDirectory() as tmp:
-            files = {}
-            for k, v in arrs.items():
-                files[k] = os.path.join(tmp, k)
-                v[:nunits].tofile(files[k])
-            if cfg["op"] == "func":
-                files["lut"] = os.path.join(tmp, "lut")
-                cube_lut(p.q).tofile(files["lut"])
-            fo = os.path.join(tmp, "out")
-            env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
-            r = subprocess.run([REF_KAT, f"ctx={cfg['ref']}", "keys=synth:1", "api=vector", f"out={fo}"]
-                               + ref_call_args(cfg, p, files), capture_output=True, text=True, env=env, timeout=1800)
-            if r.returncode:
-                raise RuntimeError(r.stderr[-2000:])
-            js = json.loads(r.stdout.strip().splitlines()[-1])
-            return js, np.fromfile(fo, dtype=np.uint64).reshape(nunits, width)
-
-    js, out = run(K, threads)
-    single = None
-    if name == "C2":  # the single-thread figure SURVEY 8(d) asks for (the other contexts' key loads cost minutes)
-        B1 = max(2, int(seconds / 4 / per))
-        js1, _ = run(B1, 1)
-        single = round(B1 * bs_per_unit / js1["best_s"], 3)
+    # one process, one key load: first a 1-thread sample of B1 units (the single-thread figure SURVEY 8(d)
+    # asks for), then all K units on `threads` threads (ref_kat sizes= / threads=); the output is the last run's
+    B1 = min(K, max(2, int(seconds / 4 / per)))
+    with tempfile.TemporaryDirectory() as tmp:
+        files = {}
+        for k, v in arrs.items():
+            files[k] = os.path.join(tmp, k)
+            v[:K].tofile(files[k])
+        if cfg["op"] == "func":
+            files["lut"] = os.path.join(tmp, "lut")
+            cube_lut(p.q).tofile(files["lut"])
+        fo = os.path.join(tmp, "out")
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        r = subprocess.run([REF_KAT, f"ctx={cfg['ref']}", "keys=synth:1", "api=vector", f"out={fo}",
+                            f"sizes={B1},{K}", f"threads=1,{threads}"]
+                           + ref_call_args(cfg, p, files), capture_output=True, text=True, env=env, timeout=1800)
+        if r.returncode:
+            raise RuntimeError(r.stderr[-2000:])
+        js = json.loads(r.stdout.strip().splitlines()[-1])
+        out = np.fromfile(fo, dtype=np.uint64).reshape(K, width)
+    sw1, swK = js["sweep"]
+    assert (sw1["B"], sw1["threads"], swK["B"], swK["threads"]) == (B1, 1, K, threads), js["sweep"]
+    js["best_s"] = swK["best_s"]
+    single = round(B1 * bs_per_unit / sw1["best_s"], 3)
     parity = {"ciphertexts": int(len(gout)), "bit_exact": bool(np.array_equal(out[:len(gout)], gout)),
               "vs": "the reference's OpenFHE CPU path (oracle/_ref/ref_kat), same context, keys and inputs"}
     unit = {"gate": "EvalBinGate(NAND)", "func": "EvalFunc", "sign": "EvalSign"}[cfg["op"]]
@@ -297,8 +297,85 @@ def cpu_baseline_reference(name, cfg, p, seconds, gpu_sample, bs_per_unit):
             "sample": f"{cfg['what']}: the vector API of the reference's OpenFHE (compiled from its sources, "
                       f"oracle/Makefile.ref) with its CPU accumulator / key switch behind the GPU symbols, OpenMP "
                       f"over ciphertexts, {threads} threads: {K} x {unit} ({bs_per_unit} bootstraps each) in "
-                      f"{js['best_s']:.1f} s (key load {js['key_load_s']:.1f} s not counted)",
+                      f"{js['best_s']:.1f} s (key load {js['key_load_s']:.1f} s not counted); single thread: "
+                      f"{B1} units in {sw1['best_s']:.1f} s",
             "gpu_parity": parity}
+
+
+SAMPLE_PER_RANK = {"gate": 8, "func": 2, "sign": 1}   # ciphertexts of every rank's shard checked by the oracle
+
+
+def oracle_params(cfg):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    spec = cfg["ctx"]
+    return pyoracle.params_from_set(spec[1]) if spec[0] == "set" else pyoracle.params_from_logq(spec[1], *spec[2:])
+
+
+def gather_rank_samples(arrs, world, dev):
+    """Every rank's sample arrays (same shape on every rank) in rank order, on every rank."""
+    if world == 1:
+        return [arrs]
+    import torch
+    import torch.distributed as dist
+
+    flat = np.concatenate([a.reshape(-1) for a in arrs]).astype(np.int64)
+    t = torch.from_numpy(flat).to(dev)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    res = []
+    for o in outs:
+        v = o.cpu().numpy().astype(np.uint64)
+        parts, off = [], 0
+        for a in arrs:
+            parts.append(v[off:off + a.size].reshape(a.shape))
+            off += a.size
+        res.append(parts)
+    return res
+
+
+def oracle_sample_check(cfg, bsk, ksk, per_rank, lut=None, threads=0):
+    """The C restatement (oracle/tfhe_oracle.c, the allowed checker) on every rank's sample:
+    per_rank = [[in1, (in2,) out] per rank].  Returns the record the bench line carries."""
+    t0 = time.perf_counter()
+    op = oracle_params(cfg)
+    import pyoracle
+
+    orc = pyoracle.Oracle(op, bsk, ksk, threads=threads)
+    passed = []
+    try:
+        for arrs in per_rank:
+            if cfg["op"] == "gate":
+                ref = orc.eval_bin_gate("NAND", arrs[0], arrs[1])
+            elif cfg["op"] == "func":
+                ref = orc.eval_func(arrs[0], lut)
+            else:
+                ref = orc.eval_sign(arrs[0], SIGN_MOD)
+            passed.append(bool(np.array_equal(ref, arrs[-1])))
+    finally:
+        orc.close()
+    return {"ranks_checked": len(per_rank), "ranks_passed": int(sum(passed)), "per_rank": passed,
+            "ciphertexts_per_rank": int(len(per_rank[0][-1])), "seconds": round(time.perf_counter() - t0, 2),
+            "vs": "oracle/tfhe_oracle.c (C restatement of the reference's CPU path) on the first ciphertexts "
+                  "of every rank's benchmarked shard, same synthetic keys, outside the timed region"}
+
+
+def parity_verdict(cpu, host_array, dropin, oracle):
+    """(ok, failed checks) over every output check the line carries; a check that did not run is not
+    a failure, one that ran and disagreed is."""
+    failed = []
+    if cpu and cpu.get("gpu_parity") and not cpu["gpu_parity"]["bit_exact"]:
+        failed.append("cpu_baseline.gpu_parity")
+    if host_array and not host_array.get("equal_to_device_resident", True):
+        failed.append("host_array.equal_to_device_resident")
+    if dropin and not dropin.get("equal_to_device_resident", True):
+        failed.append("dropin.equal_to_device_resident")
+    if oracle is None:
+        failed.append("oracle_sample (did not run)")
+    elif oracle.get("ranks_passed") != oracle.get("ranks_checked"):
+        failed.append("oracle_sample")
+    return not failed, failed
 
 
 def cpu_baseline_port(p, bsk, ksk, seconds, gpu_sample, reason):
@@ -396,10 +473,7 @@ def main():
     knobs = {k: int(v) for k, v in (x.split("=", 1) for x in args.knob)}
     if rank == 0:
         bsk, ksk = synthetic_keys(p)
-        ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)
-        if args.no_cpu_baseline or name != "C2":
-            del bsk, ksk  # (C3's KSK is 4.8 GB)
-            bsk = ksk = None
+        ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)  # keys kept: the oracle check
     else:
         bsk = ksk = None
     if world > 1:
@@ -605,8 +679,27 @@ def main():
                 if bsk is None:
                     bsk, ksk = synthetic_keys(p)
                 cpu = cpu_baseline_port(p, bsk, ksk, args.cpu_seconds, sample, reason)
-        if cpu and cpu["gpu_parity"] and not cpu["gpu_parity"]["bit_exact"]:
-            print("[bench] ERROR: GPU outputs differ from the CPU reference", file=sys.stderr)
+
+    # ---- every rank's shard: its first ciphertexts against the C restatement (rank 0 checks all) ----
+    ks = min(B, SAMPLE_PER_RANK[cfg["op"]])
+    mine = [h1[:ks]] + ([h2[:ks]] if cfg["op"] == "gate" else []) + [out_h[:ks]]
+    per_rank = gather_rank_samples(mine, world, dev)
+    oracle = None
+    if rank == 0 and not args.params:
+        try:
+            oracle = oracle_sample_check(cfg, bsk, ksk, per_rank,
+                                         lut=cube_lut(int(p.q)) if cfg["op"] == "func" else None,
+                                         threads=host_threads()[0])
+        except Exception as e:
+            print(f"[bench] oracle sample check failed to run: {e}", file=sys.stderr)
+    elif rank == 0:
+        oracle = {"skipped": "--params: no oracle context for an ad-hoc parameter run", "ranks_checked": 0,
+                  "ranks_passed": 0}
+    parity_ok, failed = parity_verdict(cpu, host_array, dropin, oracle) if rank == 0 else (True, [])
+    if world > 1:  # rank 0's verdict is every rank's exit status
+        parity_ok = tdist.max_over_ranks(0.0 if parity_ok else 1.0, dev) == 0.0
+    if rank == 0 and not parity_ok:
+        print(f"[bench] ERROR: output checks failed: {', '.join(failed)}", file=sys.stderr)
 
     if rank == 0:
         line = {
@@ -625,6 +718,7 @@ def main():
                      "world_size": dist.get_world_size() if world > 1 else 1,
                      "kernel_ms_max": round(max(rank_ms), 3), "kernel_ms_min": round(min(rank_ms), 3),
                      "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2)},
+            "parity_ok": parity_ok, "parity_failed": failed, "oracle_sample": oracle,
             "roofline": roofline, "valu": valu, "host_array": host_array, "dropin": dropin, "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2), "key_broadcast_ms": None if bcast_ms is None else round(bcast_ms, 2),
             "key_image_bytes": int(info.key_image_bytes),
@@ -635,7 +729,8 @@ def main():
     ctx.GPUClean()
     if world > 1:
         dist.destroy_process_group()
+    return 0 if parity_ok else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -107,8 +107,10 @@ typedef struct tfhe_info {
     int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
     int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
     double replicate_ms;       /* wall time of that replication (0 for one device) */
-    uint32_t duo_timeouts;     /* two-workgroup blind rotations whose partner never arrived (reads the
-                                  devices' error words: synchronises them); 0 in every correct run */
+    uint32_t duo_timeouts;     /* workgroups of the two-workgroup form (sf2duo) that timed out waiting for
+                                  their partner since setup, summed over devices (synchronises them); the
+                                  ciphertexts of such a pair are recomputed by the one-workgroup kernel
+                                  from their saved inputs in the same launch, so outputs stay exact */
 } tfhe_info;
 
 /* tfhe_info.replicate_method */
@@ -246,8 +248,12 @@ tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, siz
 /* ---- launch knobs (no reference counterpart): the kernel-form choices earlier rounds measured A/B.
  * Read from the environment once, when a context is set up (TFHE_KS_TILED_MIN, TFHE_KS_CTS,
  * TFHE_KS_SPLIT, TFHE_KS_PK, TFHE_HOST_PARTS, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2,
- * TFHE_GENERIC, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no launch reads the
- * environment.  Every setting computes the same outputs (each is a parity-tested cross-check). ---- */
+ * TFHE_GENERIC, TFHE_DUO, TFHE_SF2P, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no
+ * launch reads the environment.  Every setting computes the same outputs (each is a parity-tested
+ * cross-check).  A variable that is not a whole number, or a value out of the field's range, fails
+ * the setup with TFHE_ERR_INVALID_ARGUMENT (tfhe_set_knobs checks the same ranges).  tfhe_set_knobs
+ * must not run while another call on the same context is in flight (the calls read the knobs
+ * without a lock, as OpenFHE's BinFHEContext is not safe to reconfigure mid-call either). ---- */
 typedef struct tfhe_knobs {
     int32_t ks_tiled_min; /* smallest batch on the batch-tiled key switch; -1: the default (1); 0: never */
     int32_t ks_cts;       /* ciphertexts per thread in the tiled key switch: 0 (by key width / batch), 1, 2 */

@@ -17,7 +17,8 @@
 //   keys=valid:<seed>  the C oracle's deterministic valid keys (or_keygen), same load path
 //   op=params | lut_cube | kat | bskeval | acc | mkm | <gate> | func | funcvec | floor | sign | decomp |
 //      mulmatrix (CiphertextMulMatrix, binfhecontext.cpp:319-321: in = ciphertexts mod `mod`, matrix =
-//      int64 [K][cols] file, cols=<cols>, modulus=<m>)
+//      int64 [K][cols] file, cols=<cols>, modulus=<m>; impl=cpugemm: the reference's own CPU function
+//      CPUGEMM, examples/GEMM.cpp:30-56, compiled from that file (its main renamed) instead)
 //   api=vector (default; through the 7 boundary symbols) | single (CPU single-ciphertext API)
 //   in=<u64 file> in2=<u64 file> lut=<u64 file> acc=<u64 file> mod=<ct modulus> fmod=<m>
 //   roundbits=<r> out=<u64 file> gpus=<numGPUs for GPUSetup> reps=<timed repetitions>
@@ -29,6 +30,13 @@
 #include "rgsw-acc-cggi.h"
 #include "bootstrapping.cuh"
 #include "tfhe_oracle.h"
+
+// the reference's CPU CiphertextMulMatrix check (examples/GEMM.cpp:30-56; Makefile.ref compiles that file
+// with its main renamed)
+std::vector<lbcrypto::LWECiphertext> CPUGEMM(lbcrypto::BinFHEContext cc, std::vector<lbcrypto::LWECiphertext> ct_vec,
+                                             std::vector<std::vector<int64_t>> matrix);
+
+#include <omp.h>
 
 #include <chrono>
 #include <cstdio>
@@ -357,9 +365,15 @@ int main(int argc, char** argv) {
     std::vector<size_t> sizes;
     for (auto& f : split(arg("sizes"), ',')) sizes.push_back(std::stoull(f));
     if (sizes.empty()) sizes.push_back(0);
+    // threads=<T1,T2,...> beside sizes=: the OpenMP threads of each size's runs (the reference's CPU
+    // accumulator parallelises over ciphertexts), e.g. a 1-thread sample and the full one after one key load
+    std::vector<int> nthreads;
+    for (auto& f : split(arg("threads"), ',')) nthreads.push_back(std::stoi(f));
+    if (!nthreads.empty() && nthreads.size() != sizes.size()) die("threads= needs one entry per sizes= entry");
     std::ostringstream sweep;
     for (size_t si = 0; si < sizes.size(); ++si) {
     g_limit = sizes[si];
+    if (!nthreads.empty()) omp_set_num_threads(nthreads[si]);
     best = 1e30, total = 0;
     for (int rep = 0; rep < reps; ++rep) {
         out.clear();
@@ -447,7 +461,10 @@ int main(int argc, char** argv) {
             for (size_t k = 0; k < ct.size(); ++k)
                 for (size_t c = 0; c < cols; ++c) m[k][c] = (int64_t)mw[k * cols + c];
             ts = now_s();
-            auto res = s.cc.CiphertextMulMatrix(ct, m, arg_u64("modulus"));
+            // impl=cpugemm: GEMM.cpp's CPUGEMM, which takes the context's qKS as the modulus
+            if (arg("impl", "") == "cpugemm" && arg_u64("modulus") != s.cc.GetParams()->GetLWEParams()->GetqKS().ConvertToInt())
+                die("impl=cpugemm reduces mod the context's qKS: modulus must equal it");
+            auto res = arg("impl", "") == "cpugemm" ? CPUGEMM(s.cc, ct, m) : s.cc.CiphertextMulMatrix(ct, m, arg_u64("modulus"));
             double dt = now_s() - ts;
             best = std::min(best, dt);
             total += dt;
@@ -533,7 +550,8 @@ int main(int argc, char** argv) {
                 js << ",\"out_mod\":" << res[0]->GetModulus().ConvertToInt();
         }
     }
-    if (g_limit) sweep << (si ? "," : "") << "{\"B\":" << g_limit << ",\"best_s\":" << best << ",\"mean_s\":" << total / reps << "}";
+    if (g_limit) sweep << (si ? "," : "") << "{\"B\":" << g_limit << ",\"best_s\":" << best << ",\"mean_s\":" << total / reps
+                       << ",\"threads\":" << (nthreads.empty() ? 0 : nthreads[si]) << "}";
     }
     if (sizes.size() > 1 || sizes[0]) js << ",\"sweep\":[" << sweep.str() << "]";
     if (api == "vector") s.cc.GPUClean();

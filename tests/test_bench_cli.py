@@ -1,9 +1,13 @@
 """bench.py's launch contract on the CPU: a run whose process count differs from --gpus fails with
 exit status 2 before touching a GPU (the driver's 8-GPU run can then never report a 1-rank number as
 an 8-GPU one), and --help lists the per-configuration options."""
+import json
 import os
 import subprocess
 import sys
+
+import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -33,3 +37,64 @@ def test_help_lists_configurations():
     assert r.returncode == 0
     for opt in ("--config", "--batch", "--knob", "--pmc-json", "--test-lib"):
         assert opt in r.stdout
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+def test_parity_verdict_fails_on_any_disagreeing_check():
+    b = _bench()
+    good_oracle = {"ranks_checked": 2, "ranks_passed": 2}
+    assert b.parity_verdict(None, None, None, good_oracle) == (True, [])
+    cpu_bad = {"gpu_parity": {"bit_exact": False}}
+    assert b.parity_verdict(cpu_bad, None, None, good_oracle) == (False, ["cpu_baseline.gpu_parity"])
+    ha_bad = {"equal_to_device_resident": False}
+    assert b.parity_verdict(None, ha_bad, None, good_oracle)[1] == ["host_array.equal_to_device_resident"]
+    assert b.parity_verdict(None, None, ha_bad, good_oracle)[1] == ["dropin.equal_to_device_resident"]
+    assert b.parity_verdict(None, None, None, {"ranks_checked": 8, "ranks_passed": 7})[1] == ["oracle_sample"]
+    assert b.parity_verdict(None, None, None, None)[0] is False  # a check that did not run is not a pass
+
+
+def test_oracle_sample_check_catches_one_wrong_word(oracle):
+    b = _bench()
+    p = oracle.params_from_set("TOY")
+    rng = oracle.Rng(3)
+    sk, bsk, ksk = oracle.keygen(p, rng)
+    orc = oracle.Oracle(p, bsk, ksk, threads=1)
+    rs = np.random.default_rng(0)
+    ct = rs.integers(0, p.q, (2, p.n + 1), dtype=np.uint64)
+    cfg = {"ctx": ("set", "TOY"), "op": "sign"}
+    out = orc.eval_sign(ct, b.SIGN_MOD)
+    orc.close()
+    bad = out.copy()
+    bad[0, 0] ^= np.uint64(1)
+    rec = b.oracle_sample_check(cfg, bsk, ksk, [[ct, out], [ct, bad]], threads=1)
+    assert rec["ranks_checked"] == 2 and rec["per_rank"] == [True, False]
+
+
+@pytest.mark.gpu
+def test_bench_line_passes_its_own_checks():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--batch", "64", "--steps", "1", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-dropin"], capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["parity_ok"] is True and line["oracle_sample"]["ranks_passed"] == 1
+
+
+@pytest.mark.gpu
+def test_bench_exits_nonzero_on_wrong_outputs():
+    """A fault probe of the test library (probe 3: f64w without its prologue barrier, wrong on every
+    ciphertext, tests/test_gpu_f64w_race.py) makes the benchmarked outputs wrong: the line says so and
+    the process fails."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C5a", "--batch", "8", "--steps",
+                        "1", "--warmup", "1", "--no-cpu-baseline", "--test-lib", "--knob", "probe=3"],
+                       capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    assert r.returncode == 1, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["parity_ok"] is False and "oracle_sample" in line["parity_failed"]

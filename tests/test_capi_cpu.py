@@ -3,6 +3,7 @@ include/tfhe_hip.h declares, its parameter selection agrees with the oracle and
 the reference table, and its host-side number theory self-tests pass.
 No compute call touches a GPU here."""
 import ctypes
+import os
 
 import pytest
 
@@ -175,3 +176,38 @@ def test_knob_abi_mirrors_header(capi):
     body = re.search(r"typedef struct tfhe_knobs \{(.*?)\} tfhe_knobs;", txt, re.S).group(1)
     fields = re.findall(r"int32_t\s+(\w+);", body)
     assert fields == [k for k, _ in capi.capi.Knobs._fields_]
+
+
+@pytest.mark.parametrize("env, why", [({"TFHE_KS_CTS": "5"}, "ks_cts"), ({"TFHE_DUO": "-1"}, "duo"),
+                                      ({"TFHE_F64W": "off"}, "not a whole number"),
+                                      ({"TFHE_GENERIC": "3"}, "generic")])
+def test_environment_knobs_are_validated(env, why):
+    """A launch knob from the environment is range-checked like tfhe_set_knobs: setup fails
+    before any device call, naming the variable."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, 'tfhe-gpu_amd'); import numpy as np, tfhe_amd\n"
+            "from tfhe_amd import capi\n"
+            "p = capi.params_from_set('TOY')\n"
+            "try:\n"
+            "    tfhe_amd.BinFHEContextHIP(p).GPUSetup(np.zeros(p.bsk_words(), np.uint64), np.zeros(p.ksk_words(), np.uint64))\n"
+            "except capi.TfheError as e:\n"
+            "    print('ERR', e)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **env))
+    assert "ERR" in r.stdout and "launch knob from the environment" in r.stdout and why in r.stdout, r.stdout + r.stderr
+
+
+def test_product_library_has_no_duo_probe(capi):
+    """The sf2duo timeout probe (a partner that never arrives) is a test-library instance only."""
+    import re
+    import subprocess
+
+    def duo(path):
+        out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
+        return sorted(set(re.findall(r"k_blind_rotate_sf2duo<(\d+)>", out)))
+
+    assert duo(capi.library_path()) == ["0"]
+    assert duo(capi.capi.TEST_LIB) == ["0", "1"]

@@ -130,3 +130,47 @@ def test_engine_device_split_and_error_propagation():
     with pytest.raises(TfheError, match=r"device 7: injected fault on shard \[7168, 8192\)"):
         device_shards(8192, 8, fail_device=7)
     assert device_shards(30, 3, fail_device=5)[2] == (20, 10)  # no such device: no failure
+
+
+def _bench_check_worker(rank, world, port, outdir, corrupt_rank):
+    """bench.py's per-rank output check: each rank's first outputs (the oracle stands in for its
+    GPU; rank `corrupt_rank` flips one bit) are gathered and rank 0 checks them all."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tfhe-gpu_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import pyoracle
+
+    cfg = {"ctx": ("set", "TOY"), "op": "gate"}
+    p = pyoracle.params_from_set("TOY")
+    rng = pyoracle.Rng(5)
+    sk, bsk, ksk = pyoracle.keygen(p, rng)
+    rs = np.random.default_rng(100 + rank)
+    c1 = rs.integers(0, p.q, (3, p.n + 1), dtype=np.uint64)
+    c2 = rs.integers(0, p.q, (3, p.n + 1), dtype=np.uint64)
+    orc = pyoracle.Oracle(p, bsk, ksk, threads=1)
+    out = orc.eval_bin_gate("NAND", c1, c2)
+    orc.close()
+    if rank == corrupt_rank:
+        out[1, 3] ^= np.uint64(1)
+    per_rank = bench.gather_rank_samples([c1, c2, out], world, torch.device("cpu"))
+    if rank == 0:
+        rec = bench.oracle_sample_check(cfg, bsk, ksk, per_rank, threads=1)
+        ok, failed = bench.parity_verdict(None, None, None, rec)
+        with open(os.path.join(outdir, "check.txt"), "w") as f:
+            f.write(f"{rec['ranks_checked']} {rec['ranks_passed']} {int(ok)} {','.join(failed)}\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt_rank", [-1, 1])
+def test_gloo_world2_bench_rank_sample_check(tmp_path, oracle, corrupt_rank):
+    mp.spawn(_bench_check_worker, args=(2, _free_port(), str(tmp_path), corrupt_rank), nprocs=2, join=True)
+    checked, passed, ok, *failed = open(tmp_path / "check.txt").read().split()
+    assert int(checked) == 2
+    if corrupt_rank < 0:
+        assert int(passed) == 2 and ok == "1" and not failed
+    else:
+        assert int(passed) == 1 and ok == "0" and failed == ["oracle_sample"]

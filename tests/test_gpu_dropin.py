@@ -26,14 +26,14 @@ CASES = ["std128_NAND", "std128_AND", "std128_XOR", "std128_XNOR_FAST", "std128_
          "toy8192_sign"]
 
 
-def run_dropin(c, tmp, extra=()):
+def run_dropin(c, tmp, extra=(), gpus=1, env=None):
     files = refvec.write_inputs(c, DATA["fixtures"], tmp)
-    args = [DROPIN, f"ctx={c['ctx']}", f"keys={c['keys']}", f"op={c['op']}", "api=vector", "gpus=1"]
+    args = [DROPIN, f"ctx={c['ctx']}", f"keys={c['keys']}", f"op={c['op']}", "api=vector", f"gpus={gpus}"]
     args += [f"{k}={v}" for k, v in files.items()]
     if c["mod"] is not None:
         args.append(f"mod={c['mod']}")
     args += [f"{k}={v}" for k, v in c["args"].items()] + list(extra)
-    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
 
@@ -64,3 +64,24 @@ def test_shim_takes_the_test_vector_path():
 @pytest.fixture(autouse=True)
 def _shim_timing(monkeypatch):
     monkeypatch.setenv("TFHE_SHIM_TIMING", "1")
+
+
+STUB = os.path.join(ROOT, "tests", "stub_rccl", "librccl_stub.so")
+
+
+@pytest.mark.skipif(not (os.path.exists(DROPIN) and os.path.exists(STUB)), reason="ref_dropin or the stub RCCL not built")
+@pytest.mark.parametrize("gpus", [2, 3])
+@pytest.mark.parametrize("name", ["std128_NAND_b9", "arb12_func_cube_b7", "c5a_std128q_sign_b7"])
+def test_reference_vector_api_over_several_devices(name, gpus):
+    """The reference's unchanged caller with GPUSetup(numGPUs > 1) (binfhecontext.cpp:349-360 ->
+    bootstrapping.cu:725-764, 1005-1069): the shim's context spans `gpus` logical devices on this one GPU
+    (TFHE_LOGICAL_DEVICES), replicated by the engine's RCCL branch against the stub librccl (a real
+    communicator cannot hold one GPU twice; tests/test_gpu_rccl_stub.py), and the vector calls shard the
+    batch (>= 2 ciphertexts per device) -- the outputs are the reference's own (tests/golden: 9 gates,
+    7 EvalFunc, 7 EvalSign on the C5a context)."""
+    c = refvec.case(name, DATA)
+    assert c["B"] >= 2 * gpus  # every device gets a shard (engine.hip run_shards)
+    with tempfile.TemporaryDirectory() as tmp:
+        js, err = run_dropin(c, tmp, gpus=gpus, env={"TFHE_LOGICAL_DEVICES": str(gpus), "TFHE_RCCL_LIB": STUB})
+    assert js["fnv"] == c["vector"]["fnv"], (name, gpus, js)
+    assert f"[shim] GPUSetup devices={gpus} replicate_method=1" in err, err[-2000:]  # TFHE_REPLICATE_RCCL

@@ -110,3 +110,31 @@ def test_duo_evalsign_shard_decrypts(oracle):
     finally:
         ctx.GPUClean()
         orc.close()
+
+
+def test_duo_partner_timeout_is_recomputed(oracle):
+    """A partner that never arrives: the test library's probe 5 makes member 1 of pair 0 stop
+    publishing at round 2.  Both members time out, the pair's failed word is set, and the rescue launch
+    behind the duo kernel recomputes that ciphertext from its saved input with the one-workgroup kernel:
+    every output stays bit-exact and tfhe_info.duo_timeouts counts the two timed-out workgroups."""
+    import tfhe_amd
+
+    op, cp = _ctx_params(oracle), _ctx_params(tfhe_amd)
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(78))
+    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    try:
+        a, acc = _inputs(op, 9, 400)
+        want = orc.eval_acc(a, 2 * op.N, acc)
+        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+        assert ctx.info().duo_timeouts == 0
+        with ctx.knobs_set(probe=5):
+            got = ctx.EvalAcc(a, 2 * op.N, acc)
+        assert np.array_equal(got, want)
+        assert ctx.info().duo_timeouts == 2
+        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)  # the failed word is cleared per launch
+        assert ctx.info().duo_timeouts == 2
+    finally:
+        ctx.GPUClean()
+        orc.close()

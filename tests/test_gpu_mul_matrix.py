@@ -88,10 +88,11 @@ def test_extreme_entries(arb12, mod):
 
 
 def test_reference_fixtures(arb12):
-    """Against the reference's own CiphertextMulMatrix outputs (tests/golden/ref_vectors.json mm_*, written
-    by tools/gen_golden.py from the reference's FP64 DGEMM + fmod + static_cast<uint64_t> semantics,
-    lwe-operation.cu:79-125, whose numpy restatement refvec.mulmatrix_reference reproduces them bit for
-    bit: tests/test_oracle_ref_vectors.py).
+    """Against the reference's own CPU CiphertextMulMatrix (tests/golden/ref_vectors.json mm_*: outputs of
+    CPUGEMM, examples/GEMM.cpp:30-56, the function the reference's GEMM example checks its GPU result
+    against, compiled from that file by oracle/Makefile.ref and run by tools/gen_golden.py; its FP64 sum
+    + fmod + static_cast<uint64_t> semantics equal lwe-operation.cu:79-125's, and the numpy restatement
+    refvec.mulmatrix_reference reproduces them bit for bit: tests/test_oracle_ref_vectors.py).
       mm_gemm     GEMM.cpp's config (K = 1024, entries [0, 64)): every sum exact -> equal to the fixture.
       mm_negative entries in [-64, 64): the reference's fmod keeps a negative sum's sign and the cast
                   wraps it to 2^64 - |r| (outside [0, qKS)); the kernel returns the residue qKS - |r|.

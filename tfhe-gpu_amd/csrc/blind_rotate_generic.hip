@@ -1091,15 +1091,23 @@ __device__ __forceinline__ void sf2_ntt_inv(uint64_t* buf, uint64_t (&s)[2][4], 
     sf_inv_core<false>(v, 4, 0, T, K);
 }
 
-template <int DIG>
+// RESCUE (two digits; launched behind every sf2duo launch): only the ciphertexts whose duo pair timed
+// out (failed word of the pair set) run, from the pair's saved input (rescue_src); the others exit at once
+template <int DIG, bool RESCUE = false>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                    const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
                    const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
                    const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
-                   const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
+                   const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io,
+                   const uint32_t* __restrict__ rescue_failed = nullptr, const uint64_t* __restrict__ rescue_src = nullptr) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr uint32_t N = G3_N, TH = G3_TH, CN = G3_CN;
+    if constexpr (RESCUE) {
+        if (__hip_atomic_load(const_cast<uint32_t*>(rescue_failed + (size_t)blockIdx.x * 64 + 1), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT) == 0)
+            return;  // uniform: the pair finished
+    }
     uint64_t* buf = reinterpret_cast<uint64_t*>(smem);  // [2][N], swizzled
     const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
     const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
@@ -1122,12 +1130,13 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
     auto lpos = [t](int p, int k) -> uint32_t { return (t >> 8) * N + (t & 255) + 256 * (p * CN + k); };
 
+    const uint64_t* gin = RESCUE ? rescue_src + (size_t)blockIdx.x * twoN : g;
     uint64_t acc[2][CN];  // canonical [0, Q), pass A's layout
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
-            const uint64_t v = g[lpos(p, k)];
+            const uint64_t v = gin[lpos(p, k)];
             acc[p][k] = v >= Q ? v % Q : v;
         }
     __syncthreads();  // forward twiddles in LDS
@@ -1442,12 +1451,19 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
 // 1.1-1.3 us per round with b, b + 8 pairing).  Per workgroup and round: half the forward
 // transforms and half the products of sf2<2>, the same monomial and inverse work.
 // Pairs are blocks b and b + 8 (one XCD under round-robin dispatch; correctness does not depend
-// on it).  Every poll is bounded: a partner that never arrives sets X.err and both leave the
-// round loop (the launcher admits at most 256 pairs, all resident at two workgroups per CU).
+// on it).  Every poll is bounded (the launcher admits at most 256 pairs, all resident at two
+// workgroups per CU, so a partner can only be late behind other work on the CUs): a member that
+// times out sets its pair's failed word, adds one to X.err (a count since setup, tfhe_info.duo_timeouts)
+// and leaves the round loop; its partner then times out too (the flags it waits for never come).  Each
+// member saves its input polynomial first (X.save), and the launcher queues k_blind_rotate_sf2<2, true>
+// right behind, which recomputes exactly the failed pairs' ciphertexts from X.save -- a late partner
+// never returns wrong accumulators.
 struct SfDuo {
     uint64_t* xbuf;   // [pairs][2 members][2 round parities][N]
-    uint32_t* flags;  // [pairs][2] one 128-B line each (32 words), zero at launch
-    uint32_t* err;
+    uint32_t* flags;  // [pairs][2] one 128-B line each (32 words: 0 the round flag, 1 of member 0's the
+                      // pair's failed word), zero at launch
+    uint32_t* err;    // timed-out workgroups since setup
+    uint64_t* save;   // [pairs][2][N]: the input accumulators
 };
 constexpr uint32_t kDuoMaxPairs = 256;
 constexpr uint32_t kDuoMaxPolls = 1u << 24;
@@ -1458,6 +1474,9 @@ __device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
     return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// PROBE 1 (test library only, TFHE_TEST_PROBES; tests/test_gpu_duo.py): member 1 of pair 0 stops publishing
+// at round 2, as a partner that never arrives would, and the polls are bounded 2^14 times, not 2^24
+template <int PROBE = 0>
 __global__ void __launch_bounds__(G3_TH, 4)
 k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                       const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
@@ -1493,9 +1512,11 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     const uint32_t c0 = t & 255;                            // coefficients c0 + 256 k of acc_x
 
     uint64_t acc[8];  // acc_x, canonical [0, Q); both halves hold the same values
+    uint64_t* sv = X.save + (size_t)pair * twoN + x * N;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint64_t v = g[x * N + c0 + 256 * k];
+        if (half == 0) sv[c0 + 256 * k] = v;  // the rescue kernel's input if the pair times out
         acc[k] = v >= Q ? v % Q : v;
     }
     __syncthreads();  // forward twiddles, exponents in LDS
@@ -1577,16 +1598,22 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             for (int k = 0; k < 8; ++k) buf[c0 + 256 * k] = v[k];
         }
         if (t == 0) {
-            __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t polls = 0;
-            while (__hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
-                   ++polls < kDuoMaxPolls)
+            constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kDuoMaxPolls;
+            const bool gone = PROBE == 1 && pair == 0 && x == 1 && i >= 2;
+            if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t polls = gone ? kMaxPolls : 0;
+            while (polls < kMaxPolls &&
+                   __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
+                   ++polls < kMaxPolls)
                 __builtin_amdgcn_s_sleep(1);
-            duo_ok = polls < kDuoMaxPolls;
-            if (polls >= kDuoMaxPolls) __hip_atomic_store(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            duo_ok = polls < kMaxPolls;
+            if (polls >= kMaxPolls) {
+                __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
-        if (!duo_ok) break;  // uniform: the partner never arrived (the launcher reports X.err)
+        if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint64_t s = acc[k] + buf[c0 + 256 * k] + duo_load(theirs + c0 + 256 * k);  // < 37.2 Q
@@ -1713,7 +1740,8 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
     return hipGetLastError();
 }
 
-size_t sf_duo_bytes() { return (size_t)kDuoMaxPairs * (4 * G3_N * 8 + 2 * 128) + 128; }
+// xbuf [pairs][2][2][N] u64, flags [pairs][2][32] u32, err (one 128-B line), save [pairs][2][N] u64
+size_t sf_duo_bytes() { return (size_t)kDuoMaxPairs * (4 * G3_N * 8 + 2 * 128) + 128 + (size_t)kDuoMaxPairs * 2 * G3_N * 8; }
 uint32_t sf_duo_err_offset_words() { return (uint32_t)((size_t)kDuoMaxPairs * 4 * G3_N * 2 + kDuoMaxPairs * 2 * 32); }
 
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
@@ -1735,20 +1763,34 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
                                (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
-                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc);
+                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)nullptr,
+                               (const uint64_t*)nullptr);
         };
         if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
             SfDuo X;
             X.xbuf = (uint64_t*)duo;
             X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * G3_N);
             X.err = X.flags + kDuoMaxPairs * 2 * 32;
+            X.save = (uint64_t*)(X.err + 32);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
-            (void)hipFuncSetAttribute((const void*)k_blind_rotate_sf2duo, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            hipLaunchKernelGGL(k_blind_rotate_sf2duo, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), lds, s, P, K,
+            auto dk = k_blind_rotate_sf2duo<0>;
+#ifdef TFHE_TEST_PROBES
+            if (kn.probe == 5) dk = k_blind_rotate_sf2duo<1>;  // test library only: a partner that never arrives
+#endif
+            (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), lds, s, P, K,
                                (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono,
                                w1 + 2 * P.N, (const uint64_t*)bsk,
                                w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+            // the rescue: one-workgroup sf2 for the ciphertexts of timed-out pairs, from their saved inputs
+            // (every other workgroup reads one word and exits: a few microseconds per launch)
+            auto rk = k_blind_rotate_sf2<2, true>;
+            (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
+                               (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
+                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)X.flags,
+                               (const uint64_t*)X.save);
             return hipGetLastError();
         }
         // two ciphertexts per workgroup, the monomial table in LDS: two digits only (same box, three reps,

@@ -194,11 +194,34 @@ namespace {
 // ---------------------------------------------------------------------------
 // Launch knobs from the environment, once per context (tfhe_setup*): the A/B switches of earlier rounds'
 // measurements.  Afterwards only tfhe_set_knobs changes them; no launch reads the environment.
-Knobs knobs_from_env() {
+// The range every knob must lie in (tfhe_set_knobs and the environment alike); nullptr when valid.
+const char* knob_out_of_range(const Knobs& k) {
+    if (k.ks_tiled_min < -1) return "ks_tiled_min (TFHE_KS_TILED_MIN) < -1";
+    if (k.ks_cts < 0 || k.ks_cts > 2) return "ks_cts (TFHE_KS_CTS) not in 0..2";
+    if (k.ks_split < 1) return "ks_split (TFHE_KS_SPLIT) < 1";
+    if (k.host_parts < 1) return "host_parts (TFHE_HOST_PARTS) < 1";
+    if (k.generic < 0 || k.generic > 2) return "generic (TFHE_GENERIC) not in 0..2";
+    if (k.duo < 0 || k.duo > 256) return "duo (TFHE_DUO) not in 0..256";
+    for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.f64w, k.sf2, k.sf2p, k.trace})
+        if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2, TFHE_SF2P) "
+                                   "not 0 or 1";
+    if (k.probe < 0) return "probe < 0";
+    return nullptr;
+}
+
+// bad: the first variable that is not a whole number, or whose value is out of range
+Knobs knobs_from_env(std::string& bad) {
     Knobs k;
-    auto num = [](const char* name, int32_t& dst) {
+    auto num = [&bad](const char* name, int32_t& dst) {
         const char* e = std::getenv(name);
-        if (e && e[0]) dst = (int32_t)std::atoi(e);
+        if (!e || !e[0]) return;
+        char* end = nullptr;
+        const long v = std::strtol(e, &end, 10);
+        if (*end != '\0' || v < INT32_MIN || v > INT32_MAX) {
+            if (bad.empty()) bad = std::string(name) + "=" + e + " is not a whole number";
+            return;
+        }
+        dst = (int32_t)v;
     };
     num("TFHE_KS_TILED_MIN", k.ks_tiled_min);
     num("TFHE_KS_CTS", k.ks_cts);
@@ -215,12 +238,15 @@ Knobs knobs_from_env() {
     if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
     if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;
     k.trace = std::getenv("TFHE_TRACE") != nullptr;
+    if (const char* why = knob_out_of_range(k); why && bad.empty()) bad = why;
     return k;
 }
 
 tfhe_status init_derived(tfhe_ctx* c) {
     const tfhe_params& p = c->p;
-    c->kn = knobs_from_env();
+    std::string bad;
+    c->kn = knobs_from_env(bad);
+    if (!bad.empty()) return fail(TFHE_ERR_INVALID_ARGUMENT, "launch knob from the environment: " + bad);
     c->word_bits = word_bits_for(p);
     c->ksk_bits = ksk_bits_for(p.qKS);
     c->layout = arena_layout(p, c->word_bits);
@@ -825,7 +851,11 @@ tfhe_status wait_flags(const uint32_t* flags, size_t lo, size_t hi, hipStream_t 
         }
         // a miss: pause (the spinning thread shares its core with the host pool draining other blocks,
         // ADVICE r3), yield every 64 misses, check the stream every 1024
+#if defined(__x86_64__) || defined(__i386__)
         __builtin_ia32_pause();
+#elif defined(__aarch64__)
+        __builtin_arm_yield();
+#endif
         if ((polls & 63) == 63) std::this_thread::yield();
         if ((polls & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(cs);
@@ -1472,9 +1502,7 @@ tfhe_status tfhe_set_knobs(tfhe_ctx* c, const tfhe_knobs* in) {
         if (!in) return fail(TFHE_ERR_INVALID_ARGUMENT, "null knobs");
         Knobs k;
         std::memcpy(&k, in, sizeof(Knobs));
-        if (k.generic < 0 || k.generic > 2 || k.ks_cts < 0 || k.ks_cts > 2 || k.ks_split < 1 || k.host_parts < 1 ||
-            k.duo < 0 || k.duo > 256)
-            return fail(TFHE_ERR_INVALID_ARGUMENT, "knob out of range");
+        if (const char* why = knob_out_of_range(k)) return fail(TFHE_ERR_INVALID_ARGUMENT, std::string("knob out of range: ") + why);
         if (k.probe != 0 && !f64_test_probes_compiled())
             return fail(TFHE_ERR_UNSUPPORTED, "probe builds exist only in the test library (libtfhe_hip_test.so)");
         c->kn = k;

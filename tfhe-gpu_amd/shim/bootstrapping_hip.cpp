@@ -198,6 +198,12 @@ void GPUFFTBootstrap::GPUSetup(const std::shared_ptr<BinFHECryptoParams> params,
     check(tfhe_setup_eval(&g_ctx, &p, bsk.data(), ksk.data(), numGPUs), "tfhe_setup_eval");
     g_n = p.n;
     tm.lap("tfhe_setup_eval", 0);
+    if (tm.on) {  // which devices and replication GPUSetup(numGPUs) ended with (tests/test_gpu_dropin.py)
+        tfhe_info info{};
+        if (tfhe_get_info(g_ctx, &info) == TFHE_OK)
+            std::fprintf(stderr, "[shim] GPUSetup devices=%d replicate_method=%d\n", info.num_devices,
+                         info.replicate_method);
+    }
 }
 
 void GPUFFTBootstrap::GPUClean() {

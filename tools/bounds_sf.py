@@ -124,29 +124,38 @@ INV_FOLD_PASS = (False, False, True)   # inverse radix-8 passes C, B: fold the l
 INV_FOLD_LAST = (False, False, False)  # pass A: none (the accumulator update folds)
 
 
-def model(rows, sf2=True):
+def model(rows, sf2=True, form="sf2"):
+    """form: "sf2" / gen3sf (two-level LDS factor tables), "sf2p" (one product per factor with a row of
+    the 2N-entry table, no offset: S = fold(sf(A0, F+) + sf(A1, F-))), "duo" (sf2duo: a member sums its own
+    polynomial's rows only -- `rows` digits x 1 polynomial -- and its accumulator update adds its own
+    column's inverse output and the partner's: acc + own + partner, one fold, one conditional subtraction)."""
     Q = A.Q
     x = 2 * Q if sf2 else Q     # sf2: digits r + Q, r in [-B/2, B/2); gen3sf: canonical digits
     for _ in range(3):
         x = max(fwd_r8(x))
     D = max(fwd_r4(x))
     R = mulw(D)
-    Ap = rows * 2 * R           # rows digits x 2 polynomials per (key, column)
-    # A0j (X^a' - 1) + A1j (X^-a' - 1) by two LDS table factors per term (sf_mono_pair):
-    # sf(sf(A0, T_hi), T_lo) + sf(sf(A1, T_hi'), T_lo') + (10Q - fold(A0 + A1)), the sum folded
-    if fold(2 * Ap) > 10 * Q:
-        fail("monomial offset 10Q below the folded product sum")
-    S = fold(2 * mulw(mulw(Ap)) + 10 * Q)
+    Ap = rows * (1 if form == "duo" else 2) * R   # rows digits x polynomials per (key, column)
+    if form == "sf2p":
+        S = fold(2 * mulw(Ap))
+    else:
+        # A0j (X^a' - 1) + A1j (X^-a' - 1) by two LDS table factors per term (sf_mono_pair):
+        # sf(sf(A0, T_hi), T_lo) + sf(sf(A1, T_hi'), T_lo') + (10Q - fold(A0 + A1)), the sum folded
+        if fold(2 * Ap) > 10 * Q:
+            fail("monomial offset 10Q below the folded product sum")
+        S = fold(2 * mulw(mulw(Ap)) + 10 * Q)
     x = max(inv_r4(S, INV_FOLD_UNITS))
     x = max(inv_r8(x, INV_FOLD_PASS))
     x = max(inv_r8(x, INV_FOLD_PASS))
     out = max(inv_r8(x, INV_FOLD_LAST))
     print(f"  forward outputs < {D / Q:.1f} Q, products < {R / Q:.3f} Q, sums < {Ap / Q:.2f} Q, "
           f"S < {S / Q:.2f} Q, inverse outputs < {out / Q:.2f} Q")
-    acc = (Q - 1) + out
+    acc = (Q - 1) + (2 * out if form == "duo" else out)
     f = fold(acc)
     if f >= 2 * Q:
         fail("accumulator update needs more than one conditional subtraction")
+    if form == "duo" and acc >= 1 << 64:
+        fail("duo update sum >= 2^64")
     return ok
 
 
@@ -194,12 +203,15 @@ def main():
         exactness(c)
     for c in (77823, (1 << 20) - 1):
         A = Arith(c)
-        for name, digits, sf2 in (("sf2, C3 (one digit per polynomial)", 1, True), ("sf2, C5b (two digits)", 2, True),
-                                  ("sf2, CHES EvalFunc context (three digits)", 3, True),
-                                  ("gen3sf, 3 digits (TOY logQ 23)", 3, False),
-                                  ("gen3sf, 8 digits (the most any context has)", 8, False)):
+        for name, digits, sf2, form in (("sf2, C3 (one digit per polynomial)", 1, True, "sf2"),
+                                        ("sf2, C5b (two digits)", 2, True, "sf2"),
+                                        ("sf2, CHES EvalFunc context (three digits)", 3, True, "sf2"),
+                                        ("sf2p, C5b from 512 ciphertexts (two digits)", 2, True, "sf2p"),
+                                        ("sf2duo, C5b up to 128 ciphertexts (two digits)", 2, True, "duo"),
+                                        ("gen3sf, 3 digits (TOY logQ 23)", 3, False, "sf2"),
+                                        ("gen3sf, 8 digits (the most any context has)", 8, False, "sf2")):
             print(f"c = {c}, {name}")
-            good &= model(digits, sf2)
+            good &= model(digits, sf2, form)
     print("OK" if good and ok else "FAILED")
     return 0 if good and ok else 1
 
