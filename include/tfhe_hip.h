@@ -267,8 +267,9 @@ typedef struct tfhe_knobs {
     int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
     int32_t trace;        /* host-array runner timeline on stderr */
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
-    int32_t duo;          /* two-digit special-form contexts: batches up to this size (default 128, at most 256) run
-                             each ciphertext on two workgroups (sf2duo); 0: never */
+    int32_t duo;          /* two-digit special-form contexts (sf2duo) and STD128Q-class FP64 contexts (f64wduo):
+                             batches up to this size (default 128, at most 256) run each ciphertext on two
+                             workgroups; 0: never */
     int32_t sf2p;         /* two-digit special-form contexts, batches of 512 or more: 1 (default) runs two
                              ciphertexts per workgroup (sf2p, whose shared LDS holds the whole monomial factor
                              table); 0: one per workgroup (sf2) */

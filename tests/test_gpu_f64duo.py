@@ -1,0 +1,134 @@
+"""GPU: the two-workgroup exact-FP64 blind rotation (k_blind_rotate_f64wduo, blind_rotate_f64.hip).
+
+STD128Q-class contexts (C5a: Q = 2^50 - 2^14 + 1, two digits, the top one eliminated with the WRAP
+correction) run batches of at most `tfhe_knobs.duo` (default 128) ciphertexts with each ciphertext's
+round split over two workgroups by NTT half: member h keeps the slots of half h after the first forward
+stage, and the pair exchanges 16 KiB of stage-1 inverse values per round.  Checked through the C-ABI:
+  * EvalAcc bit-exact against the oracle at batches that leave pair groups ragged (1, 7, 9);
+  * accumulators in the WRAP range (centred c in [2^49 - 2^24, Q/2): every round runs the correction
+    digit) against the oracle;
+  * the same outputs as the one-workgroup f64w (duo = 0) at 64 and 128 ciphertexts;
+  * EvalSign at C5's per-GPU shard of an 8-GPU node (1024 / 8 = 128), decrypting with valid keys;
+  * a partner that never arrives (test library, probe 5): the rescue recomputes the pair exactly;
+  * no partner ever timed out in a normal run (tfhe_info.duo_timeouts).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+QIN = 1 << 23
+
+
+@pytest.fixture(scope="module")
+def f64duo(oracle):
+    import tfhe_amd
+
+    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(91))
+    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    assert ctx.info().br_kernel == 3 and ctx.knobs()["duo"] == 128  # f64w with the WRAP fold
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    yield dict(op=op, ctx=ctx, orc=orc)
+    assert ctx.info().duo_timeouts == 0
+    ctx.GPUClean()
+    orc.close()
+
+
+def _inputs(op, B, seed, amod=None):
+    rs = np.random.default_rng(seed)
+    a = rs.integers(0, amod or 2 * op.N, (B, op.n), dtype=np.uint64)
+    acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
+    return a, acc
+
+
+@pytest.mark.parametrize("B", [1, 7, 9])
+def test_f64duo_eval_acc_matches_oracle(f64duo, B):
+    op, ctx, orc = f64duo["op"], f64duo["ctx"], f64duo["orc"]
+    a, acc = _inputs(op, B, 500 + B)
+    out = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(out.reshape(B, -1), orc.eval_acc(a, 2 * op.N, acc).reshape(B, -1))
+
+
+def test_f64duo_wrap_rounds_match_oracle(f64duo):
+    """Accumulators whose centred coefficients sit in the WRAP range: the reference's digits sum to
+    c - 2^50 there, so round 0 (and more) runs the correction digit through the split transform."""
+    op, ctx, orc = f64duo["op"], f64duo["ctx"], f64duo["orc"]
+    rs = np.random.default_rng(77)
+    B = 3
+    a = rs.integers(0, 2 * op.N, (B, op.n), dtype=np.uint64)
+    lo, hi = (1 << 49) - (1 << 24), op.Q // 2
+    acc = rs.integers(lo, hi, (B, 2, op.N), dtype=np.uint64)
+    acc[1, :, ::3] = rs.integers(0, op.Q, (2, (op.N + 2) // 3), dtype=np.uint64)
+    out = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(out, orc.eval_acc(a, 2 * op.N, acc))
+    with ctx.knobs_set(duo=0):
+        assert np.array_equal(out, ctx.EvalAcc(a, 2 * op.N, acc))
+
+
+@pytest.mark.parametrize("B", [64, 128])
+def test_f64duo_equals_one_workgroup_form(f64duo, B):
+    op, ctx = f64duo["op"], f64duo["ctx"]
+    a, acc = _inputs(op, B, 600 + B, amod=1024)
+    two = ctx.EvalAcc(a, 1024, acc)
+    with ctx.knobs_set(duo=0):
+        one = ctx.EvalAcc(a, 1024, acc)
+    assert np.array_equal(two, one)
+    idx = [0, B // 2, B - 1]
+    assert np.array_equal(two[idx], f64duo["orc"].eval_acc(a[idx], 1024, acc[idx]))
+
+
+def test_f64duo_evalsign_shard_decrypts(oracle):
+    """EvalSign (15 chained bootstraps) at C5's per-GPU shard, 128: duo = one-workgroup form = oracle on a
+    sample, and every output decrypts to the sign away from the boundaries."""
+    import tfhe_amd
+
+    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
+    rng = oracle.Rng(33)
+    sk, bsk, ksk = oracle.keygen(op, rng)
+    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    try:
+        p = (op.q // 128 // 2) * (QIN // op.q)
+        rs = np.random.default_rng(10)
+        ms = rs.integers(0, p, 128)
+        ct = np.stack([oracle.encrypt(op, rng, sk, int(m), p, QIN) for m in ms])
+        out = ctx.EvalSign(ct, QIN)
+        with ctx.knobs_set(duo=0):
+            ref = ctx.EvalSign(ct, QIN)
+        assert np.array_equal(out, ref)
+        assert np.array_equal(out[[0, 77]], orc.eval_sign(ct[[0, 77]], QIN))
+        dec = np.array([oracle.decrypt(op, sk, r, 2, op.q) for r in out])
+        dist = np.minimum(np.abs(ms - p // 2), np.minimum(ms, p - ms))
+        bad = np.flatnonzero(dec != (ms >= p // 2))
+        assert np.all(dist[bad] < 64), (bad, ms[bad])
+        assert ctx.info().duo_timeouts == 0
+    finally:
+        ctx.GPUClean()
+        orc.close()
+
+
+def test_f64duo_partner_timeout_is_recomputed(oracle):
+    """Probe 5 (test library): member 1 of pair 0 stops publishing at round 2; both members time out, and
+    the rescue launch (f64w from the saved inputs) returns the exact result; duo_timeouts counts both."""
+    import tfhe_amd
+
+    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(92))
+    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    try:
+        a, acc = _inputs(op, 9, 700)
+        want = orc.eval_acc(a, 2 * op.N, acc)
+        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+        with ctx.knobs_set(probe=5):
+            got = ctx.EvalAcc(a, 2 * op.N, acc)
+        assert np.array_equal(got, want)
+        assert ctx.info().duo_timeouts == 2
+        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+        assert ctx.info().duo_timeouts == 2
+    finally:
+        ctx.GPUClean()
+        orc.close()

@@ -58,3 +58,10 @@ def test_fp64_kernel_bounds():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bounds_f64.py"), "--round2"],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "OVER 2^53" in r.stdout, r.stdout
+
+
+def test_duo_fp64_split_transforms():
+    """k_blind_rotate_f64wduo (blind_rotate_f64.hip): the NTT-half split transforms of the two-workgroup
+    FP64 kernel equal the stage loops, stay wave-local, and are bank-conflict-free (tools/lds_layouts_duo.py)."""
+    out = run_tool("lds_layouts_duo.py")
+    assert "OK" in out and "FAILED" not in out

@@ -713,12 +713,20 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 // inside the prologue's C' transform (between passes B and C), bit 0 omits the barrier after it --
 // together they reproduce the round-0 race of the round-2 kernel; bit 2 (timing only) drops the
 // barrier before each further digit's pass A
-template <bool RED, bool WRAP, int LD, int PROBE = 0>
+// RESCUE (launched behind every f64wduo launch): only the ciphertexts whose duo pair timed out (the pair's
+// failed word, kernels.hpp DuoBuf) run, from their saved inputs; the others exit at once
+template <bool RED, bool WRAP, int LD, int PROBE = 0, bool RESCUE = false>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
-                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
+                    const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io,
+                    const uint32_t* __restrict__ rescue_failed = nullptr, const uint64_t* __restrict__ rescue_src = nullptr) {
     extern __shared__ __align__(16) double lds_d[];
     constexpr uint32_t N = 2048, TH = 512, CN = 4;
+    if constexpr (RESCUE) {
+        if (__hip_atomic_load(const_cast<uint32_t*>(rescue_failed + (size_t)blockIdx.x * 64 + 1), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT) == 0)
+            return;  // uniform: the pair finished
+    }
     double* psi = lds_d;
     double* ipsi = lds_d + N;
     double* buf = lds_d + 2 * N;  // [2][N]
@@ -747,12 +755,13 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     // key words through a buffer resource: uniform round + row offset, 32-bit lane offset
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
 
+    const uint64_t* gin = RESCUE ? rescue_src + (size_t)blockIdx.x * twoN : g;
     double acc[2][CN];  // centred [Qhalf - Q, Qhalf), pass A's layout
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int k = 0; k < CN; ++k) {
-            uint64_t v = g[lpos(p, k)];
+            uint64_t v = gin[lpos(p, k)];
             v = v >= P.Q ? v % P.Q : v;
             acc[p][k] = (double)(v < Qhalf ? (int64_t)v : (int64_t)v - Qs);
         }
@@ -930,6 +939,417 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     }
 }
 
+// ---- f64wduo: f64w's STD128Q round on TWO workgroups per ciphertext ------------------------------
+// For batches too small to fill the chip (BASELINE C5 on an 8-GPU node: 1024 EvalSign = 128 per GPU;
+// f64w runs one 512-thread workgroup per ciphertext, so 128 ciphertexts occupy half the CUs and run at
+// 0.39 of the 1024 rate).  The split is by NTT half, not by polynomial: the negacyclic
+// transform's first stage pairs x and x + N/2, and after it the two halves of the slots are independent
+// rings until the inverse's last stage.  Member h of a pair (blocks b and b + 8, one XCD under
+// round-robin dispatch, as sf2duo) holds the whole accumulator (both polynomials, f64w's pass-A layout)
+// and per round:
+//   * extracts the digit (and the WRAP residual vote) of every coefficient, as f64w;
+//   * forward: stage 0 for its half's outputs only (one product per pair, as a full stage), stages 1-2
+//     on its 4 of the thread's 8 coefficients (one barrier), then stages 3-10 wave-local -- wave w owns
+//     256-block w & 3 of half h of polynomial w >> 2, 4 elements per lane, radix-4 passes (3,4) (5,6)
+//     (7,8) (9,10) -- so the lane ends with 4 slots of one polynomial;
+//   * products for column w >> 2 of its half's slots: the lane's own polynomial's digit and C' from
+//     registers, the other polynomial's from LDS (one barrier), 2 keys x 4 rows;
+//   * monomial factors, C' update, inverse stages 10-3 wave-local, stages 2-1 across waves (one barrier);
+//   * hands its 4 stage-1 values per thread (16 KiB) to the partner and takes the partner's (the
+//     sf2duo hand-off: sc1 stores, vmcnt(0), barrier, one flag; bounded poll; sc1 loads), and both
+//     finish inverse stage 0 and the accumulator update for all coefficients (4 products per thread).
+// Per lane and round: 96 FP64 modular products against f64w's 176 (forward 24 / 44, products 32 / 64,
+// monomials 16 / 24, inverse 24 / 44).  The reductions sit after the same stages as f64w's (forward after
+// stage 5, inverse after stages 9 (sums), 6 and 3), so every value obeys f64w's bounds
+// (tools/bounds_f64.py).  A member that times out sets the pair's failed word and the rescue launch
+// (k_blind_rotate_f64w<..., RESCUE>) recomputes that ciphertext from its saved input.
+// Buffer index of element x of a half polynomial (block x >> 8, y = x & 255): y's low five bits are
+// XORed with f(y[7:5]) so that every pass's 64-bit accesses are conflict-free per 32 lanes
+// (tools/lds_layouts_duo.py checks every pass).
+__device__ __forceinline__ uint32_t dswz(uint32_t x) {
+    const uint32_t z = (x >> 5) & 7;
+    return x ^ ((((z >> 1) & 1) << 4) | ((z & 3) << 2) | (z & 3));
+}
+
+// forward: v = coefficients tau + 256k of polynomial t >> 8 (all N) -> d = the NTT values of half h at this
+// lane's slots 4u .. 4u+3, u = 64 (w & 3) + l of half h, polynomial w >> 2 (also left in the buffer)
+template <bool RED>
+__device__ __forceinline__ void f64d_fwd(double* bf, const double (&v)[8], double (&d)[4], uint32_t h,
+                                         const double* psi, const F64Const& K) {
+    constexpr uint32_t H = 1024;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    {
+        const uint32_t tau = f64_tau();
+        double* p = bf + (t >> 8) * H + dswz(tau);
+        const double w0 = psi[1];
+        double o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // stage 0, this half's outputs
+            const double x = fmodmul(v[k + 4], w0, K);
+            o[k] = h ? __dsub_rn(v[k], x) : __dadd_rn(v[k], x);
+        }
+        const double w1 = psi[2 + h];
+        ct_bf(o[0], o[2], w1, K), ct_bf(o[1], o[3], w1, K);
+        ct_bf(o[0], o[1], psi[4 + 2 * h], K), ct_bf(o[2], o[3], psi[5 + 2 * h], K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[256 * k] = o[k];
+    }
+    __syncthreads();
+    const uint32_t B = 4 * h + (w & 3);  // 256-block of the whole polynomial
+    double* q = bf + (w >> 2) * H + 256 * (w & 3);
+    double x[4];
+    {  // stages 3, 4
+        uint32_t y = l;
+        asm volatile("" : "+v"(y));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
+        const double w3 = psi[8 + B];
+        ct_bf(x[0], x[2], w3, K), ct_bf(x[1], x[3], w3, K);
+        ct_bf(x[0], x[1], psi[16 + 2 * B], K), ct_bf(x[2], x[3], psi[17 + 2 * B], K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 5, 6 (RED: the one reduction, after stage 5, as f64w)
+        const uint32_t c = l >> 4, y = 64 * c + (l & 15);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
+        const double w5 = psi[32 + 4 * B + c];
+        ct_bf(x[0], x[2], w5, K), ct_bf(x[1], x[3], w5, K);
+        if constexpr (RED) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = fred(x[k], K);
+        }
+        ct_bf(x[0], x[1], psi[64 + 8 * B + 2 * c], K), ct_bf(x[2], x[3], psi[65 + 8 * B + 2 * c], K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 7, 8
+        const uint32_t c = l >> 2, y = 16 * c + (l & 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
+        const double w7 = psi[128 + 16 * B + c];
+        ct_bf(x[0], x[2], w7, K), ct_bf(x[1], x[3], w7, K);
+        ct_bf(x[0], x[1], psi[256 + 32 * B + 2 * c], K), ct_bf(x[2], x[3], psi[257 + 32 * B + 2 * c], K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 9, 10: slots 4u .. 4u+3 (f64w's units with u = 64 B + l)
+        const uint32_t y = 4 * l;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + k)];
+        const double w9 = psi[512 + 64 * B + l];
+        ct_bf(x[0], x[2], w9, K), ct_bf(x[1], x[3], w9, K);
+        const double2 w10 = *(const double2*)(psi + 1024 + 128 * B + 2 * l);
+        ct_bf(x[0], x[1], w10.x, K), ct_bf(x[2], x[3], w10.y, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = x[k];
+    }
+}
+
+// inverse: s = column w >> 2's NTT-domain increment at the lane's slots -> after stages 10..1 (wave-local,
+// then one barrier and stages 2-1 across waves) o = elements tau + 256k' (k' < 4) of half h of column t >> 8
+template <bool RED>
+__device__ __forceinline__ void f64d_inv(double* bi, const double (&s)[4], double (&o)[4], uint32_t h,
+                                         const double* ipsi, const F64Const& K) {
+    constexpr uint32_t H = 1024;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t B = 4 * h + (w & 3);
+    double* q = bi + (w >> 2) * H + 256 * (w & 3);
+    double x[4] = {s[0], s[1], s[2], s[3]};
+    {  // stages 10, 9 (RED: the sums, as f64w's units)
+        const uint32_t y = 4 * l;
+        const double2 w10 = *(const double2*)(ipsi + 1024 + 128 * B + 2 * l);
+        gs_bf(x[0], x[1], w10.x, K), gs_bf(x[2], x[3], w10.y, K);
+        const double w9 = ipsi[512 + 64 * B + l];
+        gs_bf(x[0], x[2], w9, K), gs_bf(x[1], x[3], w9, K);
+        if constexpr (RED) x[0] = fred(x[0], K), x[1] = fred(x[1], K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 8, 7
+        const uint32_t c = l >> 2, y = 16 * c + (l & 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
+        gs_bf(x[0], x[1], ipsi[256 + 32 * B + 2 * c], K), gs_bf(x[2], x[3], ipsi[257 + 32 * B + 2 * c], K);
+        const double w7 = ipsi[128 + 16 * B + c];
+        gs_bf(x[0], x[2], w7, K), gs_bf(x[1], x[3], w7, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 6, 5 (RED: every output of stage 6, as the end of f64w's pass C)
+        const uint32_t c = l >> 4, y = 64 * c + (l & 15);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
+        gs_bf(x[0], x[1], ipsi[64 + 8 * B + 2 * c], K), gs_bf(x[2], x[3], ipsi[65 + 8 * B + 2 * c], K);
+        if constexpr (RED) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = fred(x[k], K);
+        }
+        const double w5 = ipsi[32 + 4 * B + c];
+        gs_bf(x[0], x[2], w5, K), gs_bf(x[1], x[3], w5, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
+    }
+    f64w_sync();
+    {  // stages 4, 3 (RED: every output, as the end of f64w's pass B)
+        uint32_t y = l;
+        asm volatile("" : "+v"(y));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
+        gs_bf(x[0], x[1], ipsi[16 + 2 * B], K), gs_bf(x[2], x[3], ipsi[17 + 2 * B], K);
+        const double w3 = ipsi[8 + B];
+        gs_bf(x[0], x[2], w3, K), gs_bf(x[1], x[3], w3, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = RED ? fred(x[k], K) : x[k];
+    }
+    __syncthreads();
+    {  // stages 2, 1 of half h (no reduction, as f64w's pass A)
+        const uint32_t tau = f64_tau();
+        const double* p = bi + (t >> 8) * H + dswz(tau);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = p[256 * k];
+        gs_bf(o[0], o[1], ipsi[4 + 2 * h], K), gs_bf(o[2], o[3], ipsi[5 + 2 * h], K);
+        const double w1 = ipsi[2 + h];
+        gs_bf(o[0], o[2], w1, K), gs_bf(o[1], o[3], w1, K);
+    }
+}
+
+__device__ __forceinline__ void duo_store_d(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double duo_load_d(const double* p) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<double*>(p)),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
+
+// STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
+// (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
+// PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a
+// partner that never arrives would, and the polls are bounded 2^14 times
+template <int PROBE = 0>
+__global__ void __launch_bounds__(512, 2)
+k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, const uint64_t* __restrict__ a,
+                       uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X, uint32_t pairs) {
+    extern __shared__ __align__(16) double lds_d[];
+    constexpr uint32_t N = 2048, H = 1024, TH = 512;
+    const uint32_t b = blockIdx.x, pair = (b >> 4) * 8 + (b & 7), h = (b >> 3) & 1;
+    if (pair >= pairs) return;  // both members of a pair take this branch together
+    double* psi = lds_d;
+    double* ipsi = lds_d + N;
+    double* bf = lds_d + 2 * N;  // forward buffer [2][H]
+    double* bi = bf + 2 * H;     // inverse buffer [2][H]
+    double* cx = bi + 2 * H;     // this round's C' (+ the WRAP correction) [2][H], slot positions
+    double* mt = cx + 2 * H;     // monomial tables
+    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n]
+    __shared__ int wflag[2];
+    __shared__ uint32_t duo_ok;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6, twoN = 2 * N, logG = P.logG;
+    const uint32_t j = w >> 2;                                // this wave's polynomial / column
+    const uint32_t u4 = 4 * (256 * h + 64 * (w & 3) + l);     // this lane's slots u4 .. u4+3 (whole ring)
+    const uint32_t sp = j * H + 256 * (w & 3);                // their buffer block
+    for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
+    const double* mono = tabs + twoN;
+    for (uint32_t k = t; k < 128; k += TH) {
+        const uint32_t e = k < 64 ? 64 * k : k - 64;
+        const double v = __dadd_rn(mono[e], 1.0);
+        mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
+    }
+    const double* bsk = tabs + 2 * twoN;
+    const uint64_t Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const double Qlo = (double)(int64_t)(Qhalf - P.Q), Qhi = (double)Qhalf;
+    const double Bg = (double)(1ull << logG), Bginv = 1.0 / Bg;
+    uint64_t* g = acc_io + (size_t)pair * twoN;
+    const uint64_t* ap = a + (size_t)pair * P.n;
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(bsk), 0, -1, 0x00020000);
+    const uint32_t tau = t & 255, pp = t >> 8;  // pass-A role: coefficients tau + 256k of polynomial pp
+
+    double acc[8];  // centred, all N coefficients: tau + 256k of polynomial pp (both members)
+    uint64_t* sv = X.save + (size_t)pair * twoN;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        uint64_t v = g[pp * N + tau + 256 * k];
+        if (pp == h) sv[pp * N + tau + 256 * k] = v;  // the rescue's input if the pair times out
+        v = v >= P.Q ? v % P.Q : v;
+        acc[k] = (double)(v < Qhalf ? (int64_t)v : (int64_t)v - Qs);
+    }
+    if (t < 2) wflag[t] = 0;
+    stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
+    __syncthreads();
+    double Cn[4];  // N^-1 NTT(acc_j) at the lane's slots
+    {
+        double d[4];
+        f64d_fwd<true>(bf, acc, d, h, psi, K);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) Cn[s] = fmodmul(d[s], K.Ninv, K);
+    }
+    __syncthreads();  // the prologue's wave-local passes vs round 0's pass A (f64w's round-2 race)
+    double sl[2], kl[2];  // digit 0 and the WRAP residual (f64w<..., LD = 1>)
+    {
+        const uint32_t shift = P.digits * logG;
+        int64_t Kx = Bh;
+        for (uint32_t z = 1; z < P.digits; ++z) Kx = (Kx << logG) + Bh;
+        sl[0] = 1.0, kl[0] = 0.0;
+        sl[1] = __builtin_ldexp(1.0, -(int)shift);
+        kl[1] = __dmul_rn((double)Kx, sl[1]);
+    }
+    uint32_t* myflag = X.flags + (pair * 2 + h) * 32;
+    const uint32_t* peerflag = X.flags + (pair * 2 + (1 - h)) * 32;
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint32_t ai = ex[i];
+        const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
+        double D[4], dum[4];
+        auto digit = [&](bool corr, double (&d)[4]) {
+            double v[8];
+            bool wv = false;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double c = acc[k];
+                const double res = __builtin_floor(__fma_rn(c, sl[1], kl[1]));
+                if (corr) {
+                    v[k] = __dmul_rn(res, -K.wfac);
+                } else {
+                    v[k] = __fma_rn(-Bg, __builtin_floor(__fma_rn(c, Bginv, 0.5)), c);
+                    wv |= res != 0.0;
+                }
+            }
+            if (!corr) {
+                if (t == 0) wflag[(i + 1) & 1] = 0;
+                if (wv) wflag[i & 1] = 1;
+            }
+            f64d_fwd<true>(bf, v, d, h, psi, K);
+        };
+        digit(false, D);
+        double Cx[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) Cx[s] = Cn[s];
+        if (wflag[i & 1]) {  // (uniform: published by the forward's barrier; about 2^-14 of rounds)
+            __syncthreads();  // other waves may still read their blocks
+            digit(true, dum);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) Cx[s] = fred(__dadd_rn(Cx[s], dum[s]), K);
+        }
+        // this lane's digit and C' values for the other column's waves
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            bf[sp + dswz(4 * l + s)] = D[s];
+            cx[sp + dswz(4 * l + s)] = Cx[s];
+        }
+        __syncthreads();
+        double Do[4], Co[4];  // the other polynomial's at the same slots
+        const uint32_t so = (1 - j) * H + 256 * (w & 3);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) Do[s] = bf[so + dswz(4 * l + s)], Co[s] = cx[so + dswz(4 * l + s)];
+        // products of column j: group gi = (key kk, row rr): rr 0 own digit, 1 the other's, 2 own C', 3 the other's
+        auto krow = [j](uint32_t rr) -> uint32_t { return rr == 0 ? j : rr == 1 ? 1 - j : rr == 2 ? 2 + j : 3 - j; };
+        auto kload = [&](int gi, double (&kv)[4]) {
+            const uint32_t kk = gi >> 2, r = krow(gi & 3);
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
+            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
+            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
+        };
+        double A[2][4], kv[2][4];
+        kload(0, kv[0]);
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) {
+            if (gi + 1 < 8) kload(gi + 1, kv[(gi + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int kk = gi >> 2, rr = gi & 3;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const double dv = rr == 0 ? D[s] : rr == 1 ? Do[s] : rr == 2 ? Cx[s] : Co[s];
+                const double pr = fmodmul(dv, kv[gi & 1][s], K);
+                A[kk][s] = rr == 0 ? pr : __dadd_rn(A[kk][s], pr);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t uo = u4;
+        asm volatile("" : "+v"(uo));
+        double S[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+            const uint32_t in = (twoN - ip) & (twoN - 1);
+            const double Wp = __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
+            const double Wm = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
+            S[s] = fred(__dadd_rn(fmodmul(A[0][s], Wp, K), fmodmul(A[1][s], Wm, K)), K);
+            Cn[s] = fred(__dadd_rn(Cn[s], S[s]), K);
+        }
+        double o[4];
+        f64d_inv<true>(bi, S, o, h, ipsi, K);
+        // hand-off: this half's stage-1 values of both columns to the partner (thread t's 4 at k' 512 + t)
+        double* mine = reinterpret_cast<double*>(X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N);
+        const double* theirs = reinterpret_cast<const double*>(X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's stores drained; every read of the inverse buffer done
+        if (t == 0) {
+            constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kF64DuoMaxPolls;
+            const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
+            if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t polls = gone ? kMaxPolls : 0;
+            while (polls < kMaxPolls &&
+                   __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
+                   ++polls < kMaxPolls)
+                __builtin_amdgcn_s_sleep(1);
+            duo_ok = polls < kMaxPolls;
+            if (polls >= kMaxPolls) {
+                __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
+        double lo[4], hi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double pv = duo_load_d(theirs + 512 * k + t);
+            lo[k] = h ? pv : o[k];
+            hi[k] = h ? o[k] : pv;
+        }
+        const double w0 = ipsi[1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // stage 0 for all coefficients, then f64w's accumulator update
+            const double r[2] = {__dadd_rn(lo[k], hi[k]), fmodmul(__dsub_rn(lo[k], hi[k]), w0, K)};
+#pragma unroll
+            for (int z = 0; z < 2; ++z) {
+                double x = fred(__dadd_rn(acc[k + 4 * z], r[z]), K);
+                x = x >= Qhi ? __dsub_rn(x, K.Q) : x;
+                acc[k + 4 * z] = x < Qlo ? __dadd_rn(x, K.Q) : x;
+            }
+        }
+    }
+    __syncthreads();
+    // member h writes polynomial h (acc0 transposed, poly.cpp:762-770) through the two buffers (N doubles)
+    double* st = bf;
+    if (pp == h) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t c = (int64_t)acc[k];
+            st[tau + 256 * k] = __builtin_bit_cast(double, (uint64_t)(c < 0 ? c + Qs : c));
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {
+        if (h == 0) {
+            const uint64_t v = __builtin_bit_cast(uint64_t, st[k == 0 ? 0 : N - k]);
+            g[k] = k == 0 ? v : (v == 0 ? 0 : P.Q - v);
+        } else {
+            g[N + k] = __builtin_bit_cast(uint64_t, st[k]);
+        }
+    }
+}
+
 // canonical u64 tables / BSK (generic arena) -> centred doubles
 // a * b mod Q for Q < 2^50 in 12-bit steps (one-time packing only)
 __device__ uint64_t mulmod_slow(uint64_t a, uint64_t b, uint64_t Q) {
@@ -1048,9 +1468,13 @@ hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void
     return hipGetLastError();
 }
 
+bool f64_duo_form(const BRParams& P, bool fold) {
+    return f64_path_supported(P, 64) && fold && P.Q >= (1ull << 40) && !fold_exact(P) && P.digits == 2;
+}
+
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold,
                                    const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                   const Knobs& kn) {
+                                   const Knobs& kn, void* duo) {
     if (B == 0) return hipSuccess;
     if (P.N != 2048 || (fold && !fold_possible(P))) return hipErrorInvalidValue;
     F64Const K;
@@ -1069,6 +1493,11 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
                            amod, acc);
     };
+    auto gow = [&](auto kern) {  // f64w (two more kernel arguments: the rescue form's)
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
+                           amod, acc, (const uint32_t*)nullptr, (const uint64_t*)nullptr);
+    };
     const bool red = P.Q >= (1ull << 40);
     const int ld = (int)P.digits - 1;
     // f64w addresses the keys with 32-bit byte offsets (buffer resource)
@@ -1079,16 +1508,35 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
         // round-2 race, wrong results) and a timing-only build (4: STD192 without the barrier before
         // digit 1's pass A, results invalid; tools/f64w_barrier_probe.sh)
-        if (kn.probe != 0) {
-            if (kn.probe == 4 && !red && !wrap && ld == 2) go(k_blind_rotate_f64w<false, false, 2, 4>);
-            else if (kn.probe == 2 && red && wrap && ld == 1) go(k_blind_rotate_f64w<true, true, 1, 2>);
-            else if (kn.probe == 3 && red && wrap && ld == 1) go(k_blind_rotate_f64w<true, true, 1, 3>);
+        if (kn.probe != 0 && kn.probe != 5) {  // (5: the duo timeout probe, below)
+            if (kn.probe == 4 && !red && !wrap && ld == 2) gow(k_blind_rotate_f64w<false, false, 2, 4>);
+            else if (kn.probe == 2 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 2>);
+            else if (kn.probe == 3 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 3>);
             else return hipErrorInvalidValue;
             return hipGetLastError();
         }
 #endif
-        if (red) go(k_blind_rotate_f64w<true, true, 1>);
-        else go(k_blind_rotate_f64w<false, false, 2>);
+        if (red && wrap && ld == 1 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
+            // two workgroups per ciphertext (f64wduo), then the rescue of timed-out pairs
+            const DuoBuf X = duo_layout(duo);
+            if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
+            const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
+            auto dk = k_blind_rotate_f64wduo<0>;
+#ifdef TFHE_TEST_PROBES
+            if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
+#endif
+            (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
+            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
+                               a, amod, acc, X, (uint32_t)B);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+            auto rk = k_blind_rotate_f64w<true, true, 1, 0, true>;
+            (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(512), lds, s, P, K, (const double*)keys, T.eidx, a, amod, acc,
+                               (const uint32_t*)X.flags, (const uint64_t*)X.save);
+            return hipGetLastError();
+        }
+        if (red) gow(k_blind_rotate_f64w<true, true, 1>);
+        else gow(k_blind_rotate_f64w<false, false, 2>);
         return hipGetLastError();
     }
     if (!slot_instance(red, fold, wrap)) return hipErrorNotSupported;

@@ -1458,14 +1458,6 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
 // member saves its input polynomial first (X.save), and the launcher queues k_blind_rotate_sf2<2, true>
 // right behind, which recomputes exactly the failed pairs' ciphertexts from X.save -- a late partner
 // never returns wrong accumulators.
-struct SfDuo {
-    uint64_t* xbuf;   // [pairs][2 members][2 round parities][N]
-    uint32_t* flags;  // [pairs][2] one 128-B line each (32 words: 0 the round flag, 1 of member 0's the
-                      // pair's failed word), zero at launch
-    uint32_t* err;    // timed-out workgroups since setup
-    uint64_t* save;   // [pairs][2][N]: the input accumulators
-};
-constexpr uint32_t kDuoMaxPairs = 256;
 constexpr uint32_t kDuoMaxPolls = 1u << 24;
 __device__ __forceinline__ void duo_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1482,7 +1474,7 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
                       const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
                       const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
                       const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
-                      const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, SfDuo X,
+                      const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X,
                       uint32_t pairs) {
     extern __shared__ __align__(16) unsigned char smem[];
     constexpr uint32_t N = G3_N, TH = G3_TH;
@@ -1740,9 +1732,7 @@ hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk
     return hipGetLastError();
 }
 
-// xbuf [pairs][2][2][N] u64, flags [pairs][2][32] u32, err (one 128-B line), save [pairs][2][N] u64
-size_t sf_duo_bytes() { return (size_t)kDuoMaxPairs * (4 * G3_N * 8 + 2 * 128) + 128 + (size_t)kDuoMaxPairs * 2 * G3_N * 8; }
-uint32_t sf_duo_err_offset_words() { return (uint32_t)((size_t)kDuoMaxPairs * 4 * G3_N * 2 + kDuoMaxPairs * 2 * 32); }
+static_assert(G3_N == kDuoN, "the duo buffer holds N = 2048 polynomials");
 
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
@@ -1767,11 +1757,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)nullptr);
         };
         if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
-            SfDuo X;
-            X.xbuf = (uint64_t*)duo;
-            X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * G3_N);
-            X.err = X.flags + kDuoMaxPairs * 2 * 32;
-            X.save = (uint64_t*)(X.err + 32);
+            const DuoBuf X = duo_layout(duo);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
             auto dk = k_blind_rotate_sf2duo<0>;
 #ifdef TFHE_TEST_PROBES

@@ -121,7 +121,7 @@ struct Device {
     void* bsk_fast = nullptr;
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
     void* keys_sf = nullptr;   // special-form path: W1 = w 2^32 mod Q of the arena's tables and BSK, factor rows
-    void* sf_duo = nullptr;    // two-digit special-form path: exchange buffers of the two-workgroup form
+    void* duo = nullptr;       // exchange buffers of the two-workgroup forms (sf2duo, f64wduo; kernels.hpp DuoBuf)
     Scratch sc;
     DevTables tables{};
     hipStream_t stream2 = nullptr;  // copy stream of the host-array runner
@@ -385,14 +385,18 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
     if (c->use_f64) {
         HCHECK(hipMalloc(&d.keys_f64, bsk_f64_bytes(c->br)));
         HCHECK(launch_pack_bsk_f64(c->br, d.tables, d.arena + c->layout.bsk, c->f64_fold, d.keys_f64, d.stream));
+        if (f64_duo_form(c->br, c->f64_fold)) {
+            HCHECK(hipMalloc(&d.duo, duo_bytes()));
+            HCHECK(hipMemsetAsync(d.duo, 0, duo_bytes(), d.stream));
+        }
         HCHECK(hipStreamSynchronize(d.stream));
     }
     if (c->use_sf) {
         HCHECK(hipMalloc(&d.keys_sf, sf_bytes(c->br)));
         HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
         if (c->br.digits == 2) {
-            HCHECK(hipMalloc(&d.sf_duo, sf_duo_bytes()));
-            HCHECK(hipMemsetAsync(d.sf_duo, 0, sf_duo_bytes(), d.stream));
+            HCHECK(hipMalloc(&d.duo, duo_bytes()));
+            HCHECK(hipMemsetAsync(d.duo, 0, duo_bytes(), d.stream));
         }
         HCHECK(hipStreamSynchronize(d.stream));
     }
@@ -408,7 +412,7 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     hipFree(d.keys_sf);
-    hipFree(d.sf_duo);
+    hipFree(d.duo);
     if (d.stream2) hipStreamSynchronize(d.stream2);
     for (Scratch* sc : {&d.sc, &d.sc2}) {
         hipFree(sc->acc);
@@ -521,10 +525,11 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream,
                                         d.br_done.flags ? &d.br_done : nullptr));
     } else if (c->use_f64) {
-        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream, c->kn));
+        HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream, c->kn,
+                                       d.duo));
     } else if (c->use_sf) {
         HCHECK(launch_blind_rotate_sf(c->br, d.tables, d.arena + L.bsk, d.keys_sf, a, amod, acc, B, d.stream, c->kn,
-                                      d.sf_duo));
+                                      d.duo));
     } else {
         HCHECK(launch_blind_rotate_generic(c->word_bits, c->br, d.tables, d.arena + L.bsk, d.arena + L.bsk_sh, a,
                                            amod, acc, B, d.stream, c->kn));
@@ -1474,11 +1479,11 @@ tfhe_status tfhe_get_info(tfhe_ctx* c, tfhe_info* out) {
         out->replicate_ms = c->replicate_ms;
         out->duo_timeouts = 0;
         for (Device& d : c->devs) {
-            if (!d.sf_duo) continue;
+            if (!d.duo) continue;
             uint32_t e = 0;
             HCHECK(hipSetDevice(d.id));
             HCHECK(hipStreamSynchronize(d.stream));
-            HCHECK(hipMemcpy(&e, (const uint32_t*)d.sf_duo + sf_duo_err_offset_words(), 4, hipMemcpyDeviceToHost));
+            HCHECK(hipMemcpy(&e, (const uint32_t*)d.duo + duo_err_offset_words(), 4, hipMemcpyDeviceToHost));
             out->duo_timeouts += e;
         }
         return TFHE_OK;

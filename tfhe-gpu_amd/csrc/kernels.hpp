@@ -30,7 +30,8 @@ struct Knobs {
     int32_t generic = 0;        // 0: gen3 / v2 by N; 1: v1 (all digits in LDS); 2: v2 also at N = 2048
     int32_t trace = 0;          // host-array runner timeline on stderr
     int32_t probe = 0;          // test library only (TFHE_TEST_PROBES): f64w fault probe / timing builds
-    int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup sf2 form (two digits, <= 256); 0: never
+    int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup forms (sf2duo: two digits;
+                                // f64wduo: STD128Q class; <= 256); 0: never
     int32_t sf2p = 1;           // 0: sf2 with one ciphertext per workgroup instead of two (sf2p) above the duo batches
 };
 
@@ -102,8 +103,12 @@ bool f64_fold_enabled(const BRParams& P);
 bool f64_test_probes_compiled();
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
                                hipStream_t s);
+// duo: the device's duo buffer (STD128Q-class batches up to kn.duo run k_blind_rotate_f64wduo)
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold, const uint64_t* a,
-                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, const Knobs& kn);
+                                   uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, const Knobs& kn,
+                                   void* duo = nullptr);
+// true when the context's FP64 blind rotation has the two-workgroup form (STD128Q class)
+bool f64_duo_form(const BRParams& P, bool fold);
 
 // Special-form u64 blind rotation (gen3sf, blind_rotate_generic.hip) for N = 2048 and
 // Q = 2^54 - c, c < 2^20 (the logQ / arbFunc contexts): constants as (w, w 2^31 mod Q), five
@@ -111,11 +116,36 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
 bool sf_path_supported(const BRParams& P, int word_bits);
 size_t sf_bytes(const BRParams& P);
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
-size_t sf_duo_bytes();  // exchange buffers of the two-workgroup sf2 form (k_blind_rotate_sf2duo)
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
                                   const Knobs& kn, void* duo);
-uint32_t sf_duo_err_offset_words();  // the error word's u32 index in the duo buffer
+
+// Two-workgroup ("duo") blind rotations for batches too small to fill the chip (k_blind_rotate_sf2duo,
+// blind_rotate_generic.hip; k_blind_rotate_f64wduo, blind_rotate_f64.hip): one per-device buffer,
+// allocated at setup for the contexts that have a duo form.
+//   xbuf  [pairs][2 members][2 round parities][2048] u64   the per-round hand-off (16 KiB per member)
+//   flags [pairs][2 members][32] u32                        word 0: the member's round flag; word 1 of
+//                                                           member 0's line: the pair's failed word
+//   err   one 128-B line                                    timed-out workgroups since setup
+//   save  [pairs][2][2048] u64                              the input accumulators (the rescue's input)
+constexpr uint32_t kDuoMaxPairs = 256;
+constexpr uint32_t kDuoN = 2048;
+struct DuoBuf {
+    uint64_t* xbuf;
+    uint32_t* flags;
+    uint32_t* err;
+    uint64_t* save;
+};
+inline DuoBuf duo_layout(void* base) {
+    DuoBuf X;
+    X.xbuf = (uint64_t*)base;
+    X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * kDuoN);
+    X.err = X.flags + kDuoMaxPairs * 2 * 32;
+    X.save = (uint64_t*)(X.err + 32);
+    return X;
+}
+inline size_t duo_bytes() { return (size_t)kDuoMaxPairs * (4 * kDuoN * 8 + 2 * 128) + 128 + (size_t)kDuoMaxPairs * 2 * kDuoN * 8; }
+inline uint32_t duo_err_offset_words() { return (uint32_t)((size_t)kDuoMaxPairs * 4 * kDuoN * 2 + kDuoMaxPairs * 2 * 32); }
 
 // MKM: ModSwitch(Q->qKS), KeySwitch, ModSwitch(qKS->fmod).
 //   ext[B][N+1] mod Q -> out[B][n+1] mod fmod.
