@@ -162,10 +162,14 @@ def test_product_library_has_no_probe_builds(capi):
         out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
         return sorted(set(re.findall(r"k_blind_rotate_f64w<([^>]*)>", out)))
 
+    def probe(inst):  # <RED, WRAP, LD, PROBE, RESCUE>
+        return inst.split(", ")[3]
+
     prod = f64w_instances(capi.library_path())
     test = f64w_instances(capi.capi.TEST_LIB)
-    assert prod and all(i.endswith(", 0") for i in prod), prod
-    assert set(prod) < set(test) and any(not i.endswith(", 0") for i in test), test
+    assert prod and all(probe(i) == "0" for i in prod), prod
+    assert set(prod) < set(test) and any(probe(i) != "0" for i in test), test
+    assert "true, true, 1, 0, true" in prod  # the rescue form behind f64wduo ships
 
 
 def test_knob_abi_mirrors_header(capi):
@@ -200,14 +204,15 @@ def test_environment_knobs_are_validated(env, why):
     assert "ERR" in r.stdout and "launch knob from the environment" in r.stdout and why in r.stdout, r.stdout + r.stderr
 
 
-def test_product_library_has_no_duo_probe(capi):
-    """The sf2duo timeout probe (a partner that never arrives) is a test-library instance only."""
+@pytest.mark.parametrize("kernel", ["k_blind_rotate_sf2duo", "k_blind_rotate_f64wduo"])
+def test_product_library_has_no_duo_probe(capi, kernel):
+    """The duo timeout probes (a partner that never arrives) are test-library instances only."""
     import re
     import subprocess
 
     def duo(path):
         out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
-        return sorted(set(re.findall(r"k_blind_rotate_sf2duo<(\d+)>", out)))
+        return sorted(set(re.findall(kernel + r"<(\d+)>", out)))
 
     assert duo(capi.library_path()) == ["0"]
     assert duo(capi.capi.TEST_LIB) == ["0", "1"]
