@@ -53,11 +53,13 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 6  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
+#define TFHE_HIP_ABI_VERSION 7  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
                                    4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows);
                                    5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs;
                                    6: tfhe_knobs.duo / .sf2p, tfhe_info.duo_timeouts (two-workgroup and
-                                      two-ciphertext sf2 forms) */
+                                      two-ciphertext sf2 forms);
+                                   7: tfhe_knobs.split4 (two-group STD128 form); the duo forms cover
+                                      STD128Q (f64wduo) and timed-out pairs are recomputed */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -248,7 +250,7 @@ tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, siz
 /* ---- launch knobs (no reference counterpart): the kernel-form choices earlier rounds measured A/B.
  * Read from the environment once, when a context is set up (TFHE_KS_TILED_MIN, TFHE_KS_CTS,
  * TFHE_KS_SPLIT, TFHE_KS_PK, TFHE_HOST_PARTS, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2,
- * TFHE_GENERIC, TFHE_DUO, TFHE_SF2P, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no
+ * TFHE_GENERIC, TFHE_DUO, TFHE_SF2P, TFHE_SPLIT4, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no
  * launch reads the environment.  Every setting computes the same outputs (each is a parity-tested
  * cross-check).  A variable that is not a whole number, or a value out of the field's range, fails
  * the setup with TFHE_ERR_INVALID_ARGUMENT (tfhe_set_knobs checks the same ranges).  tfhe_set_knobs
@@ -273,6 +275,8 @@ typedef struct tfhe_knobs {
     int32_t sf2p;         /* two-digit special-form contexts, batches of 512 or more: 1 (default) runs two
                              ciphertexts per workgroup (sf2p, whose shared LDS holds the whole monomial factor
                              table); 0: one per workgroup (sf2) */
+    int32_t split4;       /* STD128-class contexts: batches up to this size (default 512) run each ciphertext's two
+                             polynomials on two groups of four wavefronts (fast4 SPLIT); 0: never */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
 tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);

@@ -141,7 +141,7 @@ hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const voi
 }
 
 hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const void* bsk_fast, const uint64_t* a,
-                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, BRDone* dn) {
+                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, BRDone* dn, int split_max) {
     if (B == 0) return hipSuccess;
     if (amod == 0 || (amod & (amod - 1)) || amod > 2 * FN) return hipErrorNotSupported;
     uint32_t loga = 0;
@@ -163,7 +163,7 @@ hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables&, const v
     K.bm = (uint32_t)((1ull << 32) / Q);
     const int32_t* tabs = (const int32_t*)bsk_fast;
     return launch_blind_rotate_fast4(fast_variant(), fast_shape(P), &K, P.n, loga, tabs, tabs + TB_WORDS, a, acc, B, s,
-                                     dn);
+                                     dn, split_max);
 }
 
 }  // namespace tfhe

@@ -242,7 +242,9 @@ struct LaneCtx {
 #define FOR_P(...)                                   \
     {                                                \
         { constexpr int p = 0; __VA_ARGS__ }         \
-        { constexpr int p = 1; __VA_ARGS__ }         \
+        if constexpr (P > 1) {                       \
+            { constexpr int p = 1; __VA_ARGS__ }     \
+        }                                            \
         if constexpr (P > 2) {                       \
             { constexpr int p = 2; __VA_ARGS__ }     \
             { constexpr int p = 3; __VA_ARGS__ }     \
@@ -352,20 +354,31 @@ __device__ __forceinline__ void ntt_inv(int32_t (&X)[P][4], const int32_t* lds, 
 // XB: cross-exchange areas (2: alternate, no barrier before the stores; 1: one area + a barrier)
 // CTS (NCT = 1): ciphertexts per workgroup, in lockstep through the transforms' barriers, so
 // their wavefronts read each key row at about the same time (L1 reuse instead of L2 traffic).
+// SPLIT (small batches; CHES-experiments.cpp's 256-gate calls): one ciphertext per 512-thread workgroup, its
+// two polynomials on two groups of four wavefronts -- group g runs this kernel's round on accumulator
+// polynomial g alone (digits, forward transforms, C_g, the inverse of column g, the update of acc_g) --
+// and the external product is split by polynomial: group g forms the row sums of its own polynomial's
+// digit / C rows for BOTH columns, reduces them (sredc), and hands the other column's 8 partial sums per
+// lane to the other group through LDS (one barrier); each then finishes column g.  Half of every
+// transform, product and monomial step per wavefront, twice the wavefronts per ciphertext: at 256
+// ciphertexts a CU runs 2 waves per SIMD instead of 1.
 // Digit shape (any N = 1024 set with Q < 2^27 and baseG <= 2^9; tools/bounds_fast4.py): DIG digits
 // per polynomial (dG2 = 2 DIG), baseG = 2^LOGG, THR thrown digits.  FOLD: the top digit is
 // eliminated (its rows carry C = N^-1 NTT(acc), k_pack_fast folds it into the other rows), valid
 // when THR = 0 and the top digit never wraps (the host checks); otherwise every digit is
 // transformed.  Pass 0's lookup tables hold digits in [-64, 64), so they need LOGG <= 7.
 template <int MINW, int NCT = 1, int EXP = 0, int OPT = 7, int XB = 2, int CTS = 1, int DIG = 4, int LOGG = 7,
-          int THR = 0, bool FOLD = true, bool FLAG = false>
-__global__ void __launch_bounds__(TPC * CTS, MINW)
+          int THR = 0, bool FOLD = true, bool FLAG = false, bool SPLIT = false>
+__global__ void __launch_bounds__(TPC * (SPLIT ? 2 : CTS), MINW)
 k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __restrict__ tabs,
                      const int32_t* __restrict__ bsk, const uint64_t* __restrict__ a, uint64_t* __restrict__ acc_io,
                      uint32_t B, uint32_t* __restrict__ done) {
-    constexpr int P = 2 * NCT;
+    constexpr int NPOL = SPLIT ? 1 : 2;   // accumulator polynomials per lane
+    constexpr int P = NPOL * NCT;         // polynomials per transform
+    constexpr int GR = SPLIT ? 2 : CTS;   // 256-thread groups per workgroup
     extern __shared__ __align__(16) int32_t lds[];
     static_assert(CTS == 1 || NCT == 1, "CTS > 1 needs NCT = 1");
+    static_assert(!SPLIT || (NCT == 1 && CTS == 1 && FOLD && !FLAG && XB == 1), "SPLIT: the folded one-ciphertext build");
     constexpr uint32_t RW = 2 * DIG;                  // key rows per (key, column)
     constexpr int TOP = DIG - 1;                       // FOLD: the eliminated digit (its rows: the C products)
     constexpr int NT = FOLD ? DIG - 1 : DIG;           // transformed digits per round
@@ -373,13 +386,14 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     static_assert(LOGG * (THR + NT) <= 32, "digit field beyond 32 bits");
     // XB = 2 alternates cross areas between consecutive transforms: laid out for STD128's order only
     static_assert(XB == 1 || (DIG == 4 && FOLD), "two cross areas need the STD128 digit order");
-    const uint32_t cl = __builtin_amdgcn_readfirstlane(threadIdx.x / TPC);  // ciphertext in the workgroup
+    const uint32_t cl = __builtin_amdgcn_readfirstlane(threadIdx.x / TPC);  // group: ciphertext (SPLIT: polynomial)
     const uint32_t tid = threadIdx.x % TPC;
-    const uint32_t wg_ct = blockIdx.x * CTS * NCT + cl;                     // first ciphertext of this lane
-    for (uint32_t k = threadIdx.x; k < L_TWI; k += TPC * CTS) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
-    for (uint32_t k = threadIdx.x; k < 2 * FN + 640; k += TPC * CTS) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1/T23/T2131
+    const uint32_t wg_ct = SPLIT ? blockIdx.x : blockIdx.x * CTS * NCT + cl;  // first ciphertext of this lane
+    const uint32_t pol = SPLIT ? cl : 0;                                      // SPLIT: this group's polynomial
+    for (uint32_t k = threadIdx.x; k < L_TWI; k += TPC * GR) lds[L_TW + k] = tabs[P1F + k], lds[L_TWI + k] = tabs[P1I + k];
+    for (uint32_t k = threadIdx.x; k < 2 * FN + 640; k += TPC * GR) lds[L_MONO + k] = tabs[T4_MONO + k];  // monomials, T1/T23/T2131
     if constexpr ((OPT & 8) != 0)
-        for (uint32_t k = threadIdx.x; k < 4 * 256; k += TPC * CTS) lds[L_P4F + k] = tabs[P4F + k];
+        for (uint32_t k = threadIdx.x; k < 4 * 256; k += TPC * GR) lds[L_P4F + k] = tabs[P4F + k];
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     constexpr uint32_t LOCW = P * LP, XAW = P * XP;       // local region per wave, cross area (words)
     constexpr uint32_t XA0 = 4 * LOCW, XA1 = XB == 2 ? XA0 + XAW : XA0;  // cross areas, relative to L_CT
@@ -403,16 +417,16 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     for (int k = 0; k < 3; ++k) C.w0f[k] = tabs[P0F + k], C.w0i[k] = tabs[P0I + k];
 
     const uint32_t Qh = (uint32_t)K.Q >> 1;
-    int32_t acc[NCT][2][4];  // L1, centred canonical
+    int32_t acc[NCT][NPOL][4];  // L1, centred canonical
 #pragma unroll
     for (int q = 0; q < NCT; ++q) {
         const uint32_t ct = wg_ct + q;
         const uint64_t* g = acc_io + (size_t)(ct < B ? ct : 0) * 2 * FN;
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < NPOL; ++p)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint64_t v0 = ct < B ? g[p * FN + elem<1>(w, lane, r)] : 0;
+                const uint64_t v0 = ct < B ? g[(SPLIT ? pol : p) * FN + elem<1>(w, lane, r)] : 0;
                 const uint32_t v = (uint32_t)(v0 >= (uint64_t)K.Q ? v0 % (uint64_t)K.Q : v0);
                 acc[q][p][r] = v < Qh ? (int32_t)v : (int32_t)v - K.Q;
             }
@@ -422,10 +436,15 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
     // C = N^-1 NTT(acc) in L5
     int32_t Cp[P][4];
     if constexpr (FOLD) {
+        if constexpr (SPLIT) {
 #pragma unroll
-        for (int q = 0; q < NCT; ++q)
+            for (int r = 0; r < 4; ++r) Cp[0][r] = acc[0][0][r];
+        } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][1][r];
+            for (int q = 0; q < NCT; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Cp[2 * q][r] = acc[q][0][r], Cp[2 * q + 1][r] = acc[q][NPOL - 1][r];
+        }
         ntt_fwd<XA1, P, EXP, 0, PRE, (OPT & 8) != 0>(Cp, lds, C, K);
 #pragma unroll
         for (int p = 0; p < P; ++p)
@@ -447,6 +466,10 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             pw[0] = v4i{(int)round_off, l, gi, 4}, pw[1] = pw[0] + 1;
             return;
         }
+        if constexpr (SPLIT) {  // this group's polynomial's row only
+            pw[0] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l + pol) * 2 + j) * FN * 4);
+            return;
+        }
         pw[0] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l) * 2 + j) * FN * 4);
         pw[1] = ld_bsk(rsrc, voff, round_off + ((k * RW + 2 * l + 1) * 2 + j) * FN * 4);
     };
@@ -459,8 +482,8 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         for (int q = 0; q < NCT; ++q)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                s[q][k][j][r] = first ? (int64_t)X[2 * q][r] * w0[r] : mac64(X[2 * q][r], w0[r], s[q][k][j][r]);
-                s[q][k][j][r] = mac64(X[2 * q + 1][r], w1[r], s[q][k][j][r]);
+                s[q][k][j][r] = first ? (int64_t)X[NPOL * q][r] * w0[r] : mac64(X[NPOL * q][r], w0[r], s[q][k][j][r]);
+                if constexpr (!SPLIT) s[q][k][j][r] = mac64(X[2 * q + 1][r], w1[r], s[q][k][j][r]);
             }
     };
 
@@ -510,13 +533,18 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
             const uint32_t lt = l + THR;
             const int32_t kl = (int32_t)(((1u << (LOGG * lt)) - 1) / ((1u << LOGG) - 1)) << (LOGG - 1);
             int32_t X[P][4];
+            if constexpr (SPLIT) {
 #pragma unroll
-            for (int q = 0; q < NCT; ++q)
+                for (int r = 0; r < 4; ++r) X[0][r] = __builtin_amdgcn_sbfe(acc[0][0][r] + kl, LOGG * lt, LOGG);
+            } else {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    X[2 * q][r] = __builtin_amdgcn_sbfe(acc[q][0][r] + kl, LOGG * lt, LOGG);
-                    X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][1][r] + kl, LOGG * lt, LOGG);
-                }
+                for (int q = 0; q < NCT; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        X[2 * q][r] = __builtin_amdgcn_sbfe(acc[q][0][r] + kl, LOGG * lt, LOGG);
+                        X[2 * q + 1][r] = __builtin_amdgcn_sbfe(acc[q][NPOL - 1][r] + kl, LOGG * lt, LOGG);
+                    }
+            }
             __builtin_amdgcn_sched_barrier(0);
             constexpr int SM = LOGG > 7 ? 0 : (OPT & 4) ? 2 : (OPT & 1) ? 1 : 0;
             if (l & 1) ntt_fwd<XA1, P, EXP, SM, PRE, (OPT & 8) != 0>(X, lds, C, K);
@@ -538,8 +566,35 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         __builtin_amdgcn_sched_barrier(0);
         const char* mono = reinterpret_cast<const char*>(lds + L_MONO);
         int32_t S[P][4];
+        if constexpr (SPLIT) {
+            // partial sums of this polynomial's rows; the other column's go to the other group (LDS word
+            // ((writer group * 2 + key) * 4 + r) * 256 + lane: conflict-free), this column's come back
+            int32_t* xch = lds + L_CT + GR * (4 * P * LP + XB * P * XP);
+            const uint32_t bp = (et * ai[0]) & 2047, bn = (0u - bp) & 2047;
+            const uint32_t F4p = ((bp >> 4) & 0x1C) | ((bp & 63) << 7), F4n = ((bn >> 4) & 0x1C) | ((bn & 63) << 7);
+            const uint32_t hp = (bp >> 4) & 0x60, hn = (bn >> 4) & 0x60;
+            int32_t Am[2][4];
 #pragma unroll
-        for (int q = 0; q < NCT; ++q) {
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    xch[((pol * 2 + k) * 4 + r) * TPC + tid] = sredc(pol ? s[0][k][0][r] : s[0][k][1][r], K);
+                    Am[k][r] = sredc(pol ? s[0][k][1][r] : s[0][k][0][r], K);
+                }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t c = ((r & 1) << 1) | (r >> 1);  // bitrev2(r)
+                const uint32_t cs = c * 32 * ai[0];             // uniform
+                const int32_t mp = *reinterpret_cast<const int32_t*>(mono + ((((hp + cs) & 0x60)) | F4p));
+                const int32_t mn = *reinterpret_cast<const int32_t*>(mono + ((((hn - cs) & 0x60)) | F4n));
+                const int32_t A0 = Am[0][r] + xch[(((1 - pol) * 2 + 0) * 4 + r) * TPC + tid];
+                const int32_t A1 = Am[1][r] + xch[(((1 - pol) * 2 + 1) * 4 + r) * TPC + tid];
+                S[0][r] = sredc((int64_t)A0 * mp + (int64_t)A1 * mn, K);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < (SPLIT ? 0 : NCT); ++q) {
             const uint32_t bp = (et * ai[q]) & 2047, bn = (0u - bp) & 2047;
             const uint32_t F4p = ((bp >> 4) & 0x1C) | ((bp & 63) << 7), F4n = ((bn >> 4) & 0x1C) | ((bn & 63) << 7);
             const uint32_t hp = (bp >> 4) & 0x60, hn = (bn >> 4) & 0x60;
@@ -573,10 +628,10 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
 #pragma unroll
         for (int q = 0; q < NCT; ++q)
 #pragma unroll
-            for (int p = 0; p < 2; ++p)
+            for (int p = 0; p < NPOL; ++p)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    uint32_t u = (uint32_t)(acc[q][p][r] + S[2 * q + p][r]) + K.kacc;  // in (0, 8Q)
+                    uint32_t u = (uint32_t)(acc[q][p][r] + S[NPOL * q + p][r]) + K.kacc;  // in (0, 8Q)
                     if constexpr ((OPT & 2) != 0) {
                         // u - floor(u / Q) Q, off by at most one Q (u < 2^30): one mul_hi + one mad
                         const uint32_t qt = __umulhi(u, K.bm);
@@ -599,9 +654,14 @@ k_blind_rotate_fast4(FastConst K, uint32_t n, uint32_t loga, const int32_t* __re
         for (int r = 0; r < 4; ++r) {
             const uint32_t k = elem<1>(w, lane, r);
             const uint32_t v = (uint32_t)(acc[q][0][r] < 0 ? acc[q][0][r] + K.Q : acc[q][0][r]);
-            const uint32_t v1 = (uint32_t)(acc[q][1][r] < 0 ? acc[q][1][r] + K.Q : acc[q][1][r]);
-            g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
-            g[FN + k] = v1;
+            if constexpr (SPLIT) {
+                if (pol == 0) g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
+                else g[FN + k] = v;
+            } else {
+                const uint32_t v1 = (uint32_t)(acc[q][NPOL - 1][r] < 0 ? acc[q][NPOL - 1][r] + K.Q : acc[q][NPOL - 1][r]);
+                g[(FN - k) & (FN - 1)] = k == 0 ? v : (v == 0 ? 0 : (uint32_t)K.Q - v);
+                g[FN + k] = v1;
+            }
         }
     }
     // FLAG (host-array EvalAcc, engine.hip d2h_flagged): done[4 ct + w] = 1 in pinned host memory once
@@ -678,7 +738,7 @@ hipError_t launch_blind_rotate_fast4_d6(const f4::FastConst& K, uint32_t n, uint
 
 hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
-                                     size_t B, hipStream_t s, BRDone* dn) {
+                                     size_t B, hipStream_t s, BRDone* dn, int split_max) {
     const f4::FastConst Kc = *reinterpret_cast<const f4::FastConst*>(K);
     auto launch = [&](auto kern, int nct, int xb = 2, int cts = 1, uint32_t* done = nullptr) {
         const size_t lb = f4::lds_bytes(2 * nct, xb, cts);
@@ -698,6 +758,15 @@ hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const vo
         return hipGetLastError();
     }
     if (!(sh.dig == 4 && sh.logg == 7 && sh.thr == 0 && sh.fold)) return hipErrorNotSupported;
+    if (variant == 60 && B <= (size_t)split_max && !(dn && dn->flags)) {
+        // small batches: one ciphertext per 512-thread workgroup, its two polynomials on two groups (SPLIT)
+        auto kern = f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 4, 7, 0, true, false, true>;
+        const size_t lb = f4::lds_bytes(1, 1, 2) + (size_t)2 * 8 * f4::TPC * 4;  // + the partial-sum exchange
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(2 * f4::TPC), lb, s, Kc, n, loga, tabs4, bsk, a, acc, (uint32_t)B,
+                           (uint32_t*)nullptr);
+        return hipGetLastError();
+    }
     if (dn && dn->flags && variant == 60) {  // the default build with completion flags (FLAG)
         launch(f4::k_blind_rotate_fast4<4, 1, 0, 7, 1, 1, 4, 7, 0, true, true>, 1, 1, 1, dn->flags);
         dn->written = true;

@@ -202,6 +202,7 @@ const char* knob_out_of_range(const Knobs& k) {
     if (k.host_parts < 1) return "host_parts (TFHE_HOST_PARTS) < 1";
     if (k.generic < 0 || k.generic > 2) return "generic (TFHE_GENERIC) not in 0..2";
     if (k.duo < 0 || k.duo > 256) return "duo (TFHE_DUO) not in 0..256";
+    if (k.split4 < 0) return "split4 (TFHE_SPLIT4) < 0";
     for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.f64w, k.sf2, k.sf2p, k.trace})
         if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2, TFHE_SF2P) "
                                    "not 0 or 1";
@@ -234,6 +235,7 @@ Knobs knobs_from_env(std::string& bad) {
     num("TFHE_SF2", k.sf2);
     num("TFHE_DUO", k.duo);
     num("TFHE_SF2P", k.sf2p);
+    num("TFHE_SPLIT4", k.split4);
     num("TFHE_GENERIC", k.generic);
     if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
     if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;
@@ -523,7 +525,7 @@ tfhe_status dev_blind_rotate(tfhe_ctx* c, Device& d, const uint64_t* a, uint64_t
     const ArenaLayout& L = c->layout;
     if (c->use_fast && (amod & (amod - 1)) == 0) {
         HCHECK(launch_blind_rotate_fast(c->br, d.tables, d.bsk_fast, a, amod, acc, B, d.stream,
-                                        d.br_done.flags ? &d.br_done : nullptr));
+                                        d.br_done.flags ? &d.br_done : nullptr, c->kn.split4));
     } else if (c->use_f64) {
         HCHECK(launch_blind_rotate_f64(c->br, d.tables, d.keys_f64, c->f64_fold, a, amod, acc, B, d.stream, c->kn,
                                        d.duo));

@@ -33,6 +33,7 @@ struct Knobs {
     int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup forms (sf2duo: two digits;
                                 // f64wduo: STD128Q class; <= 256); 0: never
     int32_t sf2p = 1;           // 0: sf2 with one ciphertext per workgroup instead of two (sf2p) above the duo batches
+    int32_t split4 = 512;       // STD128 class: batches up to this size run fast4's two-group form (SPLIT); 0: never
 };
 
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
@@ -65,8 +66,10 @@ hipError_t launch_blind_rotate_generic(int word_bits, const BRParams& P, const D
 // Fast STD128-class blind rotation (W = u32, N = 1024, dG2 = 8): register-resident
 // transforms, one wavefront per ciphertext.  Returns hipErrorNotSupported when the
 // parameters do not match its specialisation.
+// split_max: batches up to this size run the two-group form (k_blind_rotate_fast4 SPLIT; tfhe_knobs.split4)
 hipError_t launch_blind_rotate_fast(const BRParams& P, const DevTables& T, const void* bsk_fast, const uint64_t* a,
-                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, BRDone* dn = nullptr);
+                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, BRDone* dn = nullptr,
+                                    int split_max = 0);
 bool fast_path_supported(const BRParams& P, int word_bits);
 // Converts the generic device BSK and tables into the fast kernel's Montgomery form.
 hipError_t launch_pack_bsk_fast(const BRParams& P, const DevTables& T, const void* bsk, void* bsk_fast,
@@ -87,7 +90,7 @@ size_t fast4_table_words();
 hipError_t launch_pack_tables_fast4(uint32_t Q, const DevTables& T, void* out, hipStream_t s);
 hipError_t launch_blind_rotate_fast4(int variant, const Fast4Shape& sh, const void* K, uint32_t n, uint32_t loga,
                                      const int32_t* tabs4, const int32_t* bsk, const uint64_t* a, uint64_t* acc,
-                                     size_t B, hipStream_t s, BRDone* dn = nullptr);
+                                     size_t B, hipStream_t s, BRDone* dn = nullptr, int split_max = 0);
 
 // Exact-FP64 blind rotation for 2^32 <= Q < 2^50, N = 2048 (STD192 / STD192Q / STD128Q classes):
 // keys/tables as centred doubles derived on device from the generic (u64) arena.

@@ -56,8 +56,9 @@ def inv(b_in):
 
 
 
-def check(dig, logg, fold):
-    """DIG digits of base 2^logg per polynomial; fold = top digit eliminated (C rows)"""
+def check(dig, logg, fold, split=False):
+    """DIG digits of base 2^logg per polynomial; fold = top digit eliminated (C rows); split = the SPLIT
+    form: each group reduces its own polynomial's half of the row sum, and A is the sum of two such"""
     dmax = 1 << (logg - 1)
     F = max(fwd([dmax] * 1024))
     if logg <= 7:  # pass 0 from the lookup tables (digits in [-64, 64))
@@ -66,6 +67,9 @@ def check(dig, logg, fold):
     rowsum = 2 * nt * F * Qh + (2 * F * Qh if fold else 0)  # C rows kept <= F
     assert rowsum < 2 ** 63
     A = rowsum / 2 ** 32 + Qh                 # sredc of the row sum
+    if split:
+        A = 2 * (rowsum / 2 / 2 ** 32 + Qh)   # two sredc'd half sums
+        assert A < LIM
     S = (2 * A * Qh) / 2 ** 32 + Qh           # monomial combination
     msg = ""
     if fold:
@@ -75,7 +79,7 @@ def check(dig, logg, fold):
         msg = f", C {(max(C0, Cred) + 7 * S) / Q:.3f}Q"
     out = max(inv([S] * 1024))
     assert out < 3 * Q, f"inverse output {out / Q:.3f}Q"
-    print(f"Q={Q} dig={dig} logG={logg} fold={fold}: fwd {F / Q:.3f}Q{msg}, S {S / Q:.3f}Q, "
+    print(f"Q={Q} dig={dig} logG={logg} fold={fold}{' split' if split else ''}: fwd {F / Q:.3f}Q{msg}, S {S / Q:.3f}Q, "
           f"row sums 2^{rowsum.bit_length() if isinstance(rowsum, int) else __import__('math').log2(rowsum):.1f}, "
           f"inverse out {out / Q:.3f}Q (reductions {RED})  OK")
 
@@ -83,3 +87,4 @@ def check(dig, logg, fold):
 # the shapes blind_rotate_fast4.hip instantiates (fast4_shape_supported)
 for shape in ((4, 7, True), (6, 5, True), (5, 5, False), (3, 9, False)):
     check(*shape)
+check(4, 7, True, split=True)  # the SPLIT form (STD128 shape only)

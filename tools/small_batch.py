@@ -9,6 +9,8 @@
   and    the reference's CHES-experiments.cpp:30-61: STD128 AND on 256 pairs, 1000 calls
          (host-array API and device-resident), and the same through the unchanged reference
          code on the shim (oracle/_ref/ref_dropin) when present.
+  split  STD128 NAND and its blind rotation at B = 64 .. 2048, fast4's two-group form against the
+         one-group kernel (the tfhe_knobs.split4 threshold)
   func   CHES-experiments.cpp:64-126: EvalFunc(x^3 mod p) in GenerateBinFHEContext(STD128, true,
          12, 0, GINX, false, 1 << 18) at B = 1, 8, 64, 256, 512 (host-array, device-resident, and
          the drop-in through ref_dropin sizes=...).
@@ -96,9 +98,22 @@ def run_sign(reps):
             k = 4
             h = ct[:k].cpu().numpy().astype(np.uint64)
             exact = bool(np.array_equal(out[:k].cpu().numpy().astype(np.uint64), orc.eval_sign(h, SIGN_MOD)))
-            rows.append({"B": B, "ms_per_call": round(best * 1e3, 3), "mean_ms": round(mean * 1e3, 3),
-                         "bootstraps_per_ct": per, "bootstraps_per_s": round(B * per / best, 1),
-                         "blind_rotation_ms": round(br * 1e3, 3), "parity_4": exact})
+            row = {"B": B, "ms_per_call": round(best * 1e3, 3), "mean_ms": round(mean * 1e3, 3),
+                   "bootstraps_per_ct": per, "bootstraps_per_s": round(B * per / best, 1),
+                   "blind_rotation_ms": round(br * 1e3, 3), "parity_4": exact}
+            if B <= ctx.knobs()["duo"]:  # the same call on the one-workgroup form (A/B, same box)
+                with ctx.knobs_set(duo=0):
+                    b1, _ = timed(lambda: ctx.EvalSignDevice(B, ct.data_ptr(), SIGN_MOD, out.data_ptr(), stream=sp),
+                                  reps, sync)
+                    br1, _ = timed(lambda: tfhe_amd.capi.check(
+                        lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp),
+                        "eval_acc"), reps, sync)
+                    one = out[:k].cpu().numpy().astype(np.uint64)
+                ctx.EvalSignDevice(B, ct.data_ptr(), SIGN_MOD, out.data_ptr(), stream=sp)
+                sync()
+                row.update(one_workgroup_ms_per_call=round(b1 * 1e3, 3), one_workgroup_blind_rotation_ms=round(br1 * 1e3, 3),
+                           two_equal_one=bool(np.array_equal(one, out[:k].cpu().numpy().astype(np.uint64))))
+            rows.append(row)
         ref = rows[-1]["bootstraps_per_s"]
         for r in rows:
             r["rate_vs_1024"] = round(r["bootstraps_per_s"] / ref, 3)
@@ -140,9 +155,19 @@ def run_and(reps_calls=1000):
     torch.cuda.synchronize(dev)
     dev_s = time.perf_counter() - t0
     same = bool(np.array_equal(do.cpu().numpy().astype(np.uint64), ho))
+    with ctx.knobs_set(split4=0):  # the one-group kernel, same box (A/B)
+        ctx.EvalBinGateDevice("AND", B, d1.data_ptr(), d2.data_ptr(), do.data_ptr(), stream=sp)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps_calls):
+            ctx.EvalBinGateDevice("AND", B, d1.data_ptr(), d2.data_ptr(), do.data_ptr(), stream=sp)
+        torch.cuda.synchronize(dev)
+        one_s = time.perf_counter() - t0
+        same = same and bool(np.array_equal(do.cpu().numpy().astype(np.uint64), ho))
     res = {"what": "CHES-experiments.cpp:30-61: STD128 AND, 256 pairs, 1000 calls", "B": B, "calls": reps_calls,
            "host_array_total_s": round(host_s, 3), "host_array_ms_per_call": round(host_s / reps_calls * 1e3, 3),
            "device_resident_ms_per_call": round(dev_s / reps_calls * 1e3, 3),
+           "device_resident_one_group_ms_per_call": round(one_s / reps_calls * 1e3, 3),
            "host_array_bootstraps_per_s": round(B * reps_calls / host_s, 1), "outputs_equal": same}
     ctx.GPUClean()
     if os.path.exists(DROPIN):
@@ -159,6 +184,50 @@ def run_and(reps_calls=1000):
             else:
                 res["dropin_error"] = r.stderr[-500:]
     emit(res)
+
+
+def run_split(reps):
+    """STD128 NAND device-resident and the blind rotation alone, two-group form (split4 forced on) against the
+    one-group kernel (split4 = 0) at batch sizes around the default limit: picks tfhe_knobs.split4."""
+    import torch
+
+    import tfhe_amd
+    from bench import synthetic_keys
+
+    p = tfhe_amd.params_from_set("STD128")
+    bsk, ksk = synthetic_keys(p)
+    ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    sp = s.cuda_stream
+    sync = lambda: torch.cuda.synchronize(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    lib = tfhe_amd.lib()
+    rows = []
+    for B in (64, 128, 256, 384, 512, 768, 1024, 2048):
+        c1 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+        c2 = torch.randint(0, int(p.q), (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+        out = torch.empty_like(c1)
+        a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
+        acc = torch.zeros((B, 2, p.N), dtype=torch.int64, device=dev)
+        row = {"B": B}
+        outs = []
+        for tag, lim in (("split", 1 << 20), ("one_group", 0)):
+            with ctx.knobs_set(split4=lim):
+                gate, _ = timed(lambda: ctx.EvalBinGateDevice("NAND", B, c1.data_ptr(), c2.data_ptr(), out.data_ptr(),
+                                                              stream=sp), reps, sync)
+                outs.append(out.cpu().numpy())
+                br, _ = timed(lambda: tfhe_amd.capi.check(
+                    lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp), "eval_acc"),
+                    reps, sync)
+            row[f"{tag}_gate_ms"] = round(gate * 1e3, 3)
+            row[f"{tag}_blind_rotation_ms"] = round(br * 1e3, 3)
+        row["equal"] = bool(np.array_equal(outs[0], outs[1]))
+        rows.append(row)
+        progress(f"split B={B}: {row}")
+    emit({"what": "STD128 NAND device-resident: two-group fast4 (SPLIT) vs one group", "rows": rows})
+    ctx.GPUClean()
 
 
 def run_func(reps):
@@ -225,7 +294,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     for w in args.what:
-        {"sign": lambda: run_sign(args.reps), "and": lambda: run_and(), "func": lambda: run_func(args.reps)}[w]()
+        {"sign": lambda: run_sign(args.reps), "and": lambda: run_and(), "func": lambda: run_func(args.reps),
+         "split": lambda: run_split(args.reps)}[w]()
 
 
 if __name__ == "__main__":
