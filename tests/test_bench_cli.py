@@ -88,11 +88,12 @@ def test_bench_line_passes_its_own_checks():
 
 @pytest.mark.gpu
 def test_bench_exits_nonzero_on_wrong_outputs():
-    """A fault probe of the test library (probe 3: f64w without its prologue barrier, wrong on every
-    ciphertext, tests/test_gpu_f64w_race.py; duo = 0 keeps this small batch on f64w) makes the
-    benchmarked outputs wrong: the line says so and the process fails."""
+    """A fault injection of the test library (probe 6: f64w flips the lowest bit of ciphertext 0's
+    accumulator; duo = 0 keeps this small batch on f64w) makes the benchmarked outputs wrong: the line
+    says so and the process fails.  (Probe 3, the prologue race, cannot do it here: the gate pipeline's
+    test-vector accumulators have acc0 = 0, and the race only overwrites zeros with zeros.)"""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C5a", "--batch", "8", "--steps",
-                        "1", "--warmup", "1", "--no-cpu-baseline", "--test-lib", "--knob", "probe=3", "--knob", "duo=0"],
+                        "1", "--warmup", "1", "--no-cpu-baseline", "--test-lib", "--knob", "probe=6", "--knob", "duo=0"],
                        capture_output=True, text=True, timeout=300,
                        env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
     assert r.returncode == 1, r.stderr[-3000:]
