@@ -88,8 +88,8 @@ def test_bench_line_passes_its_own_checks():
 
 @pytest.mark.gpu
 def test_bench_exits_nonzero_on_wrong_outputs():
-    """A fault injection of the test library (probe 6: f64w flips the lowest bit of ciphertext 0's
-    accumulator; duo = 0 keeps this small batch on f64w) makes the benchmarked outputs wrong: the line
+    """A fault injection of the test library (probe 6: f64w flips bit 40 of ciphertext 0's accumulator
+    word acc1[0]; duo = 0 keeps this small batch on f64w) makes the benchmarked outputs wrong: the line
     says so and the process fails.  (Probe 3, the prologue race, cannot do it here: the gate pipeline's
     test-vector accumulators have acc0 = 0, and the race only overwrites zeros with zeros.)"""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "C5a", "--batch", "8", "--steps",

@@ -712,8 +712,8 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 // PROBE (test library only, TFHE_TEST_PROBES; tests/test_gpu_f64w_race.py): bit 1 delays waves 1..
 // inside the prologue's C' transform (between passes B and C), bit 0 omits the barrier after it --
 // together they reproduce the round-0 race of the round-2 kernel; bit 2 (timing only) drops the
-// barrier before each further digit's pass A; 6 (fault injection, tests/test_bench_cli.py) flips the lowest
-// bit of ciphertext 0's acc1[0], so every later output of that ciphertext is wrong
+// barrier before each further digit's pass A; 6 (fault injection, tests/test_bench_cli.py) flips bit 40 of
+// ciphertext 0's acc1[0] (the extracted b: large enough to survive every modulus switch after it)
 // RESCUE (launched behind every f64wduo launch): only the ciphertexts whose duo pair timed out (the pair's
 // failed word, kernels.hpp DuoBuf) run, from their saved inputs; the others exit at once
 template <bool RED, bool WRAP, int LD, int PROBE = 0, bool RESCUE = false>
@@ -938,8 +938,8 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         g[k] = k == 0 ? v : (v == 0 ? 0 : P.Q - v);
         g[N + k] = __builtin_bit_cast(uint64_t, buf[N + k]);
     }
-    if constexpr (PROBE == 6) {  // fault injection (test library): ciphertext 0's acc1[0] off by one
-        if (blockIdx.x == 0 && t == 0) g[N] ^= 1;
+    if constexpr (PROBE == 6) {  // fault injection (test library): ciphertext 0's acc1[0] off by 2^40
+        if (blockIdx.x == 0 && t == 0) g[N] ^= 1ull << 40;
     }
 }
 
