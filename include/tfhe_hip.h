@@ -264,7 +264,7 @@ typedef struct tfhe_knobs {
     int32_t host_parts;   /* sub-batches per device in the host-array runner (>= 1) */
     int32_t wire;         /* 0: u64 words over PCIe (no narrow wire format) */
     int32_t acc_flags;    /* 0: host-array EvalAcc waits for the whole launch (no completion flags) */
-    int32_t f64w;         /* 0: slot-layout FP64 blind rotation instead of the wave-local one */
+    int32_t f64w;         /* retired: must be 1 (round 5 removed the slot-layout FP64 kernel 0 selected) */
     int32_t sf2;          /* 0: gen3sf special-form blind rotation instead of the wave-local sf2 */
     int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
     int32_t trace;        /* host-array runner timeline on stderr */

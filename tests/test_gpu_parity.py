@@ -364,28 +364,28 @@ def test_key_file_roundtrip(std128, capi, tmp_path):
         capi.BinFHEContextHIP.from_key_file(capi.params_from_set("STD128_OPT"), path)
 
 
-@pytest.mark.parametrize("pset,path,kernel", [("STD192", "f64", 3), ("STD192", "f64-nofold", 2), ("STD192", "generic", 0),
-                                              ("STD192", "f64-slot", 3), ("STD192Q_OPT", "f64", 3),
-                                              ("STD128Q", "f64", 3), ("STD128Q", "f64-slot", 3),
-                                              ("STD128Q", "f64-exactonly", 2), ("STD128Q", "f64-nofold", 2),
+@pytest.mark.parametrize("pset,path,kernel", [("STD192", "f64", 3), ("STD192", "f64-nofold", 0), ("STD192", "generic", 0),
+                                              ("STD192Q_OPT", "f64", 3), ("STD128Q", "f64", 3),
+                                              ("STD128Q", "f64-one-workgroup", 3), ("STD128Q", "f64-exactonly", 0),
                                               ("STD128Q", "generic-v2", 0), ("STD192", "generic-v1", 0)])
 def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     """STD192 (Q = 2^37 - 2^17 + 1) and STD128Q (Q = 2^50 - 2^14 + 1, the reducing variant),
-    N = 2048, run on the exact-FP64 kernel by default with the top digit's transforms
-    eliminated (TFHE_F64_FOLD=0 keeps all of them) and on the u64 generic kernel with
-    TFHE_FORCE_GENERIC=1; all equal the oracle, including accumulator boundary values.
-    STD128Q's top digit is not always exact (centred c in [2^49 - 2^24, Q/2) leaves a
-    residual), so its fold runs the WRAP correction (TFHE_F64_FOLD=1 folds exact sets only):
-    Q/2 - 1 and Q/2 - 5000 put such coefficients in round 0, so the correction runs."""
+    N = 2048, run on the exact-FP64 kernel by default with the top digit's transforms eliminated
+    (STD128Q at this batch: the two-workgroup f64wduo; duo = 0 keeps f64w) and on the u64 generic
+    kernel with TFHE_FORCE_GENERIC=1; all equal the oracle, including accumulator boundary values.
+    STD128Q's top digit is not always exact (centred c in [2^49 - 2^24, Q/2) leaves a residual), so
+    its fold runs the WRAP correction: Q/2 - 1 and Q/2 - 5000 put such coefficients in round 0, so the
+    correction runs.  Unfolded contexts (TFHE_F64_FOLD=0, or =1 on STD128Q: exact sets only) run the
+    generic kernel since round 5 retired the slot-layout FP64 kernel."""
     op = oracle.params_from_set(pset)
     cp = capi.params_from_set(pset)
     rs = np.random.default_rng(5)
     bsk = rs.integers(0, op.Q, cp.bsk_words(), dtype=np.uint64)
     ksk = rs.integers(0, op.qKS, cp.ksk_words(), dtype=np.uint64)
     env = {"generic": ("TFHE_FORCE_GENERIC", "1"), "f64-nofold": ("TFHE_F64_FOLD", "0"),
-           "f64-exactonly": ("TFHE_F64_FOLD", "1"), "f64-slot": ("TFHE_F64W", "0"),
+           "f64-exactonly": ("TFHE_F64_FOLD", "1"),
            "generic-v2": ("TFHE_FORCE_GENERIC", "1"), "generic-v1": ("TFHE_FORCE_GENERIC", "1")}.get(path)
-    knob = {"generic-v2": {"generic": 2}, "generic-v1": {"generic": 1}}.get(path, {})
+    knob = {"generic-v2": {"generic": 2}, "generic-v1": {"generic": 1}, "f64-one-workgroup": {"duo": 0}}.get(path, {})
     if env:
         os.environ[env[0]] = env[1]
     try:  # the environment is read at setup (tfhe_knobs); the generic kernel's form is a knob

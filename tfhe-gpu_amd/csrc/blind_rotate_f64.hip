@@ -1,5 +1,5 @@
 // blind_rotate_f64.hip -- CGGI blind rotation in exact FP64 integer arithmetic for
-// 2^32 <= Q < 2^50 (STD192(_OPT), STD192Q(_OPT), STD128Q(_OPT); N = 1024 or 2048).
+// 2^32 <= Q < 2^50 (STD192(_OPT), STD192Q(_OPT), STD128Q(_OPT); N = 2048, top digit folded).
 //
 // Same math as the generic kernel (rgsw-acc-cggi.cpp:246-307, rgsw-acc.cpp:57-111), but
 // every NTT-domain value is an integer held exactly in a double, so a modular product is
@@ -8,12 +8,11 @@
 //     h = a*b (rounded), l = fma(a, b, -h)          a*b = h + l exactly
 //     q = rint(h / Q),   r = fma(-q, Q, h) + l      r = a*b - qQ exactly, |r| <~ Q/2
 // Exactness holds while |a*b| < 2^102 and every sum stays below 2^53.  Q < 2^40 (RED =
-// false): the forward transform grows by < Q/2 per stage (< 6Q after 11), the inverse
-// doubles per stage from |S| < 1.1Q (< 2^51 after 11); no reduction at all.  Q < 2^50
-// (RED = true, STD128Q class): every radix-4 unit reduces its outputs to |x| <~ Q/2
-// (x - rint(x/Q) Q, three instructions), which keeps all values below 4Q < 2^52.
-// Keys and tables are centred (|x| <= Q/2).  The accumulator stays in int64 registers
-// (canonical [0, Q)) for the closed-form digit decomposition of the generic v2 kernel.
+// false): no reduction inside the transforms; Q < 2^50 (RED = true, STD128Q class): the
+// reductions tools/bounds_f64.py places (x - rint(x/Q) Q, three instructions).  Keys and
+// tables are centred (|x| <= Q/2); the accumulator is a centred double.
+// Kernels: k_blind_rotate_f64w (one 512-thread workgroup per ciphertext, wave-local passes) and
+// k_blind_rotate_f64wduo (STD128Q class, two workgroups per ciphertext for small batches).
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -57,90 +56,6 @@ __device__ __forceinline__ double fred(double x, const F64Const& K) {
     return __fma_rn(-__builtin_rint(__dmul_rn(x, K.Qinv)), K.Q, x);
 }
 
-[[maybe_unused]] constexpr uint32_t ilog2c(uint32_t x) { return x <= 1 ? 0 : 1 + ilog2c(x >> 1); }
-
-// CT stages m and 2m fused (radix-4 units), both polynomials of buf[2][N]; TH threads, all
-// trip counts and strides compile-time; RED: reduce the unit's outputs
-template <uint32_t N, uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_fwd(double* buf, const double* psi, const F64Const& K) {
-    constexpr uint32_t logN = ilog2c(N), units = N >> 2;
-    static_assert((2 * units) % TH == 0 && N % TH == 0, "thread mapping");
-    const uint32_t t = threadIdx.x;
-#pragma unroll 1
-    for (uint32_t st = 0; st < logN / 2; ++st) {
-        const uint32_t m = 1u << (2 * st), loglen = logN - 1 - 2 * st, lh = loglen - 1, h = 1u << lh;
-#pragma unroll
-        for (uint32_t r = 0; r < 2 * units / TH; ++r) {
-            const uint32_t u = t + r * TH, poly = u >= units, uu = u - poly * units;
-            const uint32_t i = uu >> lh, jj = uu & (h - 1);
-            double* a = buf + poly * N + (i << (loglen + 1)) + jj;
-            const double w = psi[m + i], w1 = psi[2 * m + 2 * i], w2 = psi[2 * m + 2 * i + 1];
-            double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
-            double v = fmodmul(a2, w, K);
-            a2 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
-            v = fmodmul(a3, w, K);
-            a3 = __dsub_rn(a1, v), a1 = __dadd_rn(a1, v);
-            v = fmodmul(a1, w1, K);
-            a1 = __dsub_rn(a0, v), a0 = __dadd_rn(a0, v);
-            v = fmodmul(a3, w2, K);
-            a3 = __dsub_rn(a2, v), a2 = __dadd_rn(a2, v);
-            if constexpr (RED) a0 = fred(a0, K), a1 = fred(a1, K), a2 = fred(a2, K), a3 = fred(a3, K);
-            a[0] = a0, a[h] = a1, a[2 * h] = a2, a[3 * h] = a3;
-        }
-        __syncthreads();
-    }
-    if constexpr (logN & 1) {
-        constexpr uint32_t m = N >> 1, half = N >> 1;
-#pragma unroll
-        for (uint32_t r = 0; r < N / TH; ++r) {
-            const uint32_t b = t + r * TH, poly = b >= half, bb = b - poly * half;
-            double* a = buf + poly * N + 2 * bb;
-            const double v = fmodmul(a[1], psi[m + bb], K), u0 = a[0];
-            a[0] = RED ? fred(__dadd_rn(u0, v), K) : __dadd_rn(u0, v);
-            a[1] = RED ? fred(__dsub_rn(u0, v), K) : __dsub_rn(u0, v);
-        }
-        __syncthreads();
-    }
-}
-
-// GS inverse without N^-1 (folded into the BSK); RED: reduce the doubling outputs
-template <uint32_t N, uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_inv(double* buf, const double* ipsi, const F64Const& K) {
-    constexpr uint32_t logN = ilog2c(N), units = N >> 2, half = N >> 1;
-    constexpr uint32_t lg0 = logN & 1;
-    const uint32_t t = threadIdx.x;
-    if constexpr (logN & 1) {
-#pragma unroll
-        for (uint32_t r = 0; r < N / TH; ++r) {
-            const uint32_t b = t + r * TH, poly = b >= half, bb = b - poly * half;
-            double* a = buf + poly * N + 2 * bb;
-            const double u0 = a[0], u1 = a[1];
-            a[0] = RED ? fred(__dadd_rn(u0, u1), K) : __dadd_rn(u0, u1);
-            a[1] = fmodmul(__dsub_rn(u0, u1), ipsi[half + bb], K);
-        }
-        __syncthreads();
-    }
-#pragma unroll 1
-    for (uint32_t st = 0; st < logN / 2; ++st) {
-        const uint32_t lh = lg0 + 2 * st, h = 1u << lh, m = (N >> lg0) >> (1 + 2 * st);
-#pragma unroll
-        for (uint32_t r = 0; r < 2 * units / TH; ++r) {
-            const uint32_t u = t + r * TH, poly = u >= units, uu = u - poly * units;
-            const uint32_t i = uu >> lh, jj = uu & (h - 1);
-            double* a = buf + poly * N + (i << (lh + 2)) + jj;
-            const double w1 = ipsi[m + 2 * i], w2 = ipsi[m + 2 * i + 1], w = ipsi[(m >> 1) + i];
-            const double a0 = a[0], a1 = a[h], a2 = a[2 * h], a3 = a[3 * h];
-            const double s0 = __dadd_rn(a0, a1), d0 = fmodmul(__dsub_rn(a0, a1), w1, K);
-            const double s1 = __dadd_rn(a2, a3), d1 = fmodmul(__dsub_rn(a2, a3), w2, K);
-            a[0] = RED ? fred(__dadd_rn(s0, s1), K) : __dadd_rn(s0, s1);
-            a[2 * h] = fmodmul(__dsub_rn(s0, s1), w, K);
-            a[h] = RED ? fred(__dadd_rn(d0, d1), K) : __dadd_rn(d0, d1);
-            a[3 * h] = fmodmul(__dsub_rn(d0, d1), w, K);
-        }
-        __syncthreads();
-    }
-}
-
 // ---- N = 2048: radix-8 register passes over a swizzled LDS buffer -------------------------
 // One thread owns 8 elements of ONE polynomial per pass (threads 0..TH/2-1 polynomial 0), so a
 // transform is four passes -- stages (0-2) (3-5) (6-8) radix-8 and (9-10) two radix-4 units --
@@ -152,12 +67,6 @@ __device__ __forceinline__ uint32_t swz(uint32_t x) {
     const uint32_t c = (x >> 5) & 7;
     return x ^ (c << 2) ^ (c & 3);
 }
-template <uint32_t N>
-__device__ __forceinline__ uint32_t bidx(uint32_t x) {
-    if constexpr (N == 2048) return swz(x);
-    else return x;
-}
-
 __device__ __forceinline__ void ct_bf(double& a, double& b, double w, const F64Const& K) {
     const double v = fmodmul(b, w, K);
     b = __dsub_rn(a, v), a = __dadd_rn(a, v);
@@ -250,345 +159,6 @@ __device__ __forceinline__ uint32_t f64_tau() {
     uint32_t tau = threadIdx.x & 255;
     asm volatile("" : "+v"(tau));
     return tau;
-}
-
-template <uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_fwd2048(double* buf, double (&v)[8], const double* psi, const F64Const& K) {
-    static_assert(TH == 512, "one thread per 8 elements of one polynomial");
-    constexpr uint32_t N = 2048;
-    const uint32_t tau = f64_tau();
-    double* p = buf + (threadIdx.x >> 8) * N;
-    {  // pass A on v = elements tau + 256k of polynomial t >> 8, held in registers
-        uint32_t ad[8];
-        ad_A(tau, ad);
-        f64_r8_fwd_core(v, 1, 0, psi, K);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) p[ad[k]] = RED ? fred(v[k], K) : v[k];
-    }
-    __syncthreads();
-    {
-        uint32_t ad[8];
-        ad_B(tau, ad);
-        f64_r8_fwd<RED>(p, ad, 8, tau >> 5, psi, K);
-    }
-    __syncthreads();
-    {
-        uint32_t ad[8];
-        ad_C(tau, ad);
-        f64_r8_fwd<RED>(p, ad, 64, tau >> 2, psi, K);
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < 2; ++r) {  // stages 9 (h = 2) and 10 (h = 1) on units 4u .. 4u+3
-        const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
-        double v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
-        const double w = psi[N / 4 + u];
-        ct_bf(v0, v2, w, K), ct_bf(v1, v3, w, K);
-        const double2 w1 = *(const double2*)(psi + N / 2 + 2 * u);
-        ct_bf(v0, v1, w1.x, K), ct_bf(v2, v3, w1.y, K);
-        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K), v2 = fred(v2, K), v3 = fred(v3, K);
-        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
-    }
-    __syncthreads();
-}
-
-template <uint32_t TH, bool RED>
-__device__ __forceinline__ void f64_ntt_inv2048(double* buf, double (&v)[8], const double* ipsi, const F64Const& K) {
-    static_assert(TH == 512, "one thread per 8 elements of one polynomial");
-    constexpr uint32_t N = 2048;
-    const uint32_t tau = f64_tau();
-    double* p = buf + (threadIdx.x >> 8) * N;
-#pragma unroll
-    for (uint32_t r = 0; r < 2; ++r) {  // h = 1 then h = 2 on units 4u .. 4u+3
-        const uint32_t u = tau + 256 * r, u0 = swz(4 * u);
-        double v0 = p[u0], v1 = p[u0 ^ 1], v2 = p[u0 ^ 2], v3 = p[u0 ^ 3];
-        const double2 w1 = *(const double2*)(ipsi + N / 2 + 2 * u);
-        gs_bf(v0, v1, w1.x, K), gs_bf(v2, v3, w1.y, K);
-        const double w = ipsi[N / 4 + u];
-        gs_bf(v0, v2, w, K), gs_bf(v1, v3, w, K);
-        if constexpr (RED) v0 = fred(v0, K), v1 = fred(v1, K);
-        p[u0] = v0, p[u0 ^ 1] = v1, p[u0 ^ 2] = v2, p[u0 ^ 3] = v3;
-    }
-    __syncthreads();
-    {
-        uint32_t ad[8];
-        ad_C(tau, ad);
-        f64_r8_inv<RED>(p, ad, 256, tau >> 2, ipsi, K);
-    }
-    __syncthreads();
-    {
-        uint32_t ad[8];
-        ad_B(tau, ad);
-        f64_r8_inv<RED>(p, ad, 32, tau >> 5, ipsi, K);
-    }
-    __syncthreads();
-    {  // pass A: v = elements tau + 256k of polynomial t >> 8, left in registers
-        uint32_t ad[8];
-        ad_A(tau, ad);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = p[ad[k]];
-        f64_r8_inv_core(v, 4, 0, ipsi, K);
-    }
-}
-
-// exact double (|x| < 2^52, integer) -> int64
-__device__ __forceinline__ int64_t d2ll(double x) {
-    const double hi = floor(__dmul_rn(x, 0x1p-32));
-    const double lo = __fma_rn(hi, -0x1p32, x);  // in [0, 2^32)
-    return ((int64_t)(int32_t)hi << 32) + (int64_t)(uint32_t)lo;
-}
-
-// table block (doubles): psi[N] ipsi[N] mono[2N], then the BSK [n][2][dG2][2][N]
-// TH threads own CN slots each (t + TH k): N = 1024 runs 256 x 4, N = 2048 runs 512 x 4, so a
-// thread's state (acc, sums, C') fits 128 VGPRs and a CU holds 4 waves per SIMD (two 64 KiB
-// workgroups).  N = 2048 (AM): the accumulator is held in the layout of the transforms' pass A
-// instead (thread t: polynomial t >> 8, coefficients (t & 255) + 256q, q < 8), so the digits
-// enter the forward transform and the inverse transform's output enters the accumulator
-// update in registers; the products (C', sums, monomials) keep the slot layout.
-// MT: monomial factors from the two LDS tables (mt) instead of the 2N-entry table in memory
-template <int TH, int CN, bool RED, bool FOLD, bool WRAP = false, bool MT = !RED>
-__global__ void __launch_bounds__(TH, 4)
-k_blind_rotate_f64(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ eidx,
-                   const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io) {
-    extern __shared__ __align__(16) double lds_d[];
-    constexpr uint32_t N = TH * CN;
-    constexpr int F64_THREADS = TH;
-    double* psi = lds_d;
-    double* ipsi = lds_d + N;
-    double* buf = lds_d + 2 * N;  // [2][N]
-    // monomial factors from two 64-entry tables instead of gathers from the 2N-entry table in
-    // memory (cache misses in every round): mt[j] = psi^(64 j), mt[64 + j] = psi^j (centred), and
-    //     A (psi^e - 1) = fmodmul(fmodmul(A, mt[e >> 6]), mt[64 + (e & 63)]) - A
-    double* mt = lds_d + 4 * N;
-    __shared__ int wflag[2];  // WRAP vote of round i in wflag[i & 1], published by the round's first barrier
-    const uint32_t t = threadIdx.x, twoN = 2 * N, logG = P.logG;
-    const uint32_t ts = bidx<N>(t);  // swz(t + TH k) = swz(t) + TH k (TH a multiple of 256)
-    constexpr bool AM = N == 2048;
-    // logical position (polynomial * N + coefficient) of accumulator entry [p][k]
-    auto lpos = [t](int p, int k) -> uint32_t {
-        if constexpr (AM) return (t >> 8) * N + (t & 255) + 256 * (p * CN + k);
-        else return p * N + t + TH * k;
-    };
-    for (uint32_t k = t; k < twoN; k += F64_THREADS) lds_d[k] = tabs[k];
-    const double* mono = tabs + twoN;
-    constexpr uint32_t SH = 6, LM = 63;  // e = 64 hi + lo, hi < 2N / 64 <= 64
-    for (uint32_t k = t; k < 128; k += F64_THREADS) {
-        const uint32_t e = k < 64 ? 64 * k : k - 64;
-        if (e < twoN) {
-            const double v = __dadd_rn(mono[e], 1.0);  // psi^e, centred
-            mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
-        }
-    }
-    const double* bsk = tabs + 2 * twoN;
-    const uint64_t Qhalf = P.Q >> 1;
-    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
-    const uint32_t sh = 64 - logG;
-    uint64_t* g = acc_io + (size_t)blockIdx.x * twoN;
-    const uint64_t* ap = a + (size_t)blockIdx.x * P.n;
-    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n] (synchronised below)
-    stage_rot_exponents<F64_THREADS>(ex, ap, P.n, amod, twoN);
-    const size_t round_words = (size_t)4 * P.dG2 * N;
-
-    int64_t acc[2][CN];  // canonical [0, Q)
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int k = 0; k < CN; ++k) {
-            const uint64_t v = g[lpos(p, k)];
-            acc[p][k] = (int64_t)(v >= P.Q ? v % P.Q : v);
-        }
-    if (WRAP && t < 2) wflag[t] = 0;
-    __syncthreads();
-    double Cn[2][CN];  // FOLD: N^-1 NTT(acc), |Cn| <~ Q/2
-    if constexpr (FOLD) {
-        if constexpr (AM) {
-            double v[8];
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int k = 0; k < CN; ++k)
-                    v[p * CN + k] = (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
-            f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
-        } else {
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int k = 0; k < CN; ++k)
-                    buf[p * N + ts + F64_THREADS * k] =
-                        (double)((uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - (int64_t)P.Q);
-            __syncthreads();
-            f64_ntt_fwd<N, TH, RED>(buf, psi, K);
-        }
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int k = 0; k < CN; ++k) Cn[p][k] = fmodmul(buf[p * N + ts + F64_THREADS * k], K.Ninv, K);
-        __syncthreads();
-    }
-    const uint32_t Ld = FOLD ? P.digits - 1 : P.digits;  // digits that are transformed
-    int64_t KdL = 0;  // WRAP: residual after all digits = (c + KdL) >> (L g)
-    for (uint32_t z = 0; z < P.digits; ++z) KdL = (KdL << logG) + Bh;
-    const uint32_t shiftL = P.digits * logG;
-
-    for (uint32_t i = 0; i < P.n; ++i) {
-        const uint32_t ai = ex[i];  // a'_i, staged at kernel start (rgsw-acc-cggi.cpp:153)
-        double A[2][2][CN];  // |A| <= dG2 Q/2 (+)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int k = 0; k < CN; ++k) A[kk][j][k] = 0.0;
-        const double* ek = bsk + (size_t)i * round_words;
-        // One digit: extraction (registers), forward transform, products with rows 2l, 2l+1.
-        // CHECK (WRAP, digit 0): also raise the round's vote, wflag[i & 1], published by the
-        // transform's first barrier.  CORR (WRAP, after the digits, only when the vote is set):
-        // the correction "digit" -2^(gL) N^-1 w against the top rows, so that the round uses
-        // C' - 2^(gL) N^-1 NTT(w) in place of C' (w = 0 almost everywhere, |w| <= 1).
-        // CMERGE (FOLD, last digit): the C' rows' products join this digit's product loop, so a
-        // round has one key-load phase fewer
-        auto digit = [&](uint32_t l, auto corr_c, auto check_c, auto cmerge_c) {
-            constexpr bool CORR = decltype(corr_c)::value, CHECK = decltype(check_c)::value;
-            constexpr bool CMERGE = decltype(cmerge_c)::value;
-            const uint32_t lt = l + P.thr, shift = lt * logG;
-            int64_t Kd = 0;
-            for (uint32_t z = 0; z < lt; ++z) Kd = (Kd << logG) + Bh;
-            double v[8];
-            bool w = false;
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int k = 0; k < CN; ++k) {
-                    const int64_t c = (uint64_t)acc[p][k] < Qhalf ? acc[p][k] : acc[p][k] - Qs;
-                    double dv;
-                    if constexpr (CORR) {
-                        dv = __dmul_rn((double)((c + KdL) >> shiftL), -K.wfac);
-                    } else {
-                        const int64_t d = (c + Kd) >> shift;
-                        dv = (double)(int32_t)((int64_t)((uint64_t)d << sh) >> sh);  // |r| <= B/2
-                    }
-                    if constexpr (CHECK) w |= ((c + KdL) >> shiftL) != 0;
-                    if constexpr (AM) v[p * CN + k] = dv;
-                    else buf[p * N + ts + F64_THREADS * k] = dv;
-                }
-            if constexpr (CHECK) {
-                // round i - 1 read wflag[(i + 1) & 1] before its last barriers; round i + 1
-                // writes it after this round's barriers
-                if (t == 0) wflag[(i + 1) & 1] = 0;
-                if (w) wflag[i & 1] = 1;
-            }
-            if constexpr (AM) {
-                // no barrier before: pass A writes this thread's own entries
-                f64_ntt_fwd2048<TH, RED>(buf, v, psi, K);
-            } else {
-                __syncthreads();
-                f64_ntt_fwd<N, TH, RED>(buf, psi, K);
-            }
-            // Products, software-pipelined: group g = (slot k, rows) has 8 key values; the next
-            // group's loads are issued before this group's arithmetic (double-buffered
-            // registers, sched_barrier fences), so key misses overlap instead of being paid one
-            // load at a time.  Rows: the digit's (2l, 2l+1); CMERGE adds the C' rows (2Ld, 2Ld+1).
-            constexpr int GPS = CMERGE ? 2 : 1, NG = CN * GPS;
-            auto kload = [&](int g, double (&kv)[8]) {
-                const uint32_t x = t + F64_THREADS * (g / GPS);
-                const uint32_t r = (GPS == 2 && (g & 1)) ? Ld : l;
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        kv[(kk * 2 + j) * 2] = ek[((size_t)(kk * P.dG2 + 2 * r) * 2 + j) * N + x];
-                        kv[(kk * 2 + j) * 2 + 1] = ek[((size_t)(kk * P.dG2 + 2 * r + 1) * 2 + j) * N + x];
-                    }
-            };
-            double kv[2][8];
-            kload(0, kv[0]);
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                if (g + 1 < NG) kload(g + 1, kv[(g + 1) & 1]);
-                __builtin_amdgcn_sched_barrier(0);
-                const int k = g / GPS;
-                double d0, d1;
-                if (GPS == 2 && (g & 1)) {
-                    d0 = Cn[0][k], d1 = Cn[1][k];
-                } else {
-                    d0 = buf[ts + F64_THREADS * k], d1 = buf[N + ts + F64_THREADS * k];
-                }
-                const double(&cur)[8] = kv[g & 1];
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        A[kk][j][k] = __dadd_rn(A[kk][j][k], __dadd_rn(fmodmul(d0, cur[(kk * 2 + j) * 2], K),
-                                                                       fmodmul(d1, cur[(kk * 2 + j) * 2 + 1], K)));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            __syncthreads();
-        };
-        using F_ = std::false_type;
-        using T_ = std::true_type;
-        if constexpr (WRAP) {
-            if (Ld == 1) {
-                digit(0, F_{}, T_{}, T_{});
-            } else {
-                digit(0, F_{}, T_{}, F_{});
-                for (uint32_t l = 1; l + 1 < Ld; ++l) digit(l, F_{}, F_{}, F_{});
-                digit(Ld - 1, F_{}, F_{}, T_{});
-            }
-            if (wflag[i & 1]) digit(Ld, T_{}, F_{}, F_{});
-        } else if constexpr (FOLD) {
-            for (uint32_t l = 0; l + 1 < Ld; ++l) digit(l, F_{}, F_{}, F_{});
-            digit(Ld - 1, F_{}, F_{}, T_{});
-        } else {
-            for (uint32_t l = 0; l < Ld; ++l) digit(l, F_{}, F_{}, F_{});
-        }
-#pragma unroll
-        for (int k = 0; k < CN; ++k) {
-            const uint32_t x = t + F64_THREADS * k;
-            const uint32_t ip = (eidx[x] * ai) & (twoN - 1), in = (twoN - ip) & (twoN - 1);
-            double s0, s1;
-            if constexpr (MT) {
-                const double hp = mt[ip >> SH], lp = mt[64 + (ip & LM)], hn = mt[in >> SH], ln = mt[64 + (in & LM)];
-                auto mm = [&](double a, double h, double lo) { return __dsub_rn(fmodmul(fmodmul(a, h, K), lo, K), a); };
-                s0 = fred(__dadd_rn(mm(A[0][0][k], hp, lp), mm(A[1][0][k], hn, ln)), K);
-                s1 = fred(__dadd_rn(mm(A[0][1][k], hp, lp), mm(A[1][1][k], hn, ln)), K);
-            } else {
-                const double mp = mono[ip], mn = mono[in];
-                s0 = __dadd_rn(fmodmul(A[0][0][k], mp, K), fmodmul(A[1][0][k], mn, K));
-                s1 = __dadd_rn(fmodmul(A[0][1][k], mp, K), fmodmul(A[1][1][k], mn, K));
-            }
-            buf[ts + F64_THREADS * k] = s0;
-            buf[N + ts + F64_THREADS * k] = s1;
-            if constexpr (FOLD) Cn[0][k] = fred(__dadd_rn(Cn[0][k], s0), K), Cn[1][k] = fred(__dadd_rn(Cn[1][k], s1), K);
-        }
-        __syncthreads();
-        double v[8];
-        if constexpr (AM) f64_ntt_inv2048<TH, RED>(buf, v, ipsi, K);
-        else f64_ntt_inv<N, TH, RED>(buf, ipsi, K);
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int k = 0; k < CN; ++k) {
-                const double r = AM ? v[p * CN + k] : buf[p * N + ts + F64_THREADS * k];  // |r| < 2^52
-                const double q = __builtin_rint(__dmul_rn(r, K.Qinv));
-                int64_t u = acc[p][k] + d2ll(__fma_rn(-q, K.Q, r));  // in (-Q, 2Q)
-                u = u < 0 ? u + Qs : u;
-                acc[p][k] = u >= Qs ? u - Qs : u;
-            }
-        // AM: the last inverse pass only read this thread's own entries, and the next writes
-        // (the next round's pass A) are to the same entries -- no barrier
-        if constexpr (!AM) __syncthreads();
-    }
-    if constexpr (AM) __syncthreads();  // every last inverse pass has read its entries
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int k = 0; k < CN; ++k) buf[lpos(p, k)] = __builtin_bit_cast(double, acc[p][k]);
-    __syncthreads();
-    for (uint32_t k = t; k < N; k += F64_THREADS) {  // acc0 transposed (poly.cpp:762-770)
-        const uint64_t v = __builtin_bit_cast(uint64_t, buf[k == 0 ? 0 : N - k]);
-        g[k] = k == 0 ? v : (v == 0 ? 0 : P.Q - v);
-        g[N + k] = __builtin_bit_cast(uint64_t, buf[N + k]);
-    }
 }
 
 // ---- N = 2048, wave-local passes (f64w; the sf2 design of blind_rotate_generic.hip) ----------
@@ -1440,12 +1010,11 @@ bool f64_fold_enabled(const BRParams& P) {
 }
 
 namespace {
-// The instances shipped (round 4: only combinations some parameter set reaches, each in a parity test):
-//   f64w  <RED, WRAP, LD>: STD128Q(_OPT) <1, 1, 1>; STD192(_OPT), STD192Q(_OPT) <0, 0, 2>
-//   slot  <512, 4, RED, FOLD, WRAP>: STD128Q wrap <1, 1, 1>, STD192* fold <0, 1, 0>, unfolded <1, 0>, <0, 0>
-// (TFHE_F64_FOLD / the f64w knob select the slot layout and the unfolded forms: cross-checks)
+// The instances shipped (only combinations some parameter set reaches, each in a parity test):
+//   f64w  <RED, WRAP, LD>: STD128Q(_OPT) <1, 1, 1> (+ f64wduo and the rescue form); STD192(_OPT), STD192Q(_OPT)
+//   <0, 0, 2>.  Round 5 retired the slot-layout kernel (k_blind_rotate_f64, the cross-check for TFHE_F64W=0
+//   and the unfolded forms): an unfolded context (TFHE_F64_FOLD=0 / 1) now runs the generic u64 kernel.
 bool f64w_instance(bool red, bool wrap, int ld) { return (red && wrap && ld == 1) || (!red && !wrap && ld == 2); }
-bool slot_instance(bool red, bool fold, bool wrap) { return fold ? (wrap ? red : !red) : true; }
 }  // namespace
 
 bool f64_test_probes_compiled() {
@@ -1457,9 +1026,11 @@ bool f64_test_probes_compiled() {
 }
 
 bool f64_instance_available(const BRParams& P, bool fold) {
-    if (fold && !fold_possible(P)) return false;
-    const bool red = P.Q >= (1ull << 40), wrap = fold && !fold_exact(P);
-    return slot_instance(red, fold, wrap);  // (every f64w instance has its slot-layout twin)
+    if (!fold || !fold_possible(P)) return false;
+    const bool red = P.Q >= (1ull << 40), wrap = !fold_exact(P);
+    // f64w addresses the keys with 32-bit byte offsets (buffer resource)
+    const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
+    return fits32 && f64w_instance(red, wrap, (int)P.digits - 1);
 }
 
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
@@ -1480,7 +1051,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
                                    const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
                                    const Knobs& kn, void* duo) {
     if (B == 0) return hipSuccess;
-    if (P.N != 2048 || (fold && !fold_possible(P))) return hipErrorInvalidValue;
+    if (P.N != 2048 || !f64_instance_available(P, fold)) return hipErrorInvalidValue;
     F64Const K;
     K.Q = (double)P.Q;
     K.Qinv = 1.0 / K.Q;
@@ -1492,21 +1063,14 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
     const bool wrap = fold && !fold_exact(P);
     // psi, ipsi, two polynomials, monomial tables, rotation exponents
     const size_t lds = ((size_t)4 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
-    auto go = [&](auto kern) {
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
-                           amod, acc);
-    };
-    auto gow = [&](auto kern) {  // f64w (two more kernel arguments: the rescue form's)
+    auto gow = [&](auto kern) {  // f64w (the last two arguments: the rescue form's)
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(P.N / 4), lds, s, P, K, (const double*)keys, T.eidx, a,
                            amod, acc, (const uint32_t*)nullptr, (const uint64_t*)nullptr);
     };
     const bool red = P.Q >= (1ull << 40);
     const int ld = (int)P.digits - 1;
-    // f64w addresses the keys with 32-bit byte offsets (buffer resource)
-    const bool fits32 = (uint64_t)P.n * 4 * P.dG2 * P.N * 8 < (1ull << 32);
-    if (kn.f64w && fits32 && fold && f64w_instance(red, wrap, ld)) {
+    {
 #ifdef TFHE_TEST_PROBES
         // test library only (lib/libtfhe_hip_test.so): the fault probe of tests/test_gpu_f64w_race.py
         // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
@@ -1544,11 +1108,6 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         else gow(k_blind_rotate_f64w<false, false, 2>);
         return hipGetLastError();
     }
-    if (!slot_instance(red, fold, wrap)) return hipErrorNotSupported;
-    if (wrap) go(k_blind_rotate_f64<512, 4, true, true, true>);
-    else if (fold) go(k_blind_rotate_f64<512, 4, false, true>);
-    else red ? go(k_blind_rotate_f64<512, 4, true, false>) : go(k_blind_rotate_f64<512, 4, false, false>);
-    return hipGetLastError();
 }
 
 }  // namespace tfhe

@@ -203,8 +203,9 @@ const char* knob_out_of_range(const Knobs& k) {
     if (k.generic < 0 || k.generic > 2) return "generic (TFHE_GENERIC) not in 0..2";
     if (k.duo < 0 || k.duo > 256) return "duo (TFHE_DUO) not in 0..256";
     if (k.split4 < 0) return "split4 (TFHE_SPLIT4) < 0";
-    for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.f64w, k.sf2, k.sf2p, k.trace})
-        if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2, TFHE_SF2P) "
+    if (k.f64w != 1) return "f64w (TFHE_F64W): the slot-layout FP64 kernel it selected was retired in round 5 (must be 1)";
+    for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.sf2, k.sf2p, k.trace})
+        if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_SF2, TFHE_SF2P) "
                                    "not 0 or 1";
     if (k.probe < 0) return "probe < 0";
     return nullptr;

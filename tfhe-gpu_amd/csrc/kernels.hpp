@@ -25,7 +25,7 @@ struct Knobs {
     int32_t host_parts = 1;     // sub-batches per device of the host-array runner
     int32_t wire = 1;           // 0: u64 PCIe words (no narrow wire format)
     int32_t acc_flags = 1;      // 0: no completion-flagged EvalAcc output
-    int32_t f64w = 1;           // 0: slot-layout FP64 kernel instead of the wave-local f64w
+    int32_t f64w = 1;           // retired (round 5: the slot-layout FP64 kernel it selected is gone); must be 1
     int32_t sf2 = 1;            // 0: gen3sf instead of the wave-local sf2
     int32_t generic = 0;        // 0: gen3 / v2 by N; 1: v1 (all digits in LDS); 2: v2 also at N = 2048
     int32_t trace = 0;          // host-array runner timeline on stderr
