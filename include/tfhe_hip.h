@@ -275,7 +275,7 @@ typedef struct tfhe_knobs {
     int32_t sf2p;         /* two-digit special-form contexts, batches of 512 or more: 1 (default) runs two
                              ciphertexts per workgroup (sf2p, whose shared LDS holds the whole monomial factor
                              table); 0: one per workgroup (sf2) */
-    int32_t split4;       /* STD128-class contexts: batches up to this size (default 512) run each ciphertext's two
+    int32_t split4;       /* STD128-class contexts: batches up to this size (default 384) run each ciphertext's two
                              polynomials on two groups of four wavefronts (fast4 SPLIT); 0: never */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);

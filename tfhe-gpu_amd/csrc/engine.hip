@@ -1920,11 +1920,15 @@ tfhe_status tfhe_ciphertext_mul_matrix(tfhe_ctx* c, size_t K, const uint64_t* ct
     });
 }
 
+// GPULWEOperation::GPUSetup(numGPUs) (lwe-operation.cu:143-146) ignores numGPUs and works on device 0;
+// so does this (CiphertextMulMatrix runs on device 0): any count is accepted, as long as a device exists
+// (round 4 refused numGPUs above the visible count -- found by the multi-device drop-in test)
 tfhe_status tfhe_lwe_gpu_setup(int num_gpus) {
+    (void)num_gpus;
     return guarded([&]() -> tfhe_status {
         int count = 0;
         HCHECK(hipGetDeviceCount(&count));
-        if (num_gpus > count) return fail(TFHE_ERR_INVALID_ARGUMENT, "not enough GPUs");
+        if (count < 1) return fail(TFHE_ERR_DEVICE, "no HIP device visible");
         return TFHE_OK;
     });
 }

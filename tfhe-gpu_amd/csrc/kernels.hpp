@@ -33,7 +33,7 @@ struct Knobs {
     int32_t duo = 128;          // most ciphertexts per launch on the two-workgroup forms (sf2duo: two digits;
                                 // f64wduo: STD128Q class; <= 256); 0: never
     int32_t sf2p = 1;           // 0: sf2 with one ciphertext per workgroup instead of two (sf2p) above the duo batches
-    int32_t split4 = 512;       // STD128 class: batches up to this size run fast4's two-group form (SPLIT); 0: never
+    int32_t split4 = 384;       // STD128 class: batches up to this size run fast4's two-group form (SPLIT); 0: never
 };
 
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
