@@ -348,7 +348,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 #pragma unroll
             for (int k = 0; k < CN; ++k) v[p * CN + k] = acc[p][k];
         double d[2][4];
-        f64w_ntt_fwd<RED, false, (PROBE & 2) != 0>(buf, v, d, psi, K);
+        f64w_ntt_fwd<RED, false, PROBE < 5 && (PROBE & 2) != 0>(buf, v, d, psi, K);
 #pragma unroll
         for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -358,7 +358,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
     // round 0's first pass A (no barrier of its own) writes every block: without this barrier a
     // wave that gets here first overwrites blocks other waves are still reading (the wrong
     // STD128Q / STD192 ciphertexts of round 2)
-    if constexpr (!(PROBE & 1)) __syncthreads();
+    if constexpr (!(PROBE < 5 && (PROBE & 1))) __syncthreads();
     // digit l of c: low logG bits (signed) of (c + Kd_l) >> (l logG), Kd_l = sum_{z<l} Bh 2^(z logG)
     // (the closed form of the reference's carries); WRAP: residual (c + KdL) >> (L logG)
     double sl[LD + 1], kl[LD + 1];  // 2^-(l logG), Kd_l 2^-(l logG): exact
@@ -408,7 +408,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 if (wv) wflag[i & 1] = 1;
             }
             // other waves may still read their blocks (PROBE bit 2: timing experiment without it)
-            if (sync && !(PROBE & 4)) __syncthreads();
+            if (sync && !(PROBE < 5 && (PROBE & 4))) __syncthreads();
             if (!CORR && l + 1 == LD) f64w_ntt_fwd<RED, true>(buf, v, d, psi, K);
             else f64w_ntt_fwd<RED>(buf, v, d, psi, K);
         };
@@ -706,7 +706,9 @@ constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
 // STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
 // (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
 // PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a
-// partner that never arrives would, and the polls are bounded 2^14 times
+// partner that never arrives would, and the polls are bounded 2^14 times.  PROBE 2 (timing only, results
+// invalid): no hand-off at all -- each member takes its own stage-1 values for its partner's -- the
+// bound on what the exchange costs per round
 template <int PROBE = 0>
 __global__ void __launch_bounds__(512, 2)
 k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, const uint64_t* __restrict__ a,
@@ -863,11 +865,13 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         // hand-off: this half's stage-1 values of both columns to the partner (thread t's 4 at k' 512 + t)
         double* mine = reinterpret_cast<double*>(X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N);
         const double* theirs = reinterpret_cast<const double*>(X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N);
+        if constexpr (PROBE != 2) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
+            for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's stores drained; every read of the inverse buffer done
-        if (t == 0) {
+        if (PROBE != 2 && t == 0) {
             constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kF64DuoMaxPolls;
             const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
             if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -882,12 +886,14 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
                 __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        __syncthreads();
-        if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
+        if constexpr (PROBE != 2) {
+            __syncthreads();
+            if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
+        }
         double lo[4], hi[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const double pv = duo_load_d(theirs + 512 * k + t);
+            const double pv = PROBE == 2 ? o[k] : duo_load_d(theirs + 512 * k + t);
             lo[k] = h ? pv : o[k];
             hi[k] = h ? o[k] : pv;
         }
@@ -1076,7 +1082,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
         // round-2 race, wrong results) and a timing-only build (4: STD192 without the barrier before
         // digit 1's pass A, results invalid; tools/f64w_barrier_probe.sh)
-        if (kn.probe != 0 && kn.probe != 5) {  // (5: the duo timeout probe, below)
+        if (kn.probe != 0 && kn.probe != 5 && kn.probe != 7) {  // (5, 7: the duo probes, below)
             if (kn.probe == 4 && !red && !wrap && ld == 2) gow(k_blind_rotate_f64w<false, false, 2, 4>);
             else if (kn.probe == 2 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 2>);
             else if (kn.probe == 3 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 3>);
@@ -1093,6 +1099,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             auto dk = k_blind_rotate_f64wduo<0>;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
+            if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""What the per-round hand-off costs the two-workgroup FP64 blind rotation (f64wduo, C5a's 8-GPU shard).
+
+Test library (lib/libtfhe_hip_test.so): STD128Q, device-resident blind rotation at B = 64 / 128, timed
+(min of --reps, HIP stream sync) for
+  one   f64w, one workgroup per ciphertext (duo = 0)
+  duo   f64wduo (the default for B <= 128)
+  free  f64wduo with NO hand-off (probe 7: each member takes its own stage-1 values for its partner's;
+        results invalid) -- the lower bound of the duo form, i.e. the exchange's price per round.
+One JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tfhe-gpu_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+
+    import tfhe_amd
+    from bench import synthetic_keys
+
+    p = tfhe_amd.params_from_set("STD128Q")
+    bsk, ksk = synthetic_keys(p)
+    ctx = tfhe_amd.BinFHEContextHIP(p, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
+    del bsk, ksk
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    sp = s.cuda_stream
+    lib = tfhe_amd.lib(tfhe_amd.capi.TEST_LIB)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    rows = []
+    for B in (64, 128):
+        a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
+        acc0 = torch.randint(0, int(p.Q), (B, 2, p.N), dtype=torch.int64, device=dev, generator=g)
+        row = {"B": B}
+        for tag, knobs in (("one", {"duo": 0}), ("duo", {}), ("free", {"probe": 7})):
+            acc = acc0.clone()
+            with ctx.knobs_set(**knobs):
+                ts = []
+                for _ in range(args.reps + 1):
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp),
+                                        "eval_acc")
+                    torch.cuda.synchronize(dev)
+                    ts.append(time.perf_counter() - t0)
+            row[f"{tag}_ms"] = round(min(ts[1:]) * 1e3, 3)
+            row[f"{tag}_us_per_round"] = round(min(ts[1:]) * 1e6 / p.n, 2)
+        row["handoff_us_per_round"] = round(row["duo_us_per_round"] - row["free_us_per_round"], 2)
+        rows.append(row)
+    print(json.dumps({"what": "f64wduo hand-off price (STD128Q blind rotation, device-resident)", "rows": rows}), flush=True)
+    ctx.GPUClean()
+
+
+if __name__ == "__main__":
+    main()
