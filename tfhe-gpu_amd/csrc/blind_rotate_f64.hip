@@ -1150,12 +1150,17 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
             constexpr bool G = kF64DuoGran;
             auto dk = k_blind_rotate_f64wduo<0, G>;
+            bool gran = G;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1, G>;  // test library only: a partner that never arrives
             if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2, G>;  // timing only: no hand-off (results invalid)
-            if (kn.probe == 8) dk = k_blind_rotate_f64wduo<0, !G>;  // the other hand-off form (A/B)
-            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<1, !G>;  // ... with the missing partner
+            if (kn.probe == 8) dk = k_blind_rotate_f64wduo<0, !G>, gran = !G;  // the other hand-off form (A/B)
+            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<1, !G>, gran = !G;  // ... with the missing partner
 #endif
+            if (gran) {  // tags are round numbers (12 bits): a stale word of an earlier launch must not match
+                if (P.n >= 4095) return hipErrorNotSupported;
+                if (hipError_t e = hipMemsetAsync(X.xbuf, 0, (size_t)B * 4 * kDuoN * 8, s); e != hipSuccess) return e;
+            }
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
                                a, amod, acc, X, (uint32_t)B);
