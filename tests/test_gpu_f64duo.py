@@ -135,8 +135,8 @@ def test_f64duo_partner_timeout_is_recomputed(oracle):
 
 
 def test_f64duo_other_handoff_form(oracle):
-    """The hand-off form the product build does not use (test library, probe 8: one flag per wavefront vs one
-    per workgroup) computes the same outputs, and its missing-partner path (probe 9) is recomputed by the
+    """The hand-off form the product build does not use (test library, probe 8: data-tagged granules vs the
+    workgroup flag) computes the same outputs, and its missing-partner path (probe 9) is recomputed by the
     rescue."""
     import tfhe_amd
 

@@ -702,7 +702,7 @@ __device__ __forceinline__ double duo_load_d(const double* p) {
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
-constexpr bool kF64DuoWaveFlags = false;  // the hand-off form of the product build (probe 8 runs the other)
+constexpr bool kF64DuoGran = false;  // the hand-off form of the product build (probe 8 runs the other)
 
 // STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
 // (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
@@ -710,15 +710,23 @@ constexpr bool kF64DuoWaveFlags = false;  // the hand-off form of the product bu
 // partner that never arrives would, and the polls are bounded 2^14 times.  PROBE 2 (timing only, results
 // invalid): no hand-off at all -- each member takes its own stage-1 values for its partner's -- the
 // bound on what the exchange costs per round
-// WAVEF: one flag per wavefront instead of one per workgroup.  Thread t takes the partner's thread t's
-// values, and those are stored by the partner's wave t >> 6, so each wave publishes its own flag after its
-// own stores drain (lane 0, sc1, flag word 8 + w of the member's line) and polls only the partner's wave
-// flag: no workgroup barrier on either side of the hand-off.  Correct per wave: a wave's round-(i+2) stores
-// to a parity buffer follow (program order and data) its poll of the partner wave's round-(i+1) flag, which
-// that wave raised only after loading its round-i values.  (Round 5 also measured data-tagged granules --
-// 52-bit value + 12-bit round tag per 8-byte word, every thread polling its own 4 words: 8.03 against the
-// flag's 7.71 us per round at 128, profiles/r05g/duo_probe.log -- and dropped them.)
-template <int PROBE = 0, bool WAVEF = false>
+// GRAN: the hand-off as data-tagged granules (MI355X_MICROARCH.md "handoff-1to1") instead of a flag: each
+// value travels with its round number in one 8-byte word (52-bit offset value + 12-bit tag, one sc1 store),
+// and each thread polls its partner thread's 4 words -- all four loads in flight per poll -- with no drain,
+// barrier, flag and second barrier per round.  Correct without a workgroup-wide order: thread t's
+// round-(i+2) store to a parity buffer depends (through the data) on its round-(i+1) loads, which the
+// partner's thread t made only after its round-i loads.  (Measured against the workgroup flag: a first
+// granule form polling the four words one after another 8.03 us per round at 128 against 7.71, a
+// one-flag-per-wavefront form 8.8-9.2 against 7.5-7.6; profiles/r05g, r05h.)
+[[maybe_unused]] __device__ __forceinline__ uint64_t gran_pack(double x, uint32_t tag) {  // |x| < 2^51, integer-valued
+    const double y = __dadd_rn(x, 0x1.8p52);                            // mantissa = x + 2^51, exactly
+    return (__builtin_bit_cast(uint64_t, y) & ((1ull << 52) - 1)) | ((uint64_t)tag << 52);
+}
+[[maybe_unused]] __device__ __forceinline__ double gran_value(uint64_t g) {
+    return __dsub_rn(__builtin_bit_cast(double, (g & ((1ull << 52) - 1)) | (0x433ull << 52)), 0x1.8p52);
+}
+
+template <int PROBE = 0, bool GRAN = false>
 __global__ void __launch_bounds__(512, 2)
 k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, const uint64_t* __restrict__ a,
                        uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X, uint32_t pairs) {
@@ -768,7 +776,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     }
     if (t < 2) wflag[t] = 0;
     if (t == 0) duo_dead = 0;
-    bool gone_w = false;  // WAVEF: this wave's partner wave timed out once (later rounds skip the wait)
+    bool gone_t = false;  // GRAN: this thread's partner words timed out once (later rounds skip the wait)
     stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
     __syncthreads();
     double Cn[4];  // N^-1 NTT(acc_j) at the lane's slots
@@ -877,45 +885,50 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         double* mine = reinterpret_cast<double*>(X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N);
         const double* theirs = reinterpret_cast<const double*>(X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N);
         double lo[4], hi[4];
-        if constexpr (WAVEF) {
+        if constexpr (GRAN) {
+            uint64_t* gm = reinterpret_cast<uint64_t*>(mine);
+            const uint64_t* gt = reinterpret_cast<const uint64_t*>(theirs);
             const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
+            double pv[4] = {o[0], o[1], o[2], o[3]};
             if constexpr (PROBE != 2) {
                 if (!gone) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
+                    for (int k = 0; k < 4; ++k)
+                        __hip_atomic_store(gm + 512 * k + t, gran_pack(fred(o[k], K), i + 1), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores drained
                 constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kF64DuoMaxPolls;
-                uint32_t ok = 1;
-                if (l == 0) {
-                    if (!gone) __hip_atomic_store(myflag + 8 + w, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    uint32_t polls = gone_w ? kMaxPolls : 0;
-                    while (polls < kMaxPolls &&
-                           __hip_atomic_load(const_cast<uint32_t*>(peerflag + 8 + w), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
-                           ++polls < kMaxPolls)
-                        __builtin_amdgcn_s_sleep(1);
-                    ok = polls < kMaxPolls;
+                uint64_t gv[4];
+                uint32_t polls = gone_t ? kMaxPolls : 0;
+                for (;;) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        gv[k] = __hip_atomic_load(const_cast<uint64_t*>(gt + 512 * k + t), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                    const bool ready = (gv[0] >> 52) == i + 1 && (gv[1] >> 52) == i + 1 && (gv[2] >> 52) == i + 1 &&
+                                       (gv[3] >> 52) == i + 1;
+                    if (ready || ++polls >= kMaxPolls) break;
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                ok = __builtin_amdgcn_readfirstlane(ok);
-                if (!ok && !gone_w) {
-                    gone_w = true;
-                    duo_dead = 1;  // (benign race: any wave's 1)
-                    if (l == 0) __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (polls >= kMaxPolls && !gone_t) {
+                    gone_t = true;
+                    duo_dead = 1;  // (benign race: any thread's 1)
+                    __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pv[k] = gran_value(gv[k]);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const double pv = PROBE == 2 ? o[k] : duo_load_d(theirs + 512 * k + t);
-                lo[k] = h ? pv : o[k];
-                hi[k] = h ? o[k] : pv;
+                lo[k] = h ? pv[k] : o[k];
+                hi[k] = h ? o[k] : pv[k];
             }
         }
-        if constexpr (!WAVEF && PROBE != 2) {
+        if constexpr (!GRAN && PROBE != 2) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
         }
-        if constexpr (!WAVEF) {
+        if constexpr (!GRAN) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's stores drained; every read of the inverse buffer done
         if (PROBE != 2 && t == 0) {
@@ -943,7 +956,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             lo[k] = h ? pv : o[k];
             hi[k] = h ? o[k] : pv;
         }
-        }  // !WAVEF
+        }  // !GRAN
         const double w0 = ipsi[1];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // stage 0 for all coefficients, then f64w's accumulator update
@@ -957,7 +970,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         }
     }
     __syncthreads();
-    if (WAVEF && t == 0 && duo_dead) __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (GRAN && t == 0 && duo_dead) __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // member h writes polynomial h (acc0 transposed, poly.cpp:762-770) through the two buffers (N doubles)
     double* st = bf;
     if (pp == h) {
@@ -1144,14 +1157,19 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             const DuoBuf X = duo_layout(duo);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
             const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
-            constexpr bool G = kF64DuoWaveFlags;
+            constexpr bool G = kF64DuoGran;
             auto dk = k_blind_rotate_f64wduo<0, G>;
+            bool gran = G;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1, G>;  // test library only: a partner that never arrives
             if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2, G>;  // timing only: no hand-off (results invalid)
-            if (kn.probe == 8) dk = k_blind_rotate_f64wduo<0, !G>;  // the other hand-off form (A/B)
-            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<1, !G>;  // ... with the missing partner
+            if (kn.probe == 8) dk = k_blind_rotate_f64wduo<0, !G>, gran = !G;  // the other hand-off form (A/B)
+            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<1, !G>, gran = !G;  // ... with the missing partner
 #endif
+            if (gran) {  // tags are round numbers (12 bits): a stale word of an earlier launch must not match
+                if (P.n >= 4095) return hipErrorNotSupported;
+                if (hipError_t e = hipMemsetAsync(X.xbuf, 0, (size_t)B * 4 * kDuoN * 8, s); e != hipSuccess) return e;
+            }
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
                                a, amod, acc, X, (uint32_t)B);

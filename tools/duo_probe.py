@@ -5,8 +5,8 @@ Test library (lib/libtfhe_hip_test.so): STD128Q, device-resident blind rotation 
 (min of --reps, HIP stream sync) for
   one   f64w, one workgroup per ciphertext (duo = 0)
   duo   f64wduo (the default for B <= 128)
-  alt   f64wduo with the other hand-off form (probe 8: one flag per wavefront if the product build uses one
-        per workgroup, and the reverse)
+  alt   f64wduo with the other hand-off form (probe 8: data-tagged granules if the product build uses the
+        workgroup flag, and the reverse)
   free  f64wduo with NO hand-off (probe 7: each member takes its own stage-1 values for its partner's;
         results invalid) -- the lower bound of the duo form, i.e. the exchange's price per round.
 One JSON line.
