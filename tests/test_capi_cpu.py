@@ -204,9 +204,11 @@ def test_environment_knobs_are_validated(env, why):
     assert "ERR" in r.stdout and "launch knob from the environment" in r.stdout and why in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("kernel", ["k_blind_rotate_sf2duo", "k_blind_rotate_f64wduo"])
-def test_product_library_has_no_duo_probe(capi, kernel):
-    """The duo timeout probes (a partner that never arrives) are test-library instances only."""
+@pytest.mark.parametrize("kernel,probes", [("k_blind_rotate_sf2duo", ["0", "1"]),
+                                            ("k_blind_rotate_f64wduo", ["0", "1", "2"])])
+def test_product_library_has_no_duo_probe(capi, kernel, probes):
+    """The duo probes (1: a partner that never arrives; 2: f64wduo with no hand-off, timing only) are
+    test-library instances only."""
     import re
     import subprocess
 
@@ -215,4 +217,4 @@ def test_product_library_has_no_duo_probe(capi, kernel):
         return sorted(set(re.findall(kernel + r"<(\d+)>", out)))
 
     assert duo(capi.library_path()) == ["0"]
-    assert duo(capi.capi.TEST_LIB) == ["0", "1"]
+    assert duo(capi.capi.TEST_LIB) == probes

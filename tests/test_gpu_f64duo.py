@@ -133,30 +133,3 @@ def test_f64duo_partner_timeout_is_recomputed(oracle):
         ctx.GPUClean()
         orc.close()
 
-
-def test_f64duo_other_handoff_form(oracle):
-    """The hand-off form the product build does not use (test library, probe 8: data-tagged granules vs the
-    workgroup flag) computes the same outputs, and its missing-partner path (probe 9) is recomputed by the
-    rescue."""
-    import tfhe_amd
-
-    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(93))
-    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    try:
-        a, acc = _inputs(op, 9, 710)
-        want = orc.eval_acc(a, 2 * op.N, acc)
-        with ctx.knobs_set(probe=8):
-            assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
-        a2, acc2 = _inputs(op, 128, 711, amod=1024)
-        with ctx.knobs_set(probe=8):
-            alt = ctx.EvalAcc(a2, 1024, acc2)
-        assert np.array_equal(alt, ctx.EvalAcc(a2, 1024, acc2))
-        with ctx.knobs_set(probe=9):
-            assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
-        assert ctx.info().duo_timeouts >= 1
-    finally:
-        ctx.GPUClean()
-        orc.close()

@@ -702,7 +702,6 @@ __device__ __forceinline__ double duo_load_d(const double* p) {
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
-constexpr bool kF64DuoGran = false;  // the hand-off form of the product build (probe 8 runs the other)
 
 // STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
 // (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
@@ -710,23 +709,12 @@ constexpr bool kF64DuoGran = false;  // the hand-off form of the product build (
 // partner that never arrives would, and the polls are bounded 2^14 times.  PROBE 2 (timing only, results
 // invalid): no hand-off at all -- each member takes its own stage-1 values for its partner's -- the
 // bound on what the exchange costs per round
-// GRAN: the hand-off as data-tagged granules (MI355X_MICROARCH.md "handoff-1to1") instead of a flag: each
-// value travels with its round number in one 8-byte word (52-bit offset value + 12-bit tag, one sc1 store),
-// and each thread polls its partner thread's 4 words -- all four loads in flight per poll -- with no drain,
-// barrier, flag and second barrier per round.  Correct without a workgroup-wide order: thread t's
-// round-(i+2) store to a parity buffer depends (through the data) on its round-(i+1) loads, which the
-// partner's thread t made only after its round-i loads.  (Measured against the workgroup flag: a first
-// granule form polling the four words one after another 8.03 us per round at 128 against 7.71, a
-// one-flag-per-wavefront form 8.8-9.2 against 7.5-7.6; profiles/r05g, r05h.)
-[[maybe_unused]] __device__ __forceinline__ uint64_t gran_pack(double x, uint32_t tag) {  // |x| < 2^51, integer-valued
-    const double y = __dadd_rn(x, 0x1.8p52);                            // mantissa = x + 2^51, exactly
-    return (__builtin_bit_cast(uint64_t, y) & ((1ull << 52) - 1)) | ((uint64_t)tag << 52);
-}
-[[maybe_unused]] __device__ __forceinline__ double gran_value(uint64_t g) {
-    return __dsub_rn(__builtin_bit_cast(double, (g & ((1ull << 52) - 1)) | (0x433ull << 52)), 0x1.8p52);
-}
-
-template <int PROBE = 0, bool GRAN = false>
+// The hand-off is one flag per member per round (workgroup barrier, t == 0 stores / polls, barrier).  Forms
+// measured against it and removed (tools/duo_probe.py, us per round at 128 ciphertexts): data-tagged granules
+// (value + round tag in one 8-byte word, no flag or barriers) polling the four words one after another 8.03
+// against 7.71, the same with all four loads in flight per poll 7.56-7.71 against 7.51-7.66 (a tie), one flag
+// per wavefront with no workgroup barrier 8.8-9.2 against 7.5-7.6 (profiles/r05g, r05h, r05i).
+template <int PROBE = 0>
 __global__ void __launch_bounds__(512, 2)
 k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, const uint64_t* __restrict__ a,
                        uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X, uint32_t pairs) {
@@ -742,7 +730,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     double* mt = cx + 2 * H;     // monomial tables
     uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n]
     __shared__ int wflag[2];
-    __shared__ uint32_t duo_ok, duo_dead;
+    __shared__ uint32_t duo_ok;
     const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6, twoN = 2 * N, logG = P.logG;
     const uint32_t j = w >> 2;                                // this wave's polynomial / column
     const uint32_t u4 = 4 * (256 * h + 64 * (w & 3) + l);     // this lane's slots u4 .. u4+3 (whole ring)
@@ -775,8 +763,6 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         acc[k] = (double)(v < Qhalf ? (int64_t)v : (int64_t)v - Qs);
     }
     if (t < 2) wflag[t] = 0;
-    if (t == 0) duo_dead = 0;
-    bool gone_t = false;  // GRAN: this thread's partner words timed out once (later rounds skip the wait)
     stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
     __syncthreads();
     double Cn[4];  // N^-1 NTT(acc_j) at the lane's slots
@@ -885,50 +871,10 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         double* mine = reinterpret_cast<double*>(X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N);
         const double* theirs = reinterpret_cast<const double*>(X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N);
         double lo[4], hi[4];
-        if constexpr (GRAN) {
-            uint64_t* gm = reinterpret_cast<uint64_t*>(mine);
-            const uint64_t* gt = reinterpret_cast<const uint64_t*>(theirs);
-            const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
-            double pv[4] = {o[0], o[1], o[2], o[3]};
-            if constexpr (PROBE != 2) {
-                if (!gone) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        __hip_atomic_store(gm + 512 * k + t, gran_pack(fred(o[k], K), i + 1), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
-                constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kF64DuoMaxPolls;
-                uint64_t gv[4];
-                uint32_t polls = gone_t ? kMaxPolls : 0;
-                for (;;) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        gv[k] = __hip_atomic_load(const_cast<uint64_t*>(gt + 512 * k + t), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                    const bool ready = (gv[0] >> 52) == i + 1 && (gv[1] >> 52) == i + 1 && (gv[2] >> 52) == i + 1 &&
-                                       (gv[3] >> 52) == i + 1;
-                    if (ready || ++polls >= kMaxPolls) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                if (polls >= kMaxPolls && !gone_t) {
-                    gone_t = true;
-                    duo_dead = 1;  // (benign race: any thread's 1)
-                    __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) pv[k] = gran_value(gv[k]);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                lo[k] = h ? pv[k] : o[k];
-                hi[k] = h ? o[k] : pv[k];
-            }
-        }
-        if constexpr (!GRAN && PROBE != 2) {
+        if constexpr (PROBE != 2) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) duo_store_d(mine + 512 * k + t, o[k]);
         }
-        if constexpr (!GRAN) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's stores drained; every read of the inverse buffer done
         if (PROBE != 2 && t == 0) {
@@ -956,7 +902,6 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             lo[k] = h ? pv : o[k];
             hi[k] = h ? o[k] : pv;
         }
-        }  // !GRAN
         const double w0 = ipsi[1];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // stage 0 for all coefficients, then f64w's accumulator update
@@ -970,7 +915,6 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         }
     }
     __syncthreads();
-    if (GRAN && t == 0 && duo_dead) __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // member h writes polynomial h (acc0 transposed, poly.cpp:762-770) through the two buffers (N doubles)
     double* st = bf;
     if (pp == h) {
@@ -1143,7 +1087,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
         // round-2 race, wrong results) and a timing-only build (4: STD192 without the barrier before
         // digit 1's pass A, results invalid; tools/f64w_barrier_probe.sh)
-        if (kn.probe != 0 && (kn.probe < 5 || kn.probe == 6)) {  // (5, 7, 8, 9: the duo probes, below)
+        if (kn.probe != 0 && (kn.probe < 5 || kn.probe == 6)) {  // (5, 7: the duo probes, below)
             if (kn.probe == 4 && !red && !wrap && ld == 2) gow(k_blind_rotate_f64w<false, false, 2, 4>);
             else if (kn.probe == 2 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 2>);
             else if (kn.probe == 3 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 3>);
@@ -1157,19 +1101,11 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             const DuoBuf X = duo_layout(duo);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
             const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
-            constexpr bool G = kF64DuoGran;
-            auto dk = k_blind_rotate_f64wduo<0, G>;
-            bool gran = G;
+            auto dk = k_blind_rotate_f64wduo<0>;
 #ifdef TFHE_TEST_PROBES
-            if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1, G>;  // test library only: a partner that never arrives
-            if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2, G>;  // timing only: no hand-off (results invalid)
-            if (kn.probe == 8) dk = k_blind_rotate_f64wduo<0, !G>, gran = !G;  // the other hand-off form (A/B)
-            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<1, !G>, gran = !G;  // ... with the missing partner
+            if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
+            if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
 #endif
-            if (gran) {  // tags are round numbers (12 bits): a stale word of an earlier launch must not match
-                if (P.n >= 4095) return hipErrorNotSupported;
-                if (hipError_t e = hipMemsetAsync(X.xbuf, 0, (size_t)B * 4 * kDuoN * 8, s); e != hipSuccess) return e;
-            }
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
                                a, amod, acc, X, (uint32_t)B);

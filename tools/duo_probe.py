@@ -5,8 +5,6 @@ Test library (lib/libtfhe_hip_test.so): STD128Q, device-resident blind rotation 
 (min of --reps, HIP stream sync) for
   one   f64w, one workgroup per ciphertext (duo = 0)
   duo   f64wduo (the default for B <= 128)
-  alt   f64wduo with the other hand-off form (probe 8: data-tagged granules if the product build uses the
-        workgroup flag, and the reverse)
   free  f64wduo with NO hand-off (probe 7: each member takes its own stage-1 values for its partner's;
         results invalid) -- the lower bound of the duo form, i.e. the exchange's price per round.
 One JSON line.
@@ -45,7 +43,7 @@ def main():
         a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
         acc0 = torch.randint(0, int(p.Q), (B, 2, p.N), dtype=torch.int64, device=dev, generator=g)
         row = {"B": B}
-        for tag, knobs in (("one", {"duo": 0}), ("duo", {}), ("alt", {"probe": 8}), ("free", {"probe": 7})):
+        for tag, knobs in (("one", {"duo": 0}), ("duo", {}), ("free", {"probe": 7})):
             acc = acc0.clone()
             with ctx.knobs_set(**knobs):
                 ts = []
