@@ -669,14 +669,17 @@ k_blind_rotate_gen3(BRParams P, const W* __restrict__ psi, const W* __restrict__
 //     r = (S mod 2^55) + (S >> 55) 2c  < 2^55 + 2^33 c
 // -- five v_mad_u64_u32 and no quotient estimate, against ten multiplies for the u64 Shoup
 // product (round 4: nine VALU, device_math.hpp sf_mul).  Values stay unsigned and lazy: the
-// forward transform needs no reduction at all (y' = x + 3Q - v, 11 stages < 35 Q), the inverse
+// forward transform needs no reduction and no offset (its inputs carry 28Q, so y' = x - v stays
+// non-negative through 11 stages; outputs < 54 Q -- round 5: one VALU per butterfly less than
+// x + (3Q - v)), the inverse
 // folds its pure sums once per pass (x -> (x mod 2^54) + (x >> 54) c, one mad), the accumulator
 // update folds once and subtracts Q at most once.  tools/bounds_sf.py checks every bound of
 // this schedule.
 // (SF_K and sf_mul live in device_math.hpp, shared with the VALU microbenchmark)
 
 struct SfC {
-    uint64_t Q, Q3, Q10;  // Q, 3Q (forward offset), 10Q (inverse and monomial offsets; tools/bounds_sf.py)
+    uint64_t Q, Q3, Qf, Q10;  // Q, 3Q (sf2p's forward offset), 28Q (what the other forward transforms'
+                              // inputs carry), 10Q (inverse and monomial offsets; tools/bounds_sf.py)
     uint32_t c2;          // 2c: sf_mul folds at 2^55
     uint32_t c;
 };
@@ -735,10 +738,15 @@ __device__ __forceinline__ uint64_t sf_mono_pair(uint64_t A0, uint32_t e0, uint6
     return sf_fold(p0 + p1 + (K.Q10 - sf_fold(A0 + A1, K.c)), K.c);
 }
 
-template <class TW>
+// OFS: the round-4 form, the offset in the difference (inputs r + Q, outputs < 35 Q), kept for sf2p and
+// sf2duo: the offset-free form (89 / 46 fewer VALU per round there) measured 0.5 % / 0.9 % slower -- their
+// rounds wait at barriers or on the partner, and in sf2p the allocator added three scratch loads to the
+// loop (profiles/r05j, r05k).  sf2 and gen3sf use the offset-free form (C3 -1.3 %).
+template <bool OFS = false, class TW>
 __device__ __forceinline__ void sf_ct(uint64_t& x, uint64_t& y, const TW& T, uint32_t i, const SfC& K) {
     const uint64_t v = sf_mul(y, tw0(T, i), tw1(T, i), K.c2);
-    y = x + (K.Q3 - v);
+    if constexpr (OFS) y = x + (K.Q3 - v);
+    else y = x - v;  // x >= 28Q - 11 x 2.3Q: no offset (tools/bounds_sf.py)
     x = x + v;
 }
 template <bool FOLD = false, class TW>
@@ -748,14 +756,14 @@ __device__ __forceinline__ void sf_gs(uint64_t& x, uint64_t& y, const TW& T, uin
     y = sf_mul(d, tw0(T, i), tw1(T, i), K.c2);
 }
 
-template <class TW>
+template <bool OFS = false, class TW>
 __device__ __forceinline__ void sf_fwd_core(uint64_t (&v)[8], uint32_t m0, uint32_t g, const TW& T, const SfC& K) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sf_ct(v[k], v[k + 4], T, m0 + g, K);
-    sf_ct(v[0], v[2], T, 2 * m0 + 2 * g, K), sf_ct(v[1], v[3], T, 2 * m0 + 2 * g, K);
-    sf_ct(v[4], v[6], T, 2 * m0 + 2 * g + 1, K), sf_ct(v[5], v[7], T, 2 * m0 + 2 * g + 1, K);
+    for (int k = 0; k < 4; ++k) sf_ct<OFS>(v[k], v[k + 4], T, m0 + g, K);
+    sf_ct<OFS>(v[0], v[2], T, 2 * m0 + 2 * g, K), sf_ct<OFS>(v[1], v[3], T, 2 * m0 + 2 * g, K);
+    sf_ct<OFS>(v[4], v[6], T, 2 * m0 + 2 * g + 1, K), sf_ct<OFS>(v[5], v[7], T, 2 * m0 + 2 * g + 1, K);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sf_ct(v[2 * j], v[2 * j + 1], T, 4 * m0 + 4 * g + j, K);
+    for (int j = 0; j < 4; ++j) sf_ct<OFS>(v[2 * j], v[2 * j + 1], T, 4 * m0 + 4 * g + j, K);
 }
 // FOLD: fold the last stage's sums (inverse passes C and B; bounds_sf.py INV_FOLD_PASS)
 template <bool FOLD, class TW>
@@ -901,9 +909,8 @@ k_blind_rotate_gen3sf(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
                     const uint64_t x = acc[p][k];
                     const int64_t c = x < Qhalf ? (int64_t)x : (int64_t)x - Qs;
                     const int64_t d = (c + Kd) >> shift;
-                    int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
-                    if (r < 0) r += Qs;
-                    v[p * CN + k] = (uint64_t)r;
+                    const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
+                    v[p * CN + k] = (uint64_t)r + (r < 0 ? K.Qf + Q : K.Qf);  // r mod Q + 28Q
                 }
             sf_ntt_fwd(buf, v, TF, K);  // pass A writes this thread's own entries: no barrier before
             // rows 2l (poly 0) and 2l+1 (poly 1), both keys, both columns; group g = (slot k, key kk)
@@ -991,7 +998,7 @@ __device__ __forceinline__ void wl_sync() {  // order this wave's LDS accesses (
 // TO_LDS: the units' outputs stay in the buffer (read back by this wave's products)
 // PAIR: two ciphertexts per 1024-thread workgroup (k_blind_rotate_sf2p): the thread's index within its
 // ciphertext's 512 threads
-template <bool TO_LDS = false, class TW = SfTw, bool PAIR = false>
+template <bool TO_LDS = false, class TW = SfTw, bool PAIR = false, bool OFS = PAIR>
 __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uint64_t (&d)[2][4], const TW& T,
                                             const SfC& K) {
     constexpr uint32_t N = G3_N;
@@ -1001,7 +1008,7 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
         uint64_t* p = buf + (t >> 8) * N;
         uint32_t ad[8];
         g3_ad(0, tau, ad);
-        sf_fwd_core(v, 1, 0, T, K);
+        sf_fwd_core<OFS>(v, 1, 0, T, K);
 #pragma unroll
         for (int k = 0; k < 8; ++k) p[ad[k]] = v[k];
     }
@@ -1016,8 +1023,8 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
         uint64_t x[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) x[k] = p[ad[k]];
-        if (pass == 1) sf_fwd_core(x, 8, tw >> 5, T, K);
-        else sf_fwd_core(x, 64, tw >> 2, T, K);
+        if (pass == 1) sf_fwd_core<OFS>(x, 8, tw >> 5, T, K);
+        else sf_fwd_core<OFS>(x, 64, tw >> 2, T, K);
 #pragma unroll
         for (int k = 0; k < 8; ++k) p[ad[k]] = x[k];
         wl_sync();
@@ -1027,8 +1034,8 @@ __device__ __forceinline__ void sf2_ntt_fwd(uint64_t* buf, uint64_t (&v)[8], uin
     for (int q = 0; q < 2; ++q) {  // stages 9 (h = 2) and 10 (h = 1) on slots 4u .. 4u+3
         const uint64_t* pq = buf + q * N;
         uint64_t v0 = pq[u0], v1 = pq[u0 ^ 1], v2 = pq[u0 ^ 2], v3 = pq[u0 ^ 3];
-        sf_ct(v0, v2, T, N / 4 + u, K), sf_ct(v1, v3, T, N / 4 + u, K);
-        sf_ct(v0, v1, T, N / 2 + 2 * u, K), sf_ct(v2, v3, T, N / 2 + 2 * u + 1, K);
+        sf_ct<OFS>(v0, v2, T, N / 4 + u, K), sf_ct<OFS>(v1, v3, T, N / 4 + u, K);
+        sf_ct<OFS>(v0, v1, T, N / 2 + 2 * u, K), sf_ct<OFS>(v2, v3, T, N / 2 + 2 * u + 1, K);
         if constexpr (TO_LDS) {
             uint64_t* pw = buf + q * N;
             pw[u0] = v0, pw[u0 ^ 1] = v1, pw[u0 ^ 2] = v2, pw[u0 ^ 3] = v3;
@@ -1144,8 +1151,8 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
     // the decomposition's offsets: digit l of x is that of c + Kd_l, c = x or x - Q (centred), i.e. of
-    // x + (x < Q/2 ? Kd_l : Kd_l - Q); the digit r in [-B/2, B/2) enters the transform as r + Q (< 2Q,
-    // congruent, no sign test; tools/bounds_sf.py starts the forward transform at 2Q)
+    // x + (x < Q/2 ? Kd_l : Kd_l - Q); the digit r in [-B/2, B/2) enters the transform as r + 28Q
+    // (congruent, no sign test; the offset the transform's differences consume, tools/bounds_sf.py)
     int64_t Kdl[DIG];
 #pragma unroll
     for (int l = 0; l < DIG; ++l) {
@@ -1175,7 +1182,7 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
                     const uint64_t x = acc[p][k];
                     const int64_t d = ((int64_t)x + (x < Qhalf ? Klo : Khi)) >> shift;
                     const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
-                    v[p * CN + k] = (uint64_t)(r + Qs);
+                    v[p * CN + k] = (uint64_t)r + K.Qf;
                 }
             if (l > 0) __syncthreads();  // other waves may still read their blocks of digit l - 1
             // one digit: its outputs stay in LDS (frees 16 VGPRs; C3 18.8K -> 20.0K); two digits:
@@ -1356,7 +1363,7 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
                     const uint64_t x = acc[p][k];
                     const int64_t d = ((int64_t)x + (x < Qhalf ? Klo : Khi)) >> shift;
                     const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
-                    v[p * CN + k] = (uint64_t)(r + Qs);
+                    v[p * CN + k] = (uint64_t)(r + Qs);  // sf_ct<true>: inputs r + Q
                 }
             if (l > 0) __syncthreads();
             if (LAST_LDS && l == DIG - 1) sf2_ntt_fwd<true, SfTwB, true>(buf, v, D[l], TF, K);
@@ -1530,11 +1537,11 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             const uint64_t xv = acc[k];
             const int64_t d = ((int64_t)xv + (xv < Qhalf ? Klo : Khi)) >> shift;
             const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
-            v[k] = (uint64_t)(r + Qs);
+            v[k] = (uint64_t)(r + Qs);  // sf_ct<true>: inputs r + Q
         }
         uint64_t D[2][4];  // D[l][s]: digit l of acc_x at slots u4 + s
         if (i > 0) __syncthreads();  // every thread has read the previous round's exchange from the buffer
-        sf2_ntt_fwd(buf, v, D, TF, K);
+        sf2_ntt_fwd<false, SfTw, false, true>(buf, v, D, TF, K);
         // products: group g = (column j, key kk, digit l: key row 2l + x), then column j's factors
         constexpr int RW = 2, NG = 4 * RW;
         auto kload = [&](int gi, uint64_t (&kw)[8]) {
@@ -1740,7 +1747,7 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
     if (B == 0) return hipSuccess;
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
     SfC K;
-    K.Q = P.Q, K.Q3 = 3 * P.Q, K.Q10 = 10 * P.Q;
+    K.Q = P.Q, K.Q3 = 3 * P.Q, K.Qf = 28 * P.Q, K.Q10 = 10 * P.Q;
     K.c = (uint32_t)((1ull << SF_K) - P.Q);
     K.c2 = 2 * K.c;
     const uint64_t* w1 = (const uint64_t*)sf;

@@ -13,7 +13,8 @@ brings any x < 2^64 below 2^k + 2^(64-k) c.  This script walks the kernel's sche
 the worst-case bound of every element and checks
   * every value (product inputs included) is below 2^64,
   * H < 2^55, so the folded quotient S >> 55 fits the mad's 32-bit multiplier,
-  * the offsets kQ of the subtractions keep every difference non-negative,
+  * the offsets kQ of the subtractions (the forward's: the 28Q its inputs carry) keep every difference
+    non-negative,
   * the accumulator update lands in [0, Q) after one fold and one conditional subtraction.
 Usage: python3 tools/bounds_sf.py   (exit 1 on a violation; run by tests/test_layouts.py)
 """
@@ -60,11 +61,16 @@ def fold(x):
     return (1 << K) - 1 + (x >> K) * A.C
 
 
+FWD_OFF = 28   # digits enter the forward transform as r + 28Q (gen3sf: r + 28Q or r + 29Q)
+
+
 def ct(x, y):
-    v = mulw(y)
-    if v > 3 * A.Q:
-        fail("forward offset 3Q below the product bound")
-    return x + v, x + 3 * A.Q          # y' = x + 3Q - v
+    """x, y: (lower, upper) bounds.  y' = x - v with no offset: the transform's inputs carry FWD_OFF Q,
+    and the lower bound of every difference must stay >= 0 (it falls by the product bound per stage)"""
+    v = mulw(y[1])
+    if x[0] - v < 0:
+        fail(f"forward difference may go negative (lower bound {x[0] / A.Q:.2f} Q, product < {v / A.Q:.2f} Q)")
+    return (x[0], x[1] + v), (x[0] - v, x[1])
 
 
 def gs(x, y, fold_sum):
@@ -75,24 +81,35 @@ def gs(x, y, fold_sum):
     return (fold(s) if fold_sum else s), mulw(d)
 
 
-# forward radix-8 (stages (k, k+4), (0,2)(1,3)(4,6)(5,7), (2j, 2j+1)) on uniform input bound x
+def ct_ofs(x, y):
+    """sf2p's and sf2duo's (round-4) form: y' = x + 3Q - v, inputs r + Q (no lower bound needed)"""
+    v = mulw(y[1])
+    if v > 3 * A.Q:
+        fail("forward offset 3Q below the product bound")
+    return (0, x[1] + v), (0, x[1] + 3 * A.Q)
+
+
+CT = ct
+
+
+# forward radix-8 (stages (k, k+4), (0,2)(1,3)(4,6)(5,7), (2j, 2j+1)) on uniform input bounds x = (lo, hi)
 def fwd_r8(x):
     v = [x] * 8
     for k in range(4):
-        v[k], v[k + 4] = ct(v[k], v[k + 4])
+        v[k], v[k + 4] = CT(v[k], v[k + 4])
     for (a, b) in ((0, 2), (1, 3), (4, 6), (5, 7)):
-        v[a], v[b] = ct(v[a], v[b])
+        v[a], v[b] = CT(v[a], v[b])
     for j in range(4):
-        v[2 * j], v[2 * j + 1] = ct(v[2 * j], v[2 * j + 1])
+        v[2 * j], v[2 * j + 1] = CT(v[2 * j], v[2 * j + 1])
     return v
 
 
 def fwd_r4(x):
     v = [x] * 4
     for (a, b) in ((0, 2), (1, 3)):
-        v[a], v[b] = ct(v[a], v[b])
+        v[a], v[b] = CT(v[a], v[b])
     for (a, b) in ((0, 1), (2, 3)):
-        v[a], v[b] = ct(v[a], v[b])
+        v[a], v[b] = CT(v[a], v[b])
     return v
 
 
@@ -130,10 +147,18 @@ def model(rows, sf2=True, form="sf2"):
     polynomial's rows only -- `rows` digits x 1 polynomial -- and its accumulator update adds its own
     column's inverse output and the partner's: acc + own + partner, one fold, one conditional subtraction)."""
     Q = A.Q
-    x = 2 * Q if sf2 else Q     # sf2: digits r + Q, r in [-B/2, B/2); gen3sf: canonical digits
+    # sf2: digits r + 28Q, r in [-B/2, B/2), |r| <= Q/2 for any base the path admits; gen3sf: r mod Q + 28Q;
+    # sf2p, sf2duo: r + Q with the offset in the difference (ct_ofs)
+    global CT
+    CT = ct_ofs if form in ("sf2p", "duo") else ct
+    x = (FWD_OFF * Q - Q // 2, FWD_OFF * Q + Q // 2) if sf2 else (FWD_OFF * Q, (FWD_OFF + 1) * Q)
+    if form in ("sf2p", "duo"):
+        x = (0, 2 * Q)
     for _ in range(3):
-        x = max(fwd_r8(x))
-    D = max(fwd_r4(x))
+        v = fwd_r8(x)
+        x = (min(e[0] for e in v), max(e[1] for e in v))
+    v = fwd_r4(x)
+    D = max(e[1] for e in v)
     R = mulw(D)
     Ap = rows * (1 if form == "duo" else 2) * R   # rows digits x polynomials per (key, column)
     if form == "sf2p":

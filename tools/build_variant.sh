@@ -12,6 +12,6 @@ F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-resu
 /opt/rocm/bin/hipcc $F -mllvm -pragma-unroll-threshold=100000 $DEFS -c csrc/blind_rotate_generic.hip -o $O/blind_rotate_generic.o &
 /opt/rocm/bin/hipcc $F $DEFS -c csrc/blind_rotate_f64.hip -o $O/blind_rotate_f64.o &
 wait
-OBJS=$(ls build/*.o | grep -v -e blind_rotate_generic.o -e blind_rotate_f64.o -e blind_rotate_f64_probes.o)
+OBJS=$(ls build/*.o | grep -v -e blind_rotate_generic.o -e blind_rotate_f64.o -e _probes.o)
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -pthread -o ../altlib/libtfhe_hip_$NAME.so $OBJS $O/blind_rotate_generic.o $O/blind_rotate_f64.o
 echo "altlib/libtfhe_hip_$NAME.so"
