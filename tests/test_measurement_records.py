@@ -105,3 +105,41 @@ def test_r04_bench_lines_reproduce_their_roofline():
         assert cb["kind"] == "reference" and cb["gpu_parity"]["bit_exact"], cfg
         assert line["dist"]["world_size"] == 1 and line["n_gpus"] == 1, cfg
         assert line["value"] > 100 * cb["value"], cfg
+
+
+# ---- round 5: the final per-configuration records (profiles/r05x, profiles/r05_pmc_*.json) ----
+def test_r05_pmc_records_are_consistent():
+    for cfg, (units, *_rest) in R04_CONFIGS.items():
+        pmc = json.load(open(os.path.join(ROOT, "profiles", f"r05_pmc_{cfg}.json")))
+        assert pmc["units_per_launch"] == units, cfg
+        t = pmc["gui_pass_kernel_ns_per_launch"] * 1e-9
+        held = pmc["grbm_gui_active_per_launch"] / 8 / t / 1e9
+        assert 1.0 < held <= MI355X_MAX_CLOCK_GHZ, (cfg, held)
+        busy = pmc["sq_active_inst_valu_per_launch"] * 4 / 1024 / (pmc["grbm_gui_active_per_launch"] / 8)
+        assert 0.5 < busy <= 1.05, (cfg, busy)
+        assert pmc["hbm_bytes_per_launch"] / t < 8e12, cfg
+
+
+def test_r05_bench_lines_reproduce_their_roofline_and_checked_their_outputs():
+    peaks = json.load(open(os.path.join(ROOT, "profiles", "r04_valu_peak.json")))["peaks"]
+    for cfg, (units, n, N, dG2, fam) in R04_CONFIGS.items():
+        line = json.load(open(os.path.join(ROOT, "profiles", "r05x", f"bench_{cfg}.json")))
+        r = line["roofline"]
+        assert r["units_per_launch"] == units and r["peak_family"] == fam, cfg
+        assert r["alg_modmul_per_unit"] == _alg_modmul(n, N, dG2), cfg
+        achieved = r["alg_modmul_per_unit"] * units / (r["kernel_ms"] * 1e-3)
+        assert abs(achieved / 1e12 - r["achieved"]) < 0.01, cfg
+        assert abs(r["frac"] - achieved / peaks[fam]["modmul_per_s"]) < 0.002 and 0 < r["frac"] <= 1, cfg
+        assert r["traffic"] is not None, cfg  # read from the r05 PMC record of the same build
+        assert line["parity_ok"] is True and line["parity_failed"] == [], cfg
+        assert line["oracle_sample"]["ranks_passed"] == line["oracle_sample"]["ranks_checked"] == 1, cfg
+        cb = line["cpu_baseline"]
+        assert cb["kind"] == "reference" and cb["gpu_parity"]["bit_exact"], cfg
+        assert cb["single_thread_value"] and 0 < cb["single_thread_value"] < cb["value"], cfg
+        assert line["value"] > 100 * cb["value"], cfg
+        # the event-timed blind rotation agrees with rocprof's average for the same kernel (+-5 %)
+        import csv
+        rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r05x", f"kernel_stats_{cfg}.csv"))))
+        br = [row for row in rows if "k_blind_rotate" in row["Name"]]
+        top = max(br, key=lambda row: float(row["TotalDurationNs"]))
+        assert abs(float(top["AverageNs"]) * 1e-6 / r["kernel_ms"] - 1) < 0.05, cfg
