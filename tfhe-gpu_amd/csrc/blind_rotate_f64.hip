@@ -286,6 +286,9 @@ __device__ __forceinline__ void f64w_ntt_inv(double* buf, const double (&s)[2][4
 // ciphertext 0's acc1[0] (the extracted b: large enough to survive every modulus switch after it)
 // RESCUE (launched behind every f64wduo launch): only the ciphertexts whose duo pair timed out (the pair's
 // failed word, kernels.hpp DuoBuf) run, from their saved inputs; the others exit at once
+#ifndef F64W_KPRE
+#define F64W_KPRE 0
+#endif
 template <bool RED, bool WRAP, int LD, int PROBE = 0, bool RESCUE = false>
 __global__ void __launch_bounds__(512, 4)
 k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, const uint32_t* __restrict__ /*eidx*/,
@@ -379,6 +382,21 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
         // rotation exponent staged in LDS (no 64-bit remainder in the round loop)
         const uint32_t ai = ex[i];
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
+        // products: group g = (column j, key kk, row r), rows 0 .. 2LD-1 the digits', 2LD, 2LD+1
+        // the C' rows; 4 slots of key words each, the next group's loaded first
+        constexpr int RW = 2 * LD + 2, NG = 4 * RW;
+        auto kload = [&](int gi, double (&kv)[4]) {
+            const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
+            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
+            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
+        };
+        // F64W_KPRE = d > 0: the first d key groups requested at the top of the round (a ring of d + 1)
+        constexpr int KD = F64W_KPRE > 0 ? F64W_KPRE : 1, KR = KD + 1;
+        double kv[KR][4];
+#pragma unroll
+        for (int g = 0; g < (F64W_KPRE > 0 ? KD : 0); ++g) kload(g, kv[g]);
         double D[LD][2][4];  // digits before the last; the last digit's outputs stay in LDS
         // digit l (CORR: the WRAP correction -2^(gL) N^-1 w): extraction, forward transform
         auto digit = [&](uint32_t l, auto corr_c, double (&d)[2][4], bool sync) {
@@ -434,28 +452,17 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 digit(LD - 1, F_{}, D[LD - 1], true);
             }
         }
-        // products: group g = (column j, key kk, row r), rows 0 .. 2LD-1 the digits', 2LD, 2LD+1
-        // the C' rows; 4 slots of key words each, the next group's loaded first
-        constexpr int RW = 2 * LD + 2, NG = 4 * RW;
-        auto kload = [&](int gi, double (&kv)[4]) {
-            const uint32_t j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
-            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
-            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
-            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
-            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
-        };
         uint32_t ip[4];  // slot x evaluates at psi^(2 bitrev(x) + 1) (recomputed each round, the
         uint32_t uo = u4;  // opaque copy keeps the compiler from hoisting four live values)
         asm volatile("" : "+v"(uo));
 #pragma unroll
         for (int q = 0; q < 4; ++q) ip[q] = ((2 * (__builtin_bitreverse32(uo + q) >> 21) + 1) * ai) & (twoN - 1);
         double S[2][4], A[2][4];
-        double kv[2][4];
         double Wp[4], Wm[4];  // psi^e - 1, psi^-e - 1 at the 4 slots (built at j = 0)
-        kload(0, kv[0]);
+        if constexpr (F64W_KPRE == 0) kload(0, kv[0]);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
-            if (gi + 1 < NG) kload(gi + 1, kv[(gi + 1) & 1]);
+            if (gi + KD < NG) kload(gi + KD, kv[(gi + KD) % KR]);
             __builtin_amdgcn_sched_barrier(0);
             const int j = gi / (2 * RW), kk = (gi / RW) & 1, r = gi % RW;
 #pragma unroll
@@ -463,7 +470,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
                 const double dv = r < 2 * LD - 2 ? D[r >> 1][r & 1][q]
                                   : r < 2 * LD   ? buf[(r & 1) * N + (swz(u4) ^ q)]
                                                  : Cx[r & 1][q];
-                const double pr = fmodmul(dv, kv[gi & 1][q], K);
+                const double pr = fmodmul(dv, kv[gi % KR][q], K);
                 A[kk][q] = r == 0 ? pr : __dadd_rn(A[kk][q], pr);
             }
             if (kk == 1 && r == RW - 1) {
@@ -702,6 +709,9 @@ __device__ __forceinline__ double duo_load_d(const double* p) {
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
+#ifndef F64D_KPRE
+#define F64D_KPRE 4
+#endif
 
 // STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
 // (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
@@ -732,7 +742,9 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     __shared__ int wflag[2];
     __shared__ uint32_t duo_ok;
     const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6, twoN = 2 * N, logG = P.logG;
-    const uint32_t j = w >> 2;                                // this wave's polynomial / column
+    // this wave's polynomial / column, wave-uniform: through readfirstlane the key loads' row offset is an
+    // SGPR (as w >> 2 the compiler wrapped each of the 16 key loads per round in a waterfall loop)
+    const uint32_t j = __builtin_amdgcn_readfirstlane(w >> 2);
     const uint32_t u4 = 4 * (256 * h + 64 * (w & 3) + l);     // this lane's slots u4 .. u4+3 (whole ring)
     const uint32_t sp = j * H + 256 * (w & 3);                // their buffer block
     for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
@@ -788,6 +800,23 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         const uint32_t ai = ex[i];
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
         double D[4], dum[4];
+        // products of column j: group gi = (key kk, row rr): rr 0 own digit, 1 the other's, 2 own C', 3 the other's
+        auto krow = [j](uint32_t rr) -> uint32_t { return rr == 0 ? j : rr == 1 ? 1 - j : rr == 2 ? 2 + j : 3 - j; };
+        auto kload = [&](int gi, double (&kv)[4]) {
+            const uint32_t kk = gi >> 2, r = krow(gi & 3);
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
+            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
+            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
+        };
+        // F64D_KPRE: the round's first key group is requested before the forward transform, so its L2
+        // latency overlaps the transform instead of opening the products (two waves per SIMD hide little)
+        // (F64D_KPRE = d groups in flight: the first d requested here, group g + d at product group g, a ring
+        // of d + 1; 0: the round-4 form, group 0 requested at the products)
+        constexpr int KD = F64D_KPRE > 0 ? F64D_KPRE : 1, KR = KD + 1 < 8 ? KD + 1 : 8;
+        double kv[KR][4];
+#pragma unroll
+        for (int g = 0; g < (F64D_KPRE > 0 ? KD : 0); ++g) kload(g, kv[g]);
         auto digit = [&](bool corr, double (&d)[4]) {
             double v[8];
             bool wv = false;
@@ -829,26 +858,17 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         const uint32_t so = (1 - j) * H + 256 * (w & 3);
 #pragma unroll
         for (int s = 0; s < 4; ++s) Do[s] = bf[so + dswz(4 * l + s)], Co[s] = cx[so + dswz(4 * l + s)];
-        // products of column j: group gi = (key kk, row rr): rr 0 own digit, 1 the other's, 2 own C', 3 the other's
-        auto krow = [j](uint32_t rr) -> uint32_t { return rr == 0 ? j : rr == 1 ? 1 - j : rr == 2 ? 2 + j : 3 - j; };
-        auto kload = [&](int gi, double (&kv)[4]) {
-            const uint32_t kk = gi >> 2, r = krow(gi & 3);
-            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
-            const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
-            const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
-            kv[0] = lo.x, kv[1] = lo.y, kv[2] = hi.x, kv[3] = hi.y;
-        };
-        double A[2][4], kv[2][4];
-        kload(0, kv[0]);
+        double A[2][4];
+        if constexpr (F64D_KPRE == 0) kload(0, kv[0]);
 #pragma unroll
         for (int gi = 0; gi < 8; ++gi) {
-            if (gi + 1 < 8) kload(gi + 1, kv[(gi + 1) & 1]);
+            if (gi + KD < 8) kload(gi + KD, kv[(gi + KD) % KR]);
             __builtin_amdgcn_sched_barrier(0);
             const int kk = gi >> 2, rr = gi & 3;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const double dv = rr == 0 ? D[s] : rr == 1 ? Do[s] : rr == 2 ? Cx[s] : Co[s];
-                const double pr = fmodmul(dv, kv[gi & 1][s], K);
+                const double pr = fmodmul(dv, kv[gi % KR][s], K);
                 A[kk][s] = rr == 0 ? pr : __dadd_rn(A[kk][s], pr);
             }
             __builtin_amdgcn_sched_barrier(0);

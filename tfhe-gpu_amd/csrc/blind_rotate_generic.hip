@@ -1475,8 +1475,13 @@ __device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
 
 // PROBE 1 (test library only, TFHE_TEST_PROBES; tests/test_gpu_duo.py): member 1 of pair 0 stops publishing
 // at round 2, as a partner that never arrives would, and the polls are bounded 2^14 times, not 2^24
+#ifndef SF2D_KPRE
+#define SF2D_KPRE 2
+#endif
+// one workgroup per CU at the batches it serves (<= kDuoMaxPairs pairs, default 128): two waves per SIMD, so
+// the register budget is 256 -- room for the key groups in flight (SF2D_KPRE)
 template <int PROBE = 0>
-__global__ void __launch_bounds__(G3_TH, 4)
+__global__ void __launch_bounds__(G3_TH, SF2D_KPRE >= 2 ? 2 : 4)
 k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                       const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
                       const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
@@ -1539,9 +1544,6 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             const int64_t r = (int64_t)((uint64_t)d << sh) >> sh;
             v[k] = (uint64_t)(r + Qs);  // sf_ct<true>: inputs r + Q
         }
-        uint64_t D[2][4];  // D[l][s]: digit l of acc_x at slots u4 + s
-        if (i > 0) __syncthreads();  // every thread has read the previous round's exchange from the buffer
-        sf2_ntt_fwd<false, SfTw, false, true>(buf, v, D, TF, K);
         // products: group g = (column j, key kk, digit l: key row 2l + x), then column j's factors
         constexpr int RW = 2, NG = 4 * RW;
         auto kload = [&](int gi, uint64_t (&kw)[8]) {
@@ -1556,20 +1558,29 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
             kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
         };
+        // SF2D_KPRE: the round's first key group is requested before the forward transform (its L2 latency
+        // overlaps the transform; two waves per SIMD hide little -- as f64wduo, blind_rotate_f64.hip)
+        // (SF2D_KPRE = d groups in flight, a ring of d + 1 groups; 0: group 0 requested at the products)
+        constexpr int KD = SF2D_KPRE > 0 ? SF2D_KPRE : 1, KR = KD + 1 < 8 ? KD + 1 : 8;
+        uint64_t kw[KR][8];
+#pragma unroll
+        for (int g = 0; g < (SF2D_KPRE > 0 ? KD : 0); ++g) kload(g, kw[g]);
+        uint64_t D[2][4];  // D[l][s]: digit l of acc_x at slots u4 + s
+        if (i > 0) __syncthreads();  // every thread has read the previous round's exchange from the buffer
+        sf2_ntt_fwd<false, SfTw, false, true>(buf, v, D, TF, K);
         uint32_t ip[4];
         uint32_t uo = u4;
         asm volatile("" : "+v"(uo));
 #pragma unroll
         for (int s = 0; s < 4; ++s) ip[s] = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
         uint64_t S[2][4], A[2][4];
-        uint64_t kw[2][8];
-        kload(0, kw[0]);
+        if constexpr (SF2D_KPRE == 0) kload(0, kw[0]);
 #pragma unroll
         for (int gi = 0; gi < NG; ++gi) {
-            if (gi + 1 < NG) kload(gi + 1, kw[(gi + 1) & 1]);
+            if (gi + KD < NG) kload(gi + KD, kw[(gi + KD) % KR]);
             __builtin_amdgcn_sched_barrier(0);
             const int j = gi / (2 * RW), kk = (gi / RW) & 1, l = gi % RW;
-            const uint64_t(&c)[8] = kw[gi & 1];
+            const uint64_t(&c)[8] = kw[gi % KR];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const uint64_t prod = sf_mul(D[l][s], c[s], c[4 + s], K.c2);
