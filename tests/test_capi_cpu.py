@@ -205,9 +205,10 @@ def test_environment_knobs_are_validated(env, why):
 
 
 @pytest.mark.parametrize("kernel,probes", [("k_blind_rotate_sf2duo", ["0", "1"]),
-                                            ("k_blind_rotate_f64wduo", ["0", "1", "2"])])
+                                            ("k_blind_rotate_f64wduo", ["0", "1", "2", "3"])])
 def test_product_library_has_no_duo_probe(capi, kernel, probes):
-    """The duo probes (1: a partner that never arrives; 2: f64wduo with no hand-off, timing only) are
+    """The duo probes (1: a partner that never arrives; 2: f64wduo with no hand-off, 3: broadcast factor
+    rows -- both timing only) are
     test-library instances only."""
     import re
     import subprocess

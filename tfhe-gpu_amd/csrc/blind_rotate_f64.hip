@@ -548,8 +548,11 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 // XORed with f(y[7:5]) so that every pass's 64-bit accesses are conflict-free per 32 lanes
 // (tools/lds_layouts_duo.py checks every pass).
 __device__ __forceinline__ uint32_t dswz(uint32_t x) {
-    const uint32_t z = (x >> 5) & 7;
-    return x ^ ((((z >> 1) & 1) << 4) | ((z & 3) << 2) | (z & 3));
+    // bit 5 -> bits 1, 3; bit 6 -> bit 4; bit 4 -> bits 0, 2: every b64 read conflict-free per 32-lane group
+    // (64 banks) AND every b64 write per 16-lane group (32 banks; MI355X_MICROARCH.md "LDS"), for every
+    // pass, the D / C' exchange and the units (tools/lds_layouts_duo.py; the round-5 first form, bits 5-7
+    // into bits 0-4 only, left the writes of passes (7,8), (10,9), (8,7) and the exchange 2-way)
+    return x ^ (((x >> 5) & 1) * 10u) ^ (((x >> 6) & 1) << 4) ^ (((x >> 4) & 1) * 5u);
 }
 
 // forward: v = coefficients tau + 256k of polynomial t >> 8 (all N) -> d = the NTT values of half h at this
@@ -878,7 +881,8 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         double S[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+            uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+            if constexpr (PROBE == 3) ip = ai & (twoN - 1);  // timing only: wave-uniform table rows
             const uint32_t in = (twoN - ip) & (twoN - 1);
             const double Wp = __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
             const double Wm = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
@@ -1107,7 +1111,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
         // (2: waves 1.. delayed in the prologue, barrier kept; 3: the same without the barrier -- the
         // round-2 race, wrong results) and a timing-only build (4: STD192 without the barrier before
         // digit 1's pass A, results invalid; tools/f64w_barrier_probe.sh)
-        if (kn.probe != 0 && (kn.probe < 5 || kn.probe == 6)) {  // (5, 7: the duo probes, below)
+        if (kn.probe != 0 && (kn.probe < 5 || kn.probe == 6)) {  // (5, 7, 9: the duo probes, below)
             if (kn.probe == 4 && !red && !wrap && ld == 2) gow(k_blind_rotate_f64w<false, false, 2, 4>);
             else if (kn.probe == 2 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 2>);
             else if (kn.probe == 3 && red && wrap && ld == 1) gow(k_blind_rotate_f64w<true, true, 1, 3>);
@@ -1125,6 +1129,7 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
             if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
+            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<3>;  // timing only: broadcast factor-table reads
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,

@@ -7,6 +7,8 @@ Test library (lib/libtfhe_hip_test.so): STD128Q, device-resident blind rotation 
   duo   f64wduo (the default for B <= 128)
   free  f64wduo with NO hand-off (probe 7: each member takes its own stage-1 values for its partner's;
         results invalid) -- the lower bound of the duo form, i.e. the exchange's price per round.
+  bcast f64wduo with wave-uniform monomial-factor rows (probe 9, results invalid): what the factor
+        tables' LDS bank conflicts cost.
 One JSON line.
 """
 import argparse
@@ -43,7 +45,7 @@ def main():
         a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
         acc0 = torch.randint(0, int(p.Q), (B, 2, p.N), dtype=torch.int64, device=dev, generator=g)
         row = {"B": B}
-        for tag, knobs in (("one", {"duo": 0}), ("duo", {}), ("free", {"probe": 7})):
+        for tag, knobs in (("one", {"duo": 0}), ("duo", {}), ("free", {"probe": 7}), ("bcast", {"probe": 9})):
             acc = acc0.clone()
             with ctx.knobs_set(**knobs):
                 ts = []

@@ -11,9 +11,10 @@ f64d_fwd / f64d_inv, k_blind_rotate_f64wduo).
    every index matters.
 2. Wave locality: every wave-local pass of wave w touches only its own 256-block (w & 3) of polynomial
    w >> 2's half buffer.
-3. LDS banks: every 64-bit access (gfx950: a b64 access is served per half-wave, 64 four-byte banks)
-   through dswz() touches 32 distinct double slots mod 32 per half-wave, for every pass and for the
-   products' reads of the other polynomial's slots.
+3. LDS banks (MI355X_MICROARCH.md "LDS"): every ds_read_b64 through dswz() touches 32 distinct double
+   slots mod 32 per 32-lane group (64 four-byte banks), and every ds_write_b64 16 distinct slots mod 16 per
+   16-lane group (32 banks), for every pass, the D / C' exchange (writes of this column's slots, reads of
+   the other polynomial's) and the units.
 Usage: python3 tools/lds_layouts_duo.py   (run by tests/test_layouts.py)
 """
 import random
@@ -23,8 +24,7 @@ N, H, TH, P = 2048, 1024, 512, 1000000007
 
 
 def dswz(x):
-    z = (x >> 5) & 7
-    return x ^ ((((z >> 1) & 1) << 4) | ((z & 3) << 2) | (z & 3))
+    return x ^ (((x >> 5) & 1) * 10) ^ (((x >> 6) & 1) << 4) ^ (((x >> 4) & 1) * 5)
 
 
 def ref_fwd(a, psi):
@@ -68,7 +68,8 @@ class Lds:
 
     def __init__(self):
         self.m = [None] * (2 * H)
-        self.trace = []  # (pass name, instruction index, thread, address)
+        self.trace = []   # reads: (pass name, instruction index), thread, address
+        self.wtrace = []  # writes
 
     def addr(self, poly, x):
         return poly * H + (x & ~255) + dswz(x & 255)
@@ -80,7 +81,7 @@ class Lds:
 
     def wr(self, tag, t, poly, x, v):
         a = self.addr(poly, x)
-        self.trace.append((tag, t, a))
+        self.wtrace.append((tag, t, a))
         self.m[a] = v
 
 
@@ -160,19 +161,20 @@ def inv_member(s, h, ipsi, lds, wl):
     return o
 
 
-def banks(trace):
+def banks(trace, group):
+    """worst number of distinct-address lanes on one bank within a lane group of `group` lanes: reads
+    group 32 (double slots mod 32), writes group 16 (slots mod 16)"""
     by = {}
     for tag, t, a in trace:
         by.setdefault(tag, {}).setdefault(t, []).append(a)
     worst = 1
     for tag, per in by.items():
-        n = len(per[0])
+        n = len(next(iter(per.values())))
         for i in range(n):
-            for w in range(8):
-                for half in range(2):
-                    slots = [per[t][i] % 32 for t in range(64 * w + 32 * half, 64 * w + 32 * half + 32) if t in per]
-                    if slots:
-                        worst = max(worst, max(slots.count(x) for x in set(slots)))
+            for g in range(TH // group):
+                slots = [per[t][i] % group for t in range(group * g, group * g + group) if t in per]
+                if slots:
+                    worst = max(worst, max(slots.count(x) for x in set(slots)))
     return worst
 
 
@@ -196,10 +198,11 @@ def main():
                 print(f"VIOLATION: forward member {h} thread {t} slots differ")
                 ok = False
                 break
-        # products read the other polynomial's slots (the kernel's Do / Co reads)
+        # the D / C' exchange: each lane writes its column's 4 slots, then reads the other polynomial's
         for t in range(TH):
             w, l = t >> 6, t & 63
             for k in range(4):
+                lds.wtrace.append((("xw", k), t, lds.addr(w >> 2, 256 * (w & 3) + 4 * l + k)))
                 lds.rd(("prod", k), t, 1 - (w >> 2), 256 * (w & 3) + 4 * l + k)
         s = {}
         for t in range(TH):
@@ -211,9 +214,9 @@ def main():
             if any(p != w >> 2 or not (256 * (w & 3) <= x < 256 * (w & 3) + 256) for p, x in xs):
                 print(f"VIOLATION: {name} of wave {w} leaves its block")
                 ok = False
-        worst = banks(lds.trace)
-        print(f"member {h}: worst b64 bank multiplicity per half-wave = {worst}")
-        ok &= worst == 1
+        wr_, ww_ = banks(lds.trace, 32), banks(lds.wtrace, 16)
+        print(f"member {h}: worst b64 bank multiplicity: reads per 32-lane group {wr_}, writes per 16-lane group {ww_}")
+        ok &= wr_ == 1 and ww_ == 1
     # hand-off + stage 0 (both members compute every coefficient)
     for t in range(TH):
         tau, pp = t & 255, t >> 8
