@@ -712,6 +712,9 @@ __device__ __forceinline__ double duo_load_d(const double* p) {
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
+#ifndef F64D_MFULL
+#define F64D_MFULL 1
+#endif
 #ifndef F64D_KPRE
 #define F64D_KPRE 4
 #endif
@@ -740,8 +743,10 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     double* bf = lds_d + 2 * N;  // forward buffer [2][H]
     double* bi = bf + 2 * H;     // inverse buffer [2][H]
     double* cx = bi + 2 * H;     // this round's C' (+ the WRAP correction) [2][H], slot positions
+    // F64D_MFULL: the whole 2N-entry factor table psi^e - 1 (32 KiB; one workgroup per CU leaves the LDS for
+    // it), one lookup per factor; otherwise the two 64-entry tables, two lookups and a product per factor
     double* mt = cx + 2 * H;     // monomial tables
-    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 128);  // rotation exponents [n]
+    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + (F64D_MFULL ? 2 * N : 128));  // rotation exponents [n]
     __shared__ int wflag[2];
     __shared__ uint32_t duo_ok;
     const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6, twoN = 2 * N, logG = P.logG;
@@ -752,10 +757,14 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     const uint32_t sp = j * H + 256 * (w & 3);                // their buffer block
     for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
     const double* mono = tabs + twoN;
-    for (uint32_t k = t; k < 128; k += TH) {
-        const uint32_t e = k < 64 ? 64 * k : k - 64;
-        const double v = __dadd_rn(mono[e], 1.0);
-        mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
+    if constexpr (F64D_MFULL) {
+        for (uint32_t k = t; k < twoN; k += TH) mt[k] = mono[k];  // centred psi^k - 1 (k_pack_f64)
+    } else {
+        for (uint32_t k = t; k < 128; k += TH) {
+            const uint32_t e = k < 64 ? 64 * k : k - 64;
+            const double v = __dadd_rn(mono[e], 1.0);
+            mt[k] = v > 0.5 * K.Q ? __dsub_rn(v, K.Q) : v;
+        }
     }
     const double* bsk = tabs + 2 * twoN;
     const uint64_t Qhalf = P.Q >> 1;
@@ -884,8 +893,8 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
             if constexpr (PROBE == 3) ip = ai & (twoN - 1);  // timing only: wave-uniform table rows
             const uint32_t in = (twoN - ip) & (twoN - 1);
-            const double Wp = __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
-            const double Wm = __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
+            const double Wp = F64D_MFULL ? mt[ip] : __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
+            const double Wm = F64D_MFULL ? mt[in] : __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
             S[s] = fred(__dadd_rn(fmodmul(A[0][s], Wp, K), fmodmul(A[1][s], Wm, K)), K);
             Cn[s] = fred(__dadd_rn(Cn[s], S[s]), K);
         }
@@ -1124,7 +1133,8 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             // two workgroups per ciphertext (f64wduo), then the rescue of timed-out pairs
             const DuoBuf X = duo_layout(duo);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
-            const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + 128) * sizeof(double) + rot_exponent_bytes(P.n);
+            const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + (F64D_MFULL ? 2 * P.N : 128)) * sizeof(double) +
+                                rot_exponent_bytes(P.n);
             auto dk = k_blind_rotate_f64wduo<0>;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives

@@ -1478,6 +1478,12 @@ __device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
 #ifndef SF2D_KPRE
 #define SF2D_KPRE 2
 #endif
+// SF2D_MFULL: one workgroup per CU leaves the LDS for sf2p's whole 2N-row factor table (64 KiB): one table
+// product per monomial factor instead of two and the offset term (sf_mono_pair)
+#ifndef SF2D_MFULL
+#define SF2D_MFULL 1
+#endif
+constexpr size_t SF2D_MT = SF2D_MFULL ? 4 * G3_N : SF_MT;  // u64 words of the factor table(s)
 // one workgroup per CU at the batches it serves (<= kDuoMaxPairs pairs, default 128): two waves per SIMD, so
 // the register budget is 256 -- room for the key groups in flight (SF2D_KPRE)
 template <int PROBE = 0>
@@ -1502,14 +1508,21 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     uint64_t* psi_l = buf + 2 * N;
     uint64_t* psi1_l = psi_l + N;
     for (uint32_t k = t; k < N; k += TH) psi_l[k] = psi[k], psi1_l[k] = psi1[k];
-    uint64_t* mt = psi1_l + N;  // monomial tables
-    sf_mono_tables(mt, mono, mono1, Q);
+    uint64_t* mt = psi1_l + N;  // monomial tables (SF2D_MFULL: the whole 2N-row table, sf2p's layout)
+    if constexpr (SF2D_MFULL) {
+        for (uint32_t k = t; k < twoN; k += TH) {
+            mt[2 * sf_mrow(k)] = mono[k] % Q;  // psi^k - 1
+            mt[2 * sf_mrow(k) + 1] = mono1[k];
+        }
+    } else {
+        sf_mono_tables(mt, mono, mono1, Q);
+    }
     const SfTw TF{psi_l, psi1_l};
     const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
     uint64_t* g = acc_io + (size_t)pair * twoN;
     const uint64_t* ap = a + (size_t)pair * P.n;
-    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * G3_N + SF_MT) * 8);  // rotation exponents [n]
+    uint32_t* ex = reinterpret_cast<uint32_t*>(smem + ((size_t)4 * G3_N + SF2D_MT) * 8);  // rotation exponents [n]
     stage_rot_exponents<G3_TH>(ex, ap, P.n, amod, twoN);
     const size_t round_words = (size_t)4 * P.dG2 * N;
     const uint32_t u4 = 4 * (((t >> 6) << 6) | (t & 63));  // this lane's slots u4 .. u4+3
@@ -1588,7 +1601,15 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             }
             if (kk == 1 && l == RW - 1) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) S[j][s] = sf_mono_pair(A[0][s], ip[s], A[1][s], (twoN - ip[s]) & (twoN - 1), mt, K);
+                for (int s = 0; s < 4; ++s) {
+                    if constexpr (SF2D_MFULL) {  // one table product per factor (row e holds psi^e - 1), as sf2p
+                        const uint64_t* fp = mt + 2 * sf_mrow(ip[s]);
+                        const uint64_t* fm = mt + 2 * sf_mrow((twoN - ip[s]) & (twoN - 1));
+                        S[j][s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
+                    } else {
+                        S[j][s] = sf_mono_pair(A[0][s], ip[s], A[1][s], (twoN - ip[s]) & (twoN - 1), mt, K);
+                    }
+                }
                 sf2_inv_unit(buf, j, S[j], TI, K);  // the buffer is dead after the forward units
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -1776,13 +1797,14 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
         };
         if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
             const DuoBuf X = duo_layout(duo);
+            const size_t ldsd = ((size_t)4 * G3_N + SF2D_MT) * 8 + rot_exponent_bytes(P.n);
             if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
             auto dk = k_blind_rotate_sf2duo<0>;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_sf2duo<1>;  // test library only: a partner that never arrives
 #endif
-            (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), lds, s, P, K,
+            (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
+            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), ldsd, s, P, K,
                                (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono,
                                w1 + 2 * P.N, (const uint64_t*)bsk,
                                w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);

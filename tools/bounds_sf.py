@@ -141,6 +141,9 @@ INV_FOLD_PASS = (False, False, True)   # inverse radix-8 passes C, B: fold the l
 INV_FOLD_LAST = (False, False, False)  # pass A: none (the accumulator update folds)
 
 
+DUO_MFULL = True  # sf2duo's factors from the whole 2N-row table (SF2D_MFULL, blind_rotate_generic.hip)
+
+
 def model(rows, sf2=True, form="sf2"):
     """form: "sf2" / gen3sf (two-level LDS factor tables), "sf2p" (one product per factor with a row of
     the 2N-entry table, no offset: S = fold(sf(A0, F+) + sf(A1, F-))), "duo" (sf2duo: a member sums its own
@@ -151,6 +154,7 @@ def model(rows, sf2=True, form="sf2"):
     # sf2p, sf2duo: r + Q with the offset in the difference (ct_ofs)
     global CT
     CT = ct_ofs if form in ("sf2p", "duo") else ct
+    mfull = form == "sf2p" or (form == "duo" and DUO_MFULL)
     x = (FWD_OFF * Q - Q // 2, FWD_OFF * Q + Q // 2) if sf2 else (FWD_OFF * Q, (FWD_OFF + 1) * Q)
     if form in ("sf2p", "duo"):
         x = (0, 2 * Q)
@@ -161,7 +165,7 @@ def model(rows, sf2=True, form="sf2"):
     D = max(e[1] for e in v)
     R = mulw(D)
     Ap = rows * (1 if form == "duo" else 2) * R   # rows digits x polynomials per (key, column)
-    if form == "sf2p":
+    if mfull:
         S = fold(2 * mulw(Ap))
     else:
         # A0j (X^a' - 1) + A1j (X^-a' - 1) by two LDS table factors per term (sf_mono_pair):
