@@ -20,7 +20,7 @@ struct BRParams {
 struct Knobs {
     int32_t ks_tiled_min = -1;  // smallest batch on the tiled key switch; -1: default (1), 0: never
     int32_t ks_cts = 0;         // ciphertexts per thread of the tiled key switch; 0: by key width / batch
-    int32_t ks_split = 16;      // most block groups the key-switch steps split over at small batches; 1: none
+    int32_t ks_split = 32;      // most block groups the key-switch steps split over at small batches (u16 / u32 keys: 16 at most); 1: none
     int32_t ks_pk = 1;          // 0: no packed u16 column sums
     int32_t host_parts = 1;     // sub-batches per device of the host-array runner
     int32_t wire = 1;           // 0: u64 PCIe words (no narrow wire format)

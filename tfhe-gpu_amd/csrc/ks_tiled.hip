@@ -311,13 +311,20 @@ __global__ void __launch_bounds__(256) k_ks_combine(KSParams P, const uint64_t* 
 // Splits for a batch: enough blocks for two per CU (512), dividing the stage pairs; at most 4 up to
 // kSplitMaxB ciphertexts, at most kMaxSplit up to kWideSplitMaxB (round 4: a 128- or 256-ciphertext
 // batch has one ciphertext tile, 32 blocks for STD128Q -- the C5 shard of 1024 over 8 GPUs)
-constexpr uint32_t kMaxSplit = 16, kSplitMaxB = 2048, kWideSplitMaxB = 512;
-uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B, const Knobs& kn) {
+// Round 5 (profiles/r05y2, tools/ks_bench.py at 128 ciphertexts): the u64-key form there reads the whole
+// 4.8 GB KSK once per launch, at 2.96 TB/s with 704 blocks; more blocks in flight (target 2048, up to 32
+// splits) take LOGQ23's key switch 1.715 -> 1.412 ms.  The u16 / u32 forms keep at most 16 splits (32 cost
+// STD128Q's 0.324 ms 12 %).
+#ifndef KS_BLOCK_TARGET
+#define KS_BLOCK_TARGET 2048
+#endif
+constexpr uint32_t kMaxSplit = 32, kMaxSplitNarrow = 16, kSplitMaxB = 2048, kWideSplitMaxB = 512;
+uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B, const Knobs& kn, bool wide_keys) {
     const uint32_t cap = std::min<uint32_t>((uint32_t)std::max(1, kn.ks_split),  // knob (TFHE_KS_SPLIT): 1 = no split
-                                            B <= kWideSplitMaxB ? kMaxSplit : 4);
+                                            B <= kWideSplitMaxB ? (wide_keys ? kMaxSplit : kMaxSplitNarrow) : 4);
     const uint32_t pairs = P.N * P.dKS / (2 * GMAX);
     uint32_t z = 1;
-    while (2 * z <= cap && B <= kSplitMaxB && blocks * z < 512 && pairs % (2 * z) == 0) z *= 2;
+    while (2 * z <= cap && B <= kSplitMaxB && blocks * z < KS_BLOCK_TARGET && pairs % (2 * z) == 0) z *= 2;
     return z;
 }
 
@@ -351,7 +358,7 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = (P.n_pad + CT - 1) / CT;
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
-    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn);
+    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, sizeof(KW) == 8);
     hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp,
                        nct, ncol, fmod, out, nsplit, part);
     if (nsplit > 1) {
