@@ -715,6 +715,14 @@ constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
 #ifndef F64D_MFULL
 #define F64D_MFULL 1
 #endif
+#ifndef F64D_FSW
+#define F64D_FSW 1
+#endif
+// row e of the whole factor table lives at e ^ (bits 5-9 of e): a wave's exponents (2 bitrev(slot) + 1) a'
+// share their low five bits, so unswizzled every lane of a 32-lane group hit one bank pair (a 32-way
+// conflict on each of the 8 lookups per lane-round; mean 29.4 distinct addresses per bank over random a');
+// with the fold the mean is 2.0 (bit 5 up varies as m a' for the group's 32 values of m)
+__device__ __forceinline__ uint32_t fsw(uint32_t e) { return F64D_FSW ? e ^ ((e >> 5) & 31) : e; }
 #ifndef F64D_KPRE
 #define F64D_KPRE 4
 #endif
@@ -758,7 +766,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     for (uint32_t k = t; k < twoN; k += TH) lds_d[k] = tabs[k];
     const double* mono = tabs + twoN;
     if constexpr (F64D_MFULL) {
-        for (uint32_t k = t; k < twoN; k += TH) mt[k] = mono[k];  // centred psi^k - 1 (k_pack_f64)
+        for (uint32_t k = t; k < twoN; k += TH) mt[fsw(k)] = mono[k];  // centred psi^k - 1 (k_pack_f64)
     } else {
         for (uint32_t k = t; k < 128; k += TH) {
             const uint32_t e = k < 64 ? 64 * k : k - 64;
@@ -893,8 +901,8 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
             if constexpr (PROBE == 3) ip = ai & (twoN - 1);  // timing only: wave-uniform table rows
             const uint32_t in = (twoN - ip) & (twoN - 1);
-            const double Wp = F64D_MFULL ? mt[ip] : __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
-            const double Wm = F64D_MFULL ? mt[in] : __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
+            const double Wp = F64D_MFULL ? mt[fsw(ip)] : __dsub_rn(fmodmul(mt[ip >> 6], mt[64 + (ip & 63)], K), 1.0);
+            const double Wm = F64D_MFULL ? mt[fsw(in)] : __dsub_rn(fmodmul(mt[in >> 6], mt[64 + (in & 63)], K), 1.0);
             S[s] = fred(__dadd_rn(fmodmul(A[0][s], Wp, K), fmodmul(A[1][s], Wm, K)), K);
             Cn[s] = fred(__dadd_rn(Cn[s], S[s]), K);
         }
