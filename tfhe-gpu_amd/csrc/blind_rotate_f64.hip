@@ -728,7 +728,8 @@ __device__ __forceinline__ uint32_t fsw(uint32_t e) { return F64D_FSW ? e ^ ((e 
 #endif
 
 // STD128Q class only (RED, WRAP, one transformed digit: f64w<true, true, 1>).  Two waves per SIMD
-// (87 KiB of LDS: one workgroup per CU), so the round's state fits registers without spills.
+// (116 KiB of LDS with the whole factor table: one workgroup per CU), so the round's state fits registers
+// without spills (182 VGPRs with four key groups in flight).
 // PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a
 // partner that never arrives would, and the polls are bounded 2^14 times.  PROBE 2 (timing only, results
 // invalid): no hand-off at all -- each member takes its own stage-1 values for its partner's -- the
