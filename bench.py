@@ -95,7 +95,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS), help="SURVEY.md 8(d) configuration")
     ap.add_argument("--batch", type=int, default=0,
-                    help="ciphertexts per GPU (weak configs) or in all (strong configs); 0 = the config's")
+                    help="ciphertexts per GPU (weak scaling) or in all (strong scaling); 0 = the config's")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="weak: --batch per GPU (C2-C4's default: BASELINE's 'batch=8192 at 1/2/4/8 GPUs' read as "
+                         "8192 per GPU); strong: --batch in all, sharded over the GPUs (C5's default; C2 strong = "
+                         "8192 in all, 8192/N per GPU)")
     ap.add_argument("--params", default=None,
                     help="EvalBinGate(NAND) on another parameter set (e.g. STD192, STD128Q): device-resident, "
                          "no cpu_baseline (overrides --config's context)")
@@ -418,6 +422,26 @@ def cpu_baseline_port(p, bsk, ksk, seconds, gpu_sample, reason):
             "gpu_parity": parity}
 
 
+def batch_split(cfg, batch, world, rank):
+    """(this rank's batch, the whole job's): weak scaling = `batch` per GPU, strong = `batch` in all, cut into
+    contiguous shards (tfhe_shard_range)."""
+    from tfhe_amd import dist as tdist
+
+    if cfg["scaling"] == "strong":
+        lo, hi = tdist.shard_range(batch, world, rank)
+        return hi - lo, batch
+    return batch, batch * world
+
+
+def metric_name(name, cfg, total, B, world, params=False):
+    """BASELINE.json's metric with the reading stated: the global batch, and per-GPU batch (weak) or the
+    shard count (strong)."""
+    what = f"{cfg['ctx'][1]} GINX" if name == "C2" or params else f"{name}: {cfg['what']},"
+    how = (f"{B} per GPU, weak scaling" if cfg["scaling"] == "weak"
+           else f"sharded over {world} GPU{'s' if world > 1 else ''}, strong scaling")
+    return f"bootstraps/sec (whole node), {what} global batch={total} ({how})"
+
+
 def main():
     args = parse()
     name = args.config
@@ -453,13 +477,9 @@ def main():
     ctxspec = cfg["ctx"]
     p = (tfhe_amd.params_from_set(ctxspec[1]) if ctxspec[0] == "set"
          else tfhe_amd.params_from_logq(ctxspec[1], *ctxspec[2:]))
-    if cfg["scaling"] == "strong":  # the config's batch is the whole job's
-        total = args.batch or cfg["batch"]
-        lo, hi = tdist.shard_range(total, world, rank)
-        B = hi - lo
-    else:
-        B = args.batch or cfg["batch"]
-        total = B * world
+    if args.scaling:
+        cfg["scaling"] = args.scaling
+    B, total = batch_split(cfg, args.batch or cfg["batch"], world, rank)
     # a dedicated (non-null) stream: the engine's kernels, torch's tensors and the
     # HIP events below are all ordered on it
     stream = torch.cuda.Stream(dev)
@@ -473,9 +493,10 @@ def main():
     knobs = {k: int(v) for k, v in (x.split("=", 1) for x in args.knob)}
     if rank == 0:
         bsk, ksk = synthetic_keys(p)
-        ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)  # keys kept: the oracle check
-    else:
-        bsk = ksk = None
+        ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)
+    # the host keys are not held through the timed run (C3's KSK alone is 4.8 GB); the oracle check and the
+    # port fallback regenerate them deterministically (synthetic_keys) after it
+    bsk = ksk = None
     if world > 1:
         # one RCCL broadcast of the packed device key image over xGMI (tfhe_amd/dist.py)
         img = None
@@ -688,6 +709,8 @@ def main():
     oracle = None
     if rank == 0 and not args.params:
         try:
+            if bsk is None:
+                bsk, ksk = synthetic_keys(p)
             oracle = oracle_sample_check(cfg, bsk, ksk, per_rank,
                                          lut=cube_lut(int(p.q)) if cfg["op"] == "func" else None,
                                          threads=host_threads()[0])
@@ -704,8 +727,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": (f"bootstraps/sec (whole node), {ctxspec[1]} GINX batch={B}" if name == "C2" or args.params
-                       else f"bootstraps/sec (whole node), {name}: {cfg['what']}, batch={total}"),
+            "metric": metric_name(name, cfg, total, B, world, bool(args.params)),
             "value": round(value, 2), "unit": "bootstraps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": cfg["scaling"], "vs_baseline": None, "data": "synthetic",

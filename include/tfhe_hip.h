@@ -109,10 +109,12 @@ typedef struct tfhe_info {
     int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
     int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
     double replicate_ms;       /* wall time of that replication (0 for one device) */
-    uint32_t duo_timeouts;     /* workgroups of the two-workgroup form (sf2duo) that timed out waiting for
-                                  their partner since setup, summed over devices (synchronises them); the
-                                  ciphertexts of such a pair are recomputed by the one-workgroup kernel
-                                  from their saved inputs in the same launch, so outputs stay exact */
+    uint32_t duo_timeouts;     /* workgroups of the two-workgroup forms (sf2duo: two-digit special-form
+                                  contexts; f64wduo: STD128Q class) that timed out waiting for their partner
+                                  (10 ms of wall clock in one round) since setup, summed over devices
+                                  (synchronises them); the ciphertexts of such a pair are recomputed from
+                                  their saved inputs by the one-workgroup kernel (sf2 / f64w) queued behind
+                                  the same launch, so outputs stay exact */
 } tfhe_info;
 
 /* tfhe_info.replicate_method */
@@ -246,6 +248,15 @@ tfhe_status tfhe_host_selftest(const tfhe_params* p);
  * tfhe_last_error() = "device <g>: ...". ---- */
 tfhe_status tfhe_shard_range(size_t total, int world, int rank, size_t* lo, size_t* hi);
 tfhe_status tfhe_host_shard_selftest(size_t B, int devices, int fail_device, size_t* spans);
+/* The RCCL sequence of tfhe_setup(num_gpus)'s key replication (communicator over the devices, one
+ * ncclBroadcast per rank in a group, streams synchronised, communicators destroyed) run on ONE device with
+ * a one-rank communicator: `bytes` (a multiple of 8) of a seeded buffer broadcast out of place and the two
+ * copies' checksums compared.  lib NULL or "" = the system librccl (what tfhe_setup loads); *version =
+ * ncclGetVersion's (0 if the library lacks it).  TFHE_ERR_UNSUPPORTED when the library does not load;
+ * TFHE_ERR_DEVICE when a call fails or the copy differs.  Checks the engine's RCCL binding against the
+ * real library on a one-GPU box (the reference's GPUSetup(numGPUs) copies per GPU from the host,
+ * bootstrapping.cu:1005-1069). */
+tfhe_status tfhe_rccl_selftest(int device, size_t bytes, const char* lib, int* version);
 
 /* ---- launch knobs (no reference counterpart): the kernel-form choices earlier rounds measured A/B.
  * Read from the environment once, when a context is set up (TFHE_KS_TILED_MIN, TFHE_KS_CTS,
@@ -271,7 +282,8 @@ typedef struct tfhe_knobs {
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
     int32_t duo;          /* two-digit special-form contexts (sf2duo) and STD128Q-class FP64 contexts (f64wduo):
                              batches up to this size (default 128, at most 256) run each ciphertext on two
-                             workgroups; 0: never */
+                             workgroups, and only while the device holds every pair co-resident (a duo workgroup
+                             takes one CU: at most half the CU count, 128 on MI355X); 0: never */
     int32_t sf2p;         /* two-digit special-form contexts, batches of 512 or more: 1 (default) runs two
                              ciphertexts per workgroup (sf2p, whose shared LDS holds the whole monomial factor
                              table); 0: one per workgroup (sf2) */

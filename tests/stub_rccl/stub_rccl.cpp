@@ -1,4 +1,4 @@
-// stub_rccl.cpp -- TEST INFRASTRUCTURE: the six RCCL entry points the engine's in-process key replication
+// stub_rccl.cpp -- TEST INFRASTRUCTURE: the RCCL entry points the engine's in-process key replication
 // calls (engine.hip replicate_arena: ncclCommInitAll, ncclGroupStart, ncclBroadcast per device,
 // ncclGroupEnd, ncclCommDestroy, ncclGetErrorString), implemented with HIP device copies so that the
 // group / sync / destroy sequence runs on a one-GPU box, where TFHE_LOGICAL_DEVICES puts every logical
@@ -90,6 +90,12 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
     auto* sh = new Shared{ndev};
     for (int i = 0; i < ndev; ++i) comms[i] = new ncclComm{sh, i, devlist ? devlist[i] : i};
     g_comms += ndev;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclGetVersion(int* version) {
+    if (!version) return ncclInvalidArgument;
+    *version = 0;  // the stub: no RCCL version
     return ncclSuccess;
 }
 

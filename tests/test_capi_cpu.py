@@ -204,18 +204,19 @@ def test_environment_knobs_are_validated(env, why):
     assert "ERR" in r.stdout and "launch knob from the environment" in r.stdout and why in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("kernel,probes", [("k_blind_rotate_sf2duo", ["0", "1"]),
-                                            ("k_blind_rotate_f64wduo", ["0", "1", "2", "3"])])
-def test_product_library_has_no_duo_probe(capi, kernel, probes):
-    """The duo probes (1: a partner that never arrives; 2: f64wduo with no hand-off, 3: broadcast factor
-    rows -- both timing only) are
-    test-library instances only."""
+@pytest.mark.parametrize("kernel,product,probes", [("k_blind_rotate_sf2duo", ["0"], ["0", "1"]),
+                                                    ("k_blind_rotate_f64wduo", ["0"], ["0", "1", "2", "3", "4"]),
+                                                    ("k_blind_rotate_sf2p", ["2, 0"], ["2, 0", "2, 1"])])
+def test_product_library_has_no_duo_probe(capi, kernel, product, probes):
+    """The duo probes (1: a partner that never arrives; f64wduo 2: no hand-off, 3: broadcast factor rows,
+    4: no D / C' exchange barrier; sf2p<2, 1>: broadcast factor rows -- all timing only) are test-library
+    instances only."""
     import re
     import subprocess
 
     def duo(path):
         out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
-        return sorted(set(re.findall(kernel + r"<(\d+)>", out)))
+        return sorted(set(re.findall(kernel + r"<([\d, ]+)>", out)))
 
-    assert duo(capi.library_path()) == ["0"]
+    assert duo(capi.library_path()) == product
     assert duo(capi.capi.TEST_LIB) == probes

@@ -133,3 +133,60 @@ def test_f64duo_partner_timeout_is_recomputed(oracle):
         ctx.GPUClean()
         orc.close()
 
+
+
+def test_f64duo_two_streams_and_two_contexts(oracle):
+    """Verdict r5 item 7: the duo form outside its usual single-stream use.
+    * One context, two streams, no host sync between the launches: the device's one exchange buffer is
+      fenced (kernels.hpp duo_serialised), so both batches are exact and no partner times out.
+    * Two contexts (two exchange buffers), 128 + 128 ciphertexts launched at once on two streams: 512
+      workgroups that need one CU each, so some members may run while their partners wait behind the other
+      launch.  The partner wait is bounded by time (10 ms of s_memrealtime per round), a timed-out pair is
+      recomputed by the rescue launch: outputs exact, the whole thing done in well under a second (the
+      round-5 bound of 2^24 polls was seconds per stuck member).  duo_timeouts is reported, any value."""
+    import time
+
+    import torch
+
+    import tfhe_amd
+
+    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(93))
+    ctxs = [tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk) for _ in range(2)]
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    lib = tfhe_amd.lib()
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    try:
+        B = 128
+        ins = [_inputs(op, B, 800 + k, amod=1024) for k in range(2)]
+        with ctxs[0].knobs_set(duo=0):
+            want = [ctxs[0].EvalAcc(a, 1024, acc) for a, acc in ins]
+        for k in range(2):
+            assert np.array_equal(want[k][[0, B - 1]], orc.eval_acc(ins[k][0][[0, B - 1]], 1024, ins[k][1][[0, B - 1]]))
+        d_a = [torch.from_numpy(a.astype(np.int64)).to(dev) for a, _ in ins]
+
+        def run(pairs):
+            d_acc = [torch.from_numpy(acc.astype(np.int64)).to(dev) for _, acc in ins]
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k, ctx in enumerate(pairs):
+                tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, d_a[k].data_ptr(), 1024, d_acc[k].data_ptr(),
+                                                             streams[k].cuda_stream), "eval_acc_device")
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            return [x.cpu().numpy().astype(np.uint64) for x in d_acc], dt
+
+        got, dt1 = run([ctxs[0], ctxs[0]])  # one context, two streams
+        assert all(np.array_equal(g, w) for g, w in zip(got, want))
+        assert ctxs[0].info().duo_timeouts == 0
+        got, dt2 = run(ctxs)  # two contexts at once
+        assert all(np.array_equal(g, w) for g, w in zip(got, want))
+        timeouts = sum(c.info().duo_timeouts for c in ctxs)
+        print(f"one context two streams {dt1 * 1e3:.1f} ms; two contexts {dt2 * 1e3:.1f} ms, duo_timeouts {timeouts}")
+        assert dt2 < 1.0
+    finally:
+        for c in ctxs:
+            c.GPUClean()
+        orc.close()

@@ -711,7 +711,6 @@ __device__ __forceinline__ double duo_load_d(const double* p) {
     return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<double*>(p)),
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-constexpr uint32_t kF64DuoMaxPolls = 1u << 24;
 #ifndef F64D_MFULL
 #define F64D_MFULL 1
 #endif
@@ -874,7 +873,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             bf[sp + dswz(4 * l + s)] = D[s];
             cx[sp + dswz(4 * l + s)] = Cx[s];
         }
-        __syncthreads();
+        if constexpr (PROBE != 4) __syncthreads();  // (PROBE 4, timing only: no exchange barrier, results invalid)
         double Do[4], Co[4];  // the other polynomial's at the same slots
         const uint32_t so = (1 - j) * H + 256 * (w & 3);
 #pragma unroll
@@ -920,16 +919,24 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // every wave's stores drained; every read of the inverse buffer done
         if (PROBE != 2 && t == 0) {
-            constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kF64DuoMaxPolls;
+            // the wait is bounded by time (wall clock, s_memrealtime): kDuoWaitMs, PROBE 1 a 64th of it
             const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
             if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t polls = gone ? kMaxPolls : 0;
-            while (polls < kMaxPolls &&
-                   __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
-                   ++polls < kMaxPolls)
+            // (the clock is read every 8th poll, the deadline set at the first read: a partner within 8 polls
+            // costs no clock read)
+            bool ok = !gone;
+            uint64_t t_end = 0;
+            uint32_t k = 0;
+            while (ok && __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1) {
+                if ((++k & 7) == 0) {
+                    const uint64_t now = wall_clock64();
+                    if (t_end == 0) t_end = now + (PROBE ? X.wait_ticks >> 6 : X.wait_ticks);
+                    else if (now > t_end) ok = false;
+                }
                 __builtin_amdgcn_s_sleep(1);
-            duo_ok = polls < kMaxPolls;
-            if (polls >= kMaxPolls) {
+            }
+            duo_ok = ok;
+            if (!ok) {
                 __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -1102,7 +1109,7 @@ bool f64_duo_form(const BRParams& P, bool fold) {
 
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold,
                                    const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                   const Knobs& kn, void* duo) {
+                                   const Knobs& kn, DuoDev* duo) {
     if (B == 0) return hipSuccess;
     if (P.N != 2048 || !f64_instance_available(P, fold)) return hipErrorInvalidValue;
     F64Const K;
@@ -1138,10 +1145,9 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             return hipGetLastError();
         }
 #endif
-        if (red && wrap && ld == 1 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
+        if (red && wrap && ld == 1 && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs && B <= kDuoMaxPairs) {
             // two workgroups per ciphertext (f64wduo), then the rescue of timed-out pairs
-            const DuoBuf X = duo_layout(duo);
-            if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
+            const DuoBuf X = duo_layout(*duo);
             const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + (F64D_MFULL ? 2 * P.N : 128)) * sizeof(double) +
                                 rot_exponent_bytes(P.n);
             auto dk = k_blind_rotate_f64wduo<0>;
@@ -1149,16 +1155,20 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
             if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
             if (kn.probe == 9) dk = k_blind_rotate_f64wduo<3>;  // timing only: broadcast factor-table reads
+            if (kn.probe == 11) dk = k_blind_rotate_f64wduo<4>;  // timing only: no D / C' exchange barrier
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
-            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
-                               a, amod, acc, X, (uint32_t)B);
-            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
             auto rk = k_blind_rotate_f64w<true, true, 1, 0, true>;
             (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(512), lds, s, P, K, (const double*)keys, T.eidx, a, amod, acc,
-                               (const uint32_t*)X.flags, (const uint64_t*)X.save);
-            return hipGetLastError();
+            return duo_serialised(*duo, s, [&]() -> hipError_t {
+                if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
+                hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(512), ldsd, s, P, K, (const double*)keys,
+                                   a, amod, acc, X, (uint32_t)B);
+                if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+                hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(512), lds, s, P, K, (const double*)keys, T.eidx, a, amod,
+                                   acc, (const uint32_t*)X.flags, (const uint64_t*)X.save);
+                return hipGetLastError();
+            });
         }
         if (red) gow(k_blind_rotate_f64w<true, true, 1>);
         else gow(k_blind_rotate_f64w<false, false, 2>);

@@ -1287,7 +1287,9 @@ k_blind_rotate_sf2(BRParams P, SfC K, const uint64_t* __restrict__ psi, const ui
 // kernel's cycles, profiles/r04p).  XOR-ing bits 4-7 and 8-11 into the low four spreads them.
 __device__ __forceinline__ uint32_t sf_mrow(uint32_t e) { return e ^ (((e >> 4) ^ (e >> 8)) & 15); }
 
-template <int DIG>
+// PROBE 1 (test library only, timing only, results invalid): wave-uniform factor-table rows (every lane reads
+// row a'), the bound on what the table's bank conflicts cost
+template <int DIG, int PROBE = 0>
 __global__ void __launch_bounds__(2 * G3_TH, 4)
 k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
                     const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
@@ -1410,6 +1412,7 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
                 if constexpr (!IP_ONCE) slot_exponents();
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {  // one table product per factor (row e holds psi^e - 1)
+                    if constexpr (PROBE == 1) ip[s] = ai & (twoN - 1);
                     const uint64_t* fp = mtab + 2 * sf_mrow(ip[s]);
                     const uint64_t* fm = mtab + 2 * sf_mrow((twoN - ip[s]) & (twoN - 1));
                     S[j][s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
@@ -1465,7 +1468,6 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
 // member saves its input polynomial first (X.save), and the launcher queues k_blind_rotate_sf2<2, true>
 // right behind, which recomputes exactly the failed pairs' ciphertexts from X.save -- a late partner
 // never returns wrong accumulators.
-constexpr uint32_t kDuoMaxPolls = 1u << 24;
 __device__ __forceinline__ void duo_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1629,16 +1631,24 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
             for (int k = 0; k < 8; ++k) buf[c0 + 256 * k] = v[k];
         }
         if (t == 0) {
-            constexpr uint32_t kMaxPolls = PROBE ? 1u << 14 : kDuoMaxPolls;
+            // the wait is bounded by time (wall clock, s_memrealtime): kDuoWaitMs, PROBE 1 a 64th of it
             const bool gone = PROBE == 1 && pair == 0 && x == 1 && i >= 2;
             if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t polls = gone ? kMaxPolls : 0;
-            while (polls < kMaxPolls &&
-                   __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1 &&
-                   ++polls < kMaxPolls)
+            // (the clock is read every 8th poll, the deadline set at the first read: a partner within 8 polls
+            // costs no clock read)
+            bool ok = !gone;
+            uint64_t t_end = 0;
+            uint32_t k = 0;
+            while (ok && __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1) {
+                if ((++k & 7) == 0) {
+                    const uint64_t now = wall_clock64();
+                    if (t_end == 0) t_end = now + (PROBE ? X.wait_ticks >> 6 : X.wait_ticks);
+                    else if (now > t_end) ok = false;
+                }
                 __builtin_amdgcn_s_sleep(1);
-            duo_ok = polls < kMaxPolls;
-            if (polls >= kMaxPolls) {
+            }
+            duo_ok = ok;
+            if (!ok) {
                 __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -1775,7 +1785,7 @@ static_assert(G3_N == kDuoN, "the duo buffer holds N = 2048 polynomials");
 
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                  const Knobs& kn, void* duo) {
+                                  const Knobs& kn, DuoDev* duo) {
     if (B == 0) return hipSuccess;
     if (!sf_path_supported(P, 64)) return hipErrorNotSupported;
     SfC K;
@@ -1795,29 +1805,30 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)nullptr,
                                (const uint64_t*)nullptr);
         };
-        if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= kDuoMaxPairs) {
-            const DuoBuf X = duo_layout(duo);
+        if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs && B <= kDuoMaxPairs) {
+            const DuoBuf X = duo_layout(*duo);
             const size_t ldsd = ((size_t)4 * G3_N + SF2D_MT) * 8 + rot_exponent_bytes(P.n);
-            if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
             auto dk = k_blind_rotate_sf2duo<0>;
 #ifdef TFHE_TEST_PROBES
             if (kn.probe == 5) dk = k_blind_rotate_sf2duo<1>;  // test library only: a partner that never arrives
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
-            hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), ldsd, s, P, K,
-                               (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono,
-                               w1 + 2 * P.N, (const uint64_t*)bsk,
-                               w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
-            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
             // the rescue: one-workgroup sf2 for the ciphertexts of timed-out pairs, from their saved inputs
             // (every other workgroup reads one word and exits: a few microseconds per launch)
             auto rk = k_blind_rotate_sf2<2, true>;
             (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
-                               (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
-                               (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)X.flags,
-                               (const uint64_t*)X.save);
-            return hipGetLastError();
+            return duo_serialised(*duo, s, [&]() -> hipError_t {
+                if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
+                hipLaunchKernelGGL(dk, dim3((unsigned)(16 * ((B + 7) / 8))), dim3(G3_TH), ldsd, s, P, K,
+                                   (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono,
+                                   w1 + 2 * P.N, (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, X, (uint32_t)B);
+                if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+                hipLaunchKernelGGL(rk, dim3((unsigned)B), dim3(G3_TH), lds, s, P, K, (const uint64_t*)T.psi, w1,
+                                   (const uint64_t*)T.ipsi, w1 + P.N, (const uint64_t*)T.mono, w1 + 2 * P.N,
+                                   (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)X.flags,
+                                   (const uint64_t*)X.save);
+                return hipGetLastError();
+            });
         }
         // two ciphertexts per workgroup, the monomial table in LDS: two digits only (same box, three reps,
         // profiles/r04m: C5b 70.8 -> 67.7 ms per launch; one digit went the other way, 172.3 -> 178.0 ms,
@@ -1828,6 +1839,9 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
             const size_t ldsp = (size_t)8 * G3_N * 8 + 2 * rot_exponent_bytes(P.n);
             if (ldsp <= 160 * 1024) {
                 auto kern = k_blind_rotate_sf2p<2>;
+#ifdef TFHE_TEST_PROBES
+                if (kn.probe == 12) kern = k_blind_rotate_sf2p<2, 1>;  // timing only: broadcast factor rows
+#endif
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsp);
                 hipLaunchKernelGGL(kern, dim3((unsigned)((B + 1) / 2)), dim3(2 * G3_TH), ldsp, s, P, K,
                                    (const uint64_t*)T.psi, w1, (const uint64_t*)T.ipsi, w1 + P.N,

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <cstdint>
 
 namespace tfhe {
@@ -106,10 +108,12 @@ bool f64_fold_enabled(const BRParams& P);
 bool f64_test_probes_compiled();
 hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void* bsk, bool fold, void* out,
                                hipStream_t s);
-// duo: the device's duo buffer (STD128Q-class batches up to kn.duo run k_blind_rotate_f64wduo)
+struct DuoDev;
+// duo: the device's duo state (STD128Q-class batches up to kn.duo and the device's co-resident pairs run
+// k_blind_rotate_f64wduo)
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold, const uint64_t* a,
                                    uint64_t amod, uint64_t* acc, size_t B, hipStream_t s, const Knobs& kn,
-                                   void* duo = nullptr);
+                                   DuoDev* duo = nullptr);
 // true when the context's FP64 blind rotation has the two-workgroup form (STD128Q class)
 bool f64_duo_form(const BRParams& P, bool fold);
 
@@ -121,7 +125,7 @@ size_t sf_bytes(const BRParams& P);
 hipError_t launch_pack_sf(const BRParams& P, const DevTables& T, const void* bsk, void* out, hipStream_t s);
 hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const void* bsk, const void* sf,
                                   const uint64_t* a, uint64_t amod, uint64_t* acc, size_t B, hipStream_t s,
-                                  const Knobs& kn, void* duo);
+                                  const Knobs& kn, DuoDev* duo);
 
 // Two-workgroup ("duo") blind rotations for batches too small to fill the chip (k_blind_rotate_sf2duo,
 // blind_rotate_generic.hip; k_blind_rotate_f64wduo, blind_rotate_f64.hip): one per-device buffer,
@@ -133,19 +137,43 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
 //   save  [pairs][2][2048] u64                              the input accumulators (the rescue's input)
 constexpr uint32_t kDuoMaxPairs = 256;
 constexpr uint32_t kDuoN = 2048;
+// Per device (engine.hip, finish_device): the buffer above; the partner-wait deadline in wall-clock ticks
+// (s_memrealtime counts at hipDeviceAttributeWallClockRate: kDuoWaitMs of it); the pairs the device holds
+// co-resident (the duo forms take 116-135 KiB of LDS, one workgroup per CU: half the CU count) -- a larger
+// batch runs the one-workgroup kernel, so a pair's partner is never queued behind its own launch's pairs;
+// and the fence that orders duo launches from different streams on the one buffer (event + host mutex).
+constexpr uint32_t kDuoWaitMs = 10;
+struct DuoDev {
+    void* base = nullptr;
+    uint64_t wait_ticks = 0;
+    uint32_t resident_pairs = 0;
+    hipEvent_t fence = nullptr;
+    std::mutex* mu = nullptr;
+};
 struct DuoBuf {
     uint64_t* xbuf;
     uint32_t* flags;
     uint32_t* err;
     uint64_t* save;
+    uint64_t wait_ticks;  // a member waits at most this long for its partner's flag in any round
 };
-inline DuoBuf duo_layout(void* base) {
+inline DuoBuf duo_layout(const DuoDev& D) {
     DuoBuf X;
-    X.xbuf = (uint64_t*)base;
+    X.xbuf = (uint64_t*)D.base;
     X.flags = (uint32_t*)(X.xbuf + (size_t)kDuoMaxPairs * 4 * kDuoN);
     X.err = X.flags + kDuoMaxPairs * 2 * 32;
     X.save = (uint64_t*)(X.err + 32);
+    X.wait_ticks = D.wait_ticks;
     return X;
+}
+// Runs `launch` (the duo kernel and its rescue, on stream s) after every earlier duo launch on this device's
+// buffer, whatever stream it was queued on.
+template <class F>
+hipError_t duo_serialised(DuoDev& D, hipStream_t s, F&& launch) {
+    std::lock_guard<std::mutex> lock(*D.mu);
+    if (hipError_t e = hipStreamWaitEvent(s, D.fence, 0); e != hipSuccess) return e;
+    if (hipError_t e = launch(); e != hipSuccess) return e;
+    return hipEventRecord(D.fence, s);
 }
 inline size_t duo_bytes() { return (size_t)kDuoMaxPairs * (4 * kDuoN * 8 + 2 * 128) + 128 + (size_t)kDuoMaxPairs * 2 * kDuoN * 8; }
 inline uint32_t duo_err_offset_words() { return (uint32_t)((size_t)kDuoMaxPairs * 4 * kDuoN * 2 + kDuoMaxPairs * 2 * 32); }

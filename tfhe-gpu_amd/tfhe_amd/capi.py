@@ -83,6 +83,7 @@ _SIGS = {
     "tfhe_eval_acc": ([VP, SZ, u64p, U64, u64p], C.c_int),
     "tfhe_shard_range": ([SZ, C.c_int, C.c_int, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)], C.c_int),
     "tfhe_host_shard_selftest": ([SZ, C.c_int, C.c_int, C.POINTER(C.c_size_t)], C.c_int),
+    "tfhe_rccl_selftest": ([C.c_int, SZ, C.c_char_p, C.POINTER(C.c_int)], C.c_int),
     "tfhe_eval_acc_tv": ([VP, SZ, u64p, U64, u64p, C.c_uint32, u64p], C.c_int),
     "tfhe_mkm_switch": ([VP, SZ, u64p, U64, u64p], C.c_int),
     "tfhe_eval_acc_tv_rows": ([VP, SZ, VP, U64, u64p, C.c_uint32, VP], C.c_int),
