@@ -53,13 +53,15 @@
 extern "C" {
 #endif
 
-#define TFHE_HIP_ABI_VERSION 7  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
+#define TFHE_HIP_ABI_VERSION 8  /* 2: tfhe_info.br_kernel; 3: tfhe_info.replicate_*, tfhe_eval_acc_tv, sharding;
                                    4: row-pointer host arrays (tfhe_eval_acc_tv_rows, tfhe_mkm_switch_rows);
                                    5: device-resident EvalFunc / EvalFloor / EvalSign; tfhe_knobs;
                                    6: tfhe_knobs.duo / .sf2p, tfhe_info.duo_timeouts (two-workgroup and
                                       two-ciphertext sf2 forms);
                                    7: tfhe_knobs.split4 (two-group STD128 form); the duo forms cover
-                                      STD128Q (f64wduo) and timed-out pairs are recomputed */
+                                      STD128Q (f64wduo) and timed-out pairs are recomputed;
+                                   8: tfhe_knobs.ks40 (split-word key-switch records for 8-byte keys);
+                                      tfhe_rccl_selftest */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -261,7 +263,7 @@ tfhe_status tfhe_rccl_selftest(int device, size_t bytes, const char* lib, int* v
 /* ---- launch knobs (no reference counterpart): the kernel-form choices earlier rounds measured A/B.
  * Read from the environment once, when a context is set up (TFHE_KS_TILED_MIN, TFHE_KS_CTS,
  * TFHE_KS_SPLIT, TFHE_KS_PK, TFHE_HOST_PARTS, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_F64W, TFHE_SF2,
- * TFHE_GENERIC, TFHE_DUO, TFHE_SF2P, TFHE_SPLIT4, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no
+ * TFHE_GENERIC, TFHE_DUO, TFHE_SF2P, TFHE_SPLIT4, TFHE_KS40, TFHE_TRACE); afterwards only tfhe_set_knobs changes them -- no
  * launch reads the environment.  Every setting computes the same outputs (each is a parity-tested
  * cross-check).  A variable that is not a whole number, or a value out of the field's range, fails
  * the setup with TFHE_ERR_INVALID_ARGUMENT (tfhe_set_knobs checks the same ranges).  tfhe_set_knobs
@@ -289,6 +291,10 @@ typedef struct tfhe_knobs {
                              table); 0: one per workgroup (sf2) */
     int32_t split4;       /* STD128-class contexts: batches up to this size (default 384) run each ciphertext's two
                              polynomials on two groups of four wavefronts (fast4 SPLIT); 0: never */
+    int32_t ks40;         /* contexts whose key-switching keys need 8-byte words with qKS = 2^33 .. 2^37 (the logQ
+                             contexts: 2^35): 1 (default) runs the tiled key switch on split-word records derived
+                             at setup (u32 low word + u8 high part per key, 80 B per 16-column row segment instead
+                             of 128 B); 0: on the u64 words */
 } tfhe_knobs;
 tfhe_status tfhe_get_knobs(tfhe_ctx* ctx, tfhe_knobs* out);
 tfhe_status tfhe_set_knobs(tfhe_ctx* ctx, const tfhe_knobs* in);

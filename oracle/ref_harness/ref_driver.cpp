@@ -25,7 +25,8 @@
 //   sizes=<B1,B2,...>  batch sweep (gates / func / floor / sign / decomp): the reps are timed on the
 //                      first B1, then B2, ... ciphertexts of the input, keys loaded once (the
 //                      reference's CHES-experiments.cpp:95-121 sweep); "sweep" lists best/mean per size
-// Prints one JSON line (digests, timings) on stdout.
+//   batch=<file>       several ops on one context and key load: one line of key=value overrides per op
+// Prints one JSON line (digests, timings) on stdout (one per op in batch mode).
 #include "binfhecontext.h"
 #include "rgsw-acc-cggi.h"
 #include "bootstrapping.cuh"
@@ -204,6 +205,8 @@ void load_keys(Setup& s, const uint64_t* bsk_coeff, const uint64_t* ksk) {
 
 // ---- ciphertexts ------------------------------------------------------------------------
 size_t g_limit = 0;  // sizes= sweep: ciphertexts read from each input (0 = all)
+bool g_batch = false;      // batch= mode: several ops per process
+bool g_gpu_setup = false;  // batch= mode: GPUSetup done (once, by the first vector op)
 
 std::vector<LWECiphertext> read_cts(const std::string& path, uint32_t n, uint64_t mod) {
     auto w = read_u64(path);
@@ -242,6 +245,8 @@ BINGATE gate_of(const std::string& g) {
 }
 
 }  // namespace
+
+int run_op(Setup& s, or_rng& rng, std::ostringstream& js);
 
 int main(int argc, char** argv) {
     for (int i = 1; i < argc; ++i) {
@@ -300,7 +305,39 @@ int main(int argc, char** argv) {
     }
     double t_keys = now_s() - t0;
     js << ",\"keys\":\"" << keys << "\",\"key_load_s\":" << t_keys;
+    const std::string batch = arg("batch");
+    if (batch.empty()) return run_op(s, rng, js);
+    // batch=<file>: one op per line (key=value overrides of this command line's arguments; ctx and keys are
+    // the command line's), all on the context and keys loaded above -- one JSON line per op.  Vector ops share
+    // one GPUSetup, cleaned after the last (the GPU test suite's drop-in cases, tests/test_gpu_dropin.py)
+    const auto base = g_args;
+    std::ifstream in(batch);
+    if (!in) die("cannot read " + batch);
+    std::string line;
+    g_batch = true;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        g_args = base;
+        std::istringstream ls(line);
+        std::string tok;
+        while (ls >> tok) {
+            const size_t e = tok.find('=');
+            if (e == std::string::npos) die("batch line token without '=': " + tok);
+            if (tok.compare(0, e, "ctx") == 0 || tok.compare(0, e, "keys") == 0) die("batch lines cannot change ctx / keys");
+            g_args[tok.substr(0, e)] = tok.substr(e + 1);
+        }
+        g_limit = 0;
+        std::ostringstream jl;
+        jl << "{\"op\":\"" << arg("op") << "\",\"keys\":\"" << keys << "\",\"key_load_s\":" << t_keys;
+        if (int r = run_op(s, rng, jl)) return r;
+        fflush(stdout);
+    }
+    if (g_gpu_setup) s.cc.GPUClean();
+    return 0;
+}
 
+int run_op(Setup& s, or_rng& rng, std::ostringstream& js) {
+    const std::string op = arg("op");
     if (op == "bskeval") {  // OpenFHE's EVALUATION-format BSK, [n][2][dG2][2][N] order
         auto bt = s.cc.GetRefreshKey();
         uint64_t h = 0xcbf29ce484222325ULL;
@@ -354,10 +391,11 @@ int main(int argc, char** argv) {
 
     const std::string api = arg("api", "vector");
     const int reps = (int)arg_u64("reps", 1);
-    if (api == "vector") {
+    if (api == "vector" && !g_gpu_setup) {
         double ts = now_s();
         s.cc.GPUSetup((int)arg_u64("gpus", 0));
         js << ",\"gpu_setup_s\":" << (now_s() - ts);
+        g_gpu_setup = g_batch;  // a batch keeps it for its later ops
     }
     std::vector<uint64_t> out;
     double best = 1e30, total = 0;
@@ -554,7 +592,7 @@ int main(int argc, char** argv) {
                        << ",\"threads\":" << (nthreads.empty() ? 0 : nthreads[si]) << "}";
     }
     if (sizes.size() > 1 || sizes[0]) js << ",\"sweep\":[" << sweep.str() << "]";
-    if (api == "vector") s.cc.GPUClean();
+    if (api == "vector" && !g_batch) s.cc.GPUClean();
     write_u64(arg("out"), out);
     js << ",\"api\":\"" << api << "\",\"reps\":" << reps << ",\"best_s\":" << best << ",\"mean_s\":" << total / reps
        << ",\"words\":" << out.size() << ",\"fnv\":\"" << hex64(fnv1a64(out.data(), out.size())) << "\"";

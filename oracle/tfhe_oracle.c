@@ -549,6 +549,17 @@ static uint64_t to_mod(int64_t v, uint64_t m) {
     return (uint64_t)(r < 0 ? r + (int64_t)m : r);
 }
 
+/* Keys from ONE splitmix64 stream, in this order: s (n ternary), sN (N ternary); per KSK row (i, j, k) its
+ * Gaussian (2 draws) then n uniforms; per BSK row (i, key, row) N uniforms then N Gaussians.  Every draw is
+ * one or two fixed steps of the counter-based generator (state_k = state_0 + k gamma), so each row reads
+ * its own stream position and the rows are filled in parallel (OpenMP) -- the same keys as a sequential
+ * walk, bit for bit (round 6: tests/test_oracle_units.py pins the digest; the GPU suite's valid-key tests
+ * spent most of their time here). */
+static or_rng rng_at(const or_rng* r0, uint64_t draws) {
+    or_rng r = {r0->s + draws * 0x9E3779B97F4A7C15ull};
+    return r;
+}
+
 void or_keygen(const or_params* p, or_rng* r, uint64_t* sk, uint64_t* bsk, uint64_t* ksk) {
     const uint32_t n = p->n, N = p->N, dG2 = p->dG2, bks = p->baseKS, dks = p->dKS;
     const uint64_t Q = p->Q, qKS = p->qKS;
@@ -556,43 +567,62 @@ void or_keygen(const or_params* p, or_rng* r, uint64_t* sk, uint64_t* bsk, uint6
     int64_t* sN = (int64_t*)malloc(sizeof(int64_t) * N);
     for (uint32_t i = 0; i < n; ++i) { s[i] = rng_ternary(r); sk[i] = to_mod(s[i], qKS); }
     for (uint32_t i = 0; i < N; ++i) sN[i] = rng_ternary(r);
+    const or_rng r_ksk = *r;
     /* KSK: lwe-pke.cpp:218-295; A[i][j][k] uniform, B = e + sN[i]*j*baseKS^k + <A, s> mod qKS */
-    for (uint32_t i = 0; i < N; ++i)
-        for (uint32_t j = 0; j < bks; ++j) {
-            uint64_t pw = 1;
-            for (uint32_t k = 0; k < dks; ++k, pw = mulmod(pw, bks, qKS)) {
-                uint64_t* row = ksk + (((size_t)i * bks + j) * dks + k) * (n + 1);
-                uint64_t b = addmod(to_mod(rng_gauss(r), qKS), mulmod(to_mod(sN[i], qKS), mulmod(j, pw, qKS), qKS), qKS);
-                for (uint32_t l = 0; l < n; ++l) {
-                    row[l] = rng_uniform(r, qKS);
-                    b = addmod(b, mulmod(row[l], to_mod(s[l], qKS), qKS), qKS);
-                }
-                row[n] = b;
-            }
+    const size_t ksk_rows = (size_t)N * bks * dks, ksk_draws = 2 + (size_t)n;
+    uint64_t* smod = (uint64_t*)malloc(sizeof(uint64_t) * n);
+    for (uint32_t l = 0; l < n; ++l) smod[l] = to_mod(s[l], qKS);
+#pragma omp parallel for schedule(static)
+    for (size_t rowi = 0; rowi < ksk_rows; ++rowi) {
+        const uint32_t k = (uint32_t)(rowi % dks), j = (uint32_t)((rowi / dks) % bks), i = (uint32_t)(rowi / dks / bks);
+        uint64_t pw = 1;
+        for (uint32_t z = 0; z < k; ++z) pw = mulmod(pw, bks, qKS);
+        or_rng rr = rng_at(&r_ksk, rowi * ksk_draws);
+        uint64_t* row = ksk + rowi * (n + 1);
+        uint64_t b = addmod(to_mod(rng_gauss(&rr), qKS), mulmod(to_mod(sN[i], qKS), mulmod(j, pw, qKS), qKS), qKS);
+        for (uint32_t l = 0; l < n; ++l) {
+            row[l] = rng_uniform(&rr, qKS);
+            b = addmod(b, mulmod(row[l], smod[l], qKS), qKS);
         }
+        row[n] = b;
+    }
+    free(smod);
     /* BSK: rgsw-acc-cggi.cpp:43-77 (ternary MUX keys) and 213-240 (KeyGenCGGI), coefficient form.
      * row i: (a_i, a_i*sN + e_i); m ? row[i][i&1][0] += G^((i>>1)+throw) */
-    uint64_t* sNm = (uint64_t*)malloc(sizeof(uint64_t) * N);
-    uint64_t* prod = (uint64_t*)malloc(sizeof(uint64_t) * N);
-    for (uint32_t x = 0; x < N; ++x) sNm[x] = to_mod(sN[x], Q);
-    for (uint32_t i = 0; i < n; ++i)
-        for (uint32_t key = 0; key < 2; ++key) {
-            int m = key == 0 ? (s[i] == 1) : (s[i] == -1);
-            for (uint32_t row = 0; row < dG2; ++row) {
-                uint64_t* pa = bsk + ((((size_t)i * 2 + key) * dG2 + row) * 2 + 0) * N;
-                uint64_t* pb = bsk + ((((size_t)i * 2 + key) * dG2 + row) * 2 + 1) * N;
-                for (uint32_t x = 0; x < N; ++x) pa[x] = rng_uniform(r, Q);
-                or_polymul_ntt(p, pa, sNm, prod);
-                for (uint32_t x = 0; x < N; ++x) pb[x] = addmod(prod[x], to_mod(rng_gauss(r), Q), Q);
-                if (m) {
-                    uint64_t g = powmod(p->baseG, (row >> 1) + p->numDigitsToThrow, Q);
-                    uint64_t* tgt = (row & 1) ? pb : pa;
-                    tgt[0] = addmod(tgt[0], g, Q);
-                }
+    const or_rng r_bsk = rng_at(&r_ksk, ksk_rows * ksk_draws);
+    const size_t bsk_rows = (size_t)n * 2 * dG2, bsk_draws = 3 * (size_t)N;
+    ntt_tab t;
+    ntt_init(&t, Q, N);
+    uint64_t* sNt = (uint64_t*)malloc(sizeof(uint64_t) * N);  /* NTT(sN mod Q), once */
+    for (uint32_t x = 0; x < N; ++x) sNt[x] = to_mod(sN[x], Q);
+    ntt_fwd(&t, sNt);
+#pragma omp parallel
+    {
+        uint64_t* prod = (uint64_t*)malloc(sizeof(uint64_t) * N);
+#pragma omp for schedule(dynamic, 4)
+        for (size_t rowi = 0; rowi < bsk_rows; ++rowi) {
+            const uint32_t row = (uint32_t)(rowi % dG2), key = (uint32_t)((rowi / dG2) % 2), i = (uint32_t)(rowi / dG2 / 2);
+            const int m = key == 0 ? (s[i] == 1) : (s[i] == -1);
+            uint64_t* pa = bsk + (rowi * 2 + 0) * N;
+            uint64_t* pb = bsk + (rowi * 2 + 1) * N;
+            or_rng rr = rng_at(&r_bsk, rowi * bsk_draws);
+            for (uint32_t x = 0; x < N; ++x) pa[x] = rng_uniform(&rr, Q);
+            memcpy(prod, pa, sizeof(uint64_t) * N);
+            ntt_fwd(&t, prod);
+            for (uint32_t x = 0; x < N; ++x) prod[x] = mulmod(prod[x], sNt[x], Q);
+            ntt_inv(&t, prod);
+            for (uint32_t x = 0; x < N; ++x) pb[x] = addmod(prod[x], to_mod(rng_gauss(&rr), Q), Q);
+            if (m) {
+                uint64_t g = powmod(p->baseG, (row >> 1) + p->numDigitsToThrow, Q);
+                uint64_t* tgt = (row & 1) ? pb : pa;
+                tgt[0] = addmod(tgt[0], g, Q);
             }
         }
-    free(sNm);
-    free(prod);
+        free(prod);
+    }
+    *r = rng_at(&r_bsk, bsk_rows * bsk_draws);  /* the caller's stream continues after the keys */
+    ntt_free(&t);
+    free(sNt);
     free(s);
     free(sN);
 }

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol(capi):
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(lib, s), s
-    assert lib.tfhe_abi_version() == capi.capi.ABI_VERSION == 7
+    assert lib.tfhe_abi_version() == capi.capi.ABI_VERSION == 8
 
 
 @pytest.mark.parametrize("name", ["TOY", "MEDIUM", "STD128", "STD128_OPT", "STD192", "STD192_OPT", "STD256",

@@ -5,7 +5,8 @@ Batches of >= ks_tiled_min (knob; TFHE_KS_TILED_MIN at setup) ciphertexts (defau
 ones the per-ciphertext gather; both must equal the oracle bit for bit.  Every KSK word
 width the engine packs is covered: u16 (STD128, qKS = 2^14), u32 with 32-bit sums
 (STD192, qKS = 2^19, N dKS (qKS-1) < 2^32), u32 with 64-bit sums (STD128Q, qKS = 2^25)
-and u64 (the logQ = 12 arbFunc context, qKS = 2^35, dKS = 7).  Batches are ragged
+and u64 (the logQ = 12 arbFunc context, qKS = 2^35, dKS = 7; since round 6 its tiled form runs on
+split-word records, u32 + u8 per key, and the u64-word form stays as the ks40 = 0 cross-check).  Batches are ragged
 (not multiples of the 512/1024-ciphertext tiles) and include all-zero and all-(Q-1)
 extracts.  Random keys: bit-exactness does not need valid ones."""
 
@@ -119,3 +120,24 @@ def test_u16_keys_without_packed_sums(ks_ctx):
         plain = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
     gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
     assert np.array_equal(packed, plain) and np.array_equal(plain, gather)
+
+
+@pytest.mark.parametrize("B", [1, 128, 1029])
+def test_split_word_keys_equal_u64_words(ks_ctx, B):
+    """8-byte keys with qKS = 2^35 (ARB12 / the logQ contexts; TOY_N8192 takes the gather): the tiled key
+    switch on the split-word records (ks40 = 1, the default: u32 low word + u8 high part, high parts summed
+    as byte fields mod 2^3) equals the u64-word form, the gather and the oracle -- at B = 1 and 128 through
+    the step split (partial sums + k_ks_combine), at 1029 without it; the rows of maximal entries (qKS - 1)
+    put every byte field at its bound."""
+    name, op, ctx, orc = ks_ctx
+    if op.qKS != (1 << 35) or name == "TOY_N8192":
+        pytest.skip("split-word records: qKS = 2^35 with the tiled form")
+    assert ctx.knobs()["ks40"] == 1
+    ext = _ext(op, B, 40 + B)
+    split40 = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+    with ctx.knobs_set(ks40=0):
+        words = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+    gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
+    assert np.array_equal(split40, words) and np.array_equal(words, gather)
+    idx = np.unique(np.r_[0:min(B, 3), B - 1])
+    assert np.array_equal(split40[idx], orc.mkm_switch(np.ascontiguousarray(ext[idx]), op.q))

@@ -20,10 +20,49 @@ def capi():
     return tfhe_amd
 
 
-def make_pair(capi, oracle, op, cp, bsk, ksk):
+def make_pair(capi, oracle, op, cp, bsk, ksk, memo=None):
+    """(context, oracle); memo = a case key: the oracle is a MemoOracle (below)."""
     ctx = capi.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
+    orc = MemoOracle(oracle, op, bsk, ksk, memo) if memo is not None else oracle.Oracle(op, bsk, ksk)
     return ctx, orc
+
+
+_MEMO = {}
+
+
+class MemoOracle:
+    """The oracle of one case whose kernel-form parametrisations (fast / generic / gen3sf / ...) feed the same
+    keys and inputs: its results are memoised by (case, call, input digest), so the CPU restatement runs once
+    per case instead of once per kernel form (the GPU suite's time, verdict r5 item 8).  The C oracle context
+    (a copy of the keys) is created only when a result is missing."""
+
+    def __init__(self, oracle, op, bsk, ksk, key):
+        self._args, self.key, self._o = (oracle, op, bsk, ksk), key, None
+
+    def _call(self, name, *args):
+        import hashlib
+
+        h = hashlib.blake2b(digest_size=16)
+        for x in args:
+            h.update(np.ascontiguousarray(x).tobytes() if isinstance(x, np.ndarray) else repr(x).encode())
+        k = (self.key, name, h.hexdigest())
+        if k not in _MEMO:
+            if self._o is None:
+                oracle, op, bsk, ksk = self._args
+                self._o = oracle.Oracle(op, bsk, ksk)
+            _MEMO[k] = getattr(self._o, name)(*args)
+        return _MEMO[k]
+
+    def eval_acc(self, a, amod, acc):
+        return self._call("eval_acc", a, amod, acc)
+
+    def eval_floor(self, ct, mod, rb):
+        return self._call("eval_floor", ct, mod, rb)
+
+    def close(self):
+        if self._o is not None:
+            self._o.close()
+            self._o = None
 
 
 # ---------------------------------------------------------------- KATs
@@ -56,7 +95,7 @@ def std128(request, capi, oracle):
     if request.param == "generic":
         os.environ["TFHE_FORCE_GENERIC"] = "1"
     try:
-        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk, memo=("n1024", shape))
     finally:
         os.environ.pop("TFHE_FORCE_GENERIC", None)
     yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng, path=request.param)
@@ -389,7 +428,7 @@ def test_n2048_blind_rotation_parity(capi, oracle, pset, path, kernel):
     if env:
         os.environ[env[0]] = env[1]
     try:  # the environment is read at setup (tfhe_knobs); the generic kernel's form is a knob
-        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk, memo=("n2048", pset))
         assert ctx.info().br_kernel == kernel
         ctx.set_knobs(**knob)
         B = 2
@@ -424,7 +463,7 @@ def test_logq_blind_rotation_parity(capi, oracle, arb, logq, path, kernel):
     if env:
         os.environ[env[0]] = env[1]
     try:  # both read at setup (TFHE_SF2 into the sf2 knob)
-        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk, memo=("logq", arb, logq))
         assert ctx.info().br_kernel == kernel
         B = 3
         acc = rs.integers(0, op.Q, (B, 2, op.N), dtype=np.uint64)
@@ -463,7 +502,7 @@ def test_n1024_digit_shapes_parity(capi, oracle, shape, path):
     if path == "generic":
         os.environ["TFHE_FORCE_GENERIC"] = "1"
     try:
-        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk, memo=("n1024", shape))
     finally:
         os.environ.pop("TFHE_FORCE_GENERIC", None)
     assert ctx.info().br_kernel == (1 if path == "fast" else 0)

@@ -78,3 +78,15 @@ def test_valid_keys_gates_decrypt(oracle):
         out = o.eval_bin_gate(g, c1, c2)
         got = [oracle.decrypt(p, sk, r, 4, p.q) for r in out]
         assert got == [f(int(x), int(y)) for x, y in zip(m1, m2)], g
+
+
+def test_keygen_stream_is_pinned(oracle):
+    """or_keygen draws every key row from its own position of the one splitmix64 stream (counter-addressed, so
+    the rows fill in parallel since round 6); the digests were recorded from the sequential round-5 walk, and
+    the caller's stream continues after the keys exactly as it did."""
+    op = oracle.params_from_set("TOY")
+    r = oracle.Rng(31)
+    sk, bsk, ksk = oracle.keygen(op, r)
+    assert (oracle.fnv1a64(sk), oracle.fnv1a64(bsk), oracle.fnv1a64(ksk)) == (
+        0x3045E07F7AFCD29, 0x7865F86830D66F63, 0x95776A0E9FA5F7EC)
+    assert int(oracle.splitmix(r, 1, 1 << 62)[0]) == 1223636499923748511

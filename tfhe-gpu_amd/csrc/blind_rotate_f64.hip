@@ -730,9 +730,21 @@ __device__ __forceinline__ uint32_t fsw(uint32_t e) { return F64D_FSW ? e ^ ((e 
 // (116 KiB of LDS with the whole factor table: one workgroup per CU), so the round's state fits registers
 // without spills (182 VGPRs with four key groups in flight).
 // PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a
-// partner that never arrives would, and the polls are bounded 2^14 times.  PROBE 2 (timing only, results
+// partner that never arrives would, and the wait is a 64th of the 10 ms bound.  PROBE 2 (timing only, results
 // invalid): no hand-off at all -- each member takes its own stage-1 values for its partner's -- the
 // bound on what the exchange costs per round
+// Hardware assumptions of the hand-off (verdict r5 item 7):
+//  * ordering: the data stores and the flag are RELAXED agent-scope atomics (write-through past the CU, `sc1`);
+//    the data is ordered before the flag by every wave's `s_waitcnt vmcnt(0)` (each store acknowledged) and the
+//    workgroup barrier, and on the reader by the poll's load returning before the barrier and the loads behind
+//    it.  That is gfx9 ISA behaviour (the MI355X_MICROARCH.md hand-off table's sc1 row), not a HIP-memory-model
+//    release / acquire pair -- one of those costs about 1.7 us per round, more than the hand-off itself;
+//  * pairing: members b and b + 8 share an XCD only through round-robin workgroup dispatch; correctness never
+//    depends on it (agent scope), the latency does (same-XCD hand-offs measured 1.1-1.3 us, cross-XCD 1.9-2.0);
+//  * liveness: both members must be resident at once.  The launcher runs the duo form only for batches up to the
+//    device's co-resident pairs (one 116-KiB workgroup per CU: half the CU count) and fences duo launches of one
+//    device's buffer across streams; a partner still missing after 10 ms of wall clock (s_memrealtime, e.g.
+//    behind another context's kernel) fails the pair, and the rescue launch recomputes it exactly.
 // The hand-off is one flag per member per round (workgroup barrier, t == 0 stores / polls, barrier).  Forms
 // measured against it and removed (tools/duo_probe.py, us per round at 128 ciphertexts): data-tagged granules
 // (value + round tag in one 8-byte word, no flag or barriers) polling the four words one after another 8.03

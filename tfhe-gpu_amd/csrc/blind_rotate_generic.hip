@@ -1461,8 +1461,11 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
 // 1.1-1.3 us per round with b, b + 8 pairing).  Per workgroup and round: half the forward
 // transforms and half the products of sf2<2>, the same monomial and inverse work.
 // Pairs are blocks b and b + 8 (one XCD under round-robin dispatch; correctness does not depend
-// on it).  Every poll is bounded (the launcher admits at most 256 pairs, all resident at two
-// workgroups per CU, so a partner can only be late behind other work on the CUs): a member that
+// on it).  The hand-off's ordering rests on gfx9 ISA behaviour (relaxed agent-scope stores drained by
+// vmcnt(0) before the barrier and the flag), as f64wduo's (blind_rotate_f64.hip states the assumptions).
+// Every wait is bounded by 10 ms of wall clock (s_memrealtime); the launcher admits only batches whose
+// pairs are all co-resident (one 135-KiB workgroup per CU: half the CU count) and fences duo launches
+// across streams, so a partner can only be late behind another context's work: a member that
 // times out sets its pair's failed word, adds one to X.err (a count since setup, tfhe_info.duo_timeouts)
 // and leaves the round loop; its partner then times out too (the flags it waits for never come).  Each
 // member saves its input polynomial first (X.save), and the launcher queues k_blind_rotate_sf2<2, true>
@@ -1476,7 +1479,7 @@ __device__ __forceinline__ uint64_t duo_load(const uint64_t* p) {
 }
 
 // PROBE 1 (test library only, TFHE_TEST_PROBES; tests/test_gpu_duo.py): member 1 of pair 0 stops publishing
-// at round 2, as a partner that never arrives would, and the polls are bounded 2^14 times, not 2^24
+// at round 2, as a partner that never arrives would, and the wait is a 64th of the 10 ms bound
 #ifndef SF2D_KPRE
 #define SF2D_KPRE 2
 #endif

@@ -121,6 +121,7 @@ struct Device {
     void* bsk_fast = nullptr;
     void* keys_f64 = nullptr;  // exact-FP64 path: centred double tables + BSK
     void* keys_sf = nullptr;   // special-form path: W1 = w 2^32 mod Q of the arena's tables and BSK, factor rows
+    void* ks40 = nullptr;      // split-word key-switch records of 8-byte keys (ks_tiled.hip k_pack_ks40)
     DuoDev duo;                // two-workgroup forms (sf2duo, f64wduo): exchange buffers, wait deadline, co-resident
                                // pairs, launch fence (kernels.hpp DuoDev; alloc_duo)
     Scratch sc;
@@ -205,8 +206,8 @@ const char* knob_out_of_range(const Knobs& k) {
     if (k.duo < 0 || k.duo > 256) return "duo (TFHE_DUO) not in 0..256";
     if (k.split4 < 0) return "split4 (TFHE_SPLIT4) < 0";
     if (k.f64w != 1) return "f64w (TFHE_F64W): the slot-layout FP64 kernel it selected was retired in round 5 (must be 1)";
-    for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.sf2, k.sf2p, k.trace})
-        if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_SF2, TFHE_SF2P) "
+    for (int32_t v : {k.ks_pk, k.wire, k.acc_flags, k.sf2, k.sf2p, k.trace, k.ks40})
+        if (v < 0 || v > 1) return "a 0/1 knob (TFHE_KS_PK, TFHE_WIRE, TFHE_ACC_FLAGS, TFHE_SF2, TFHE_SF2P, TFHE_KS40) "
                                    "not 0 or 1";
     if (k.probe < 0) return "probe < 0";
     return nullptr;
@@ -246,6 +247,7 @@ Knobs knobs_from_env(std::string& bad) {
     num("TFHE_DUO", k.duo);
     num("TFHE_SF2P", k.sf2p);
     num("TFHE_SPLIT4", k.split4);
+    num("TFHE_KS40", k.ks40);
     num("TFHE_GENERIC", k.generic);
     if (const char* e = std::getenv("TFHE_GENERIC_V1"); e && e[0] == '1') k.generic = 1;    // round-3 names
     if (const char* e = std::getenv("TFHE_GENERIC_GEN3"); e && e[0] == '0') k.generic = 2;
@@ -415,6 +417,11 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
         if (f64_duo_form(c->br, c->f64_fold)) SCHECK(alloc_duo(d));
         HCHECK(hipStreamSynchronize(d.stream));
     }
+    if (c->ksk_bits == 64 && ks40_bytes(c->ks) > 0) {  // the logQ contexts' KSK (qKS = 2^35) as split words
+        HCHECK(hipMalloc(&d.ks40, ks40_bytes(c->ks)));
+        HCHECK(launch_pack_ks40(c->ks, d.arena + c->layout.ksk, d.ks40, d.stream));
+        HCHECK(hipStreamSynchronize(d.stream));
+    }
     if (c->use_sf) {
         HCHECK(hipMalloc(&d.keys_sf, sf_bytes(c->br)));
         HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
@@ -433,6 +440,7 @@ void free_device(Device& d) {
     hipFree(d.bsk_fast);
     hipFree(d.keys_f64);
     hipFree(d.keys_sf);
+    hipFree(d.ks40);
     hipFree(d.duo.base);
     if (d.duo.fence) hipEventDestroy(d.duo.fence);
     delete d.duo.mu;
@@ -580,7 +588,7 @@ tfhe_status dev_mkm(tfhe_ctx* c, Device& d, const uint64_t* ext, uint64_t fmod, 
     const size_t tmin = ks_tiled_min(c);
     if (tmin && B >= tmin && d.sc.ks && B <= d.sc.ks_cap) {
         const hipError_t e = launch_ks_tiled(c->ks, c->ksk_bits, d.arena + c->layout.ksk, d.arena + c->layout.kskb,
-                                             ext, fmod, out, B, d.sc.ks, d.stream, c->kn);
+                                             ext, fmod, out, B, d.sc.ks, d.stream, c->kn, d.ks40);
         if (e != hipErrorNotSupported) {
             HCHECK(e);
             return TFHE_OK;

@@ -36,6 +36,7 @@ struct Knobs {
                                 // f64wduo: STD128Q class; <= 256); 0: never
     int32_t sf2p = 1;           // 0: sf2 with one ciphertext per workgroup instead of two (sf2p) above the duo batches
     int32_t split4 = 384;       // STD128 class: batches up to this size run fast4's two-group form (SPLIT); 0: never
+    int32_t ks40 = 1;           // 8-byte keys with qKS = 2^(33..37): the tiled key switch on split-word records; 0: u64
 };
 
 // Device tables for one (Q, N), word type W (uint32_t or uint64_t storage).
@@ -193,8 +194,13 @@ hipError_t launch_mkm(const KSParams& P, int ksk_bits, const void* kska, const v
 // (transposed digit planes).  hipErrorNotSupported when dKS > 16 or baseKS too large.
 size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B);
 bool ks_tiled_supported(const KSParams& P);
+// ksk40: the split-word records of 8-byte keys (ks40_bytes > 0: qKS = 2^(32+b), 1 <= b <= 5, the logQ contexts;
+// derived at setup by launch_pack_ks40 from the arena's u64 KSK); nullptr: the u64 form
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
-                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn);
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn,
+                           const void* ksk40 = nullptr);
+size_t ks40_bytes(const KSParams& P);
+hipError_t launch_pack_ks40(const KSParams& P, const void* kska, void* out, hipStream_t s);
 
 // ---- test vectors, extraction and LWE glue (binfhe-base-scheme.cpp) ----
 enum TvMode : uint32_t {

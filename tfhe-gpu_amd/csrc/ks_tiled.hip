@@ -287,6 +287,202 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split-word form for the logQ contexts' 8-byte keys (verdict r5 item 5): qKS = 2^(32+b), 1 <= b <= 5
+// (2^35 there), so every key word is below 2^(32+b).  k_pack_ks40 derives, once at setup, one 80-byte
+// record per (KSK row, 16-column tile): the 16 low words (u32, 64 B), then the 16 high parts (u8, 16 B) --
+// 80 B of LDS and L2 traffic per row segment against 128 B of u64 words.  The column sums only matter mod
+// qKS: the low words sum exactly in u64 (one v_mad_u64_u32 with a unit factor each, as the u64 form's add);
+// the high parts sum as byte fields of u32 words, four columns per add, reduced mod 2^b after every stage
+// of four steps (a field stays below 5 * 2^b <= 160, no carry into its neighbour); a column's sum is
+// lo + (field mod 2^b) 2^32, congruent to the exact sum mod qKS.  Records are contiguous, so a row
+// segment is five 16-byte pieces and the staging of k_ks_tiled carries over unchanged.
+constexpr int K40_CT = 16, K40_REC = 80, K40_PIECES = K40_REC / 16;
+
+__global__ void k_pack_ks40(const uint64_t* __restrict__ ksk, size_t rows, uint32_t n, uint32_t npad64,
+                            uint32_t ntiles, unsigned char* __restrict__ out) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;  // (row, tile, column)
+    if (idx >= rows * ntiles * K40_CT) return;
+    const uint32_t col = (uint32_t)(idx % K40_CT);
+    const size_t rt = idx / K40_CT, row = rt / ntiles;
+    const uint32_t cc = (uint32_t)(rt % ntiles) * K40_CT + col;
+    const uint64_t w = cc < n ? ksk[row * npad64 + cc] : 0;  // columns past n are never written out
+    unsigned char* rec = out + rt * K40_REC;
+    reinterpret_cast<uint32_t*>(rec)[col] = (uint32_t)w;
+    rec[64 + col] = (unsigned char)(w >> 32);
+}
+
+__device__ __forceinline__ uint64_t mad_u64_u32_1(uint32_t x, uint64_t acc) {  // acc + x in one VALU
+    uint64_t r, junk;  // (the carry-out lane mask is never read)
+    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(junk) : "v"(x), "v"(acc));
+    return r;
+}
+
+template <int CTS, int MAXL, int G>
+__global__ void __launch_bounds__(KT, 2) k_ks_tiled40(KSParams P, const unsigned char* __restrict__ rec,
+                                                   const uint64_t* __restrict__ kskb, const uint32_t* __restrict__ dig,
+                                                   const uint64_t* __restrict__ bq, size_t B, size_t Bp, uint32_t nct,
+                                                   uint32_t ncol, uint64_t fmod, uint64_t* __restrict__ out,
+                                                   uint32_t nsplit, uint64_t* __restrict__ part, uint32_t hbits) {
+    static_assert(G == 2 || G == 4, "a stage is half or all of a digit word");
+    extern __shared__ __align__(16) unsigned char sm[];
+    const uint32_t bks = P.baseKS, dks = P.dKS, n = P.n;
+    const uint32_t th = threadIdx.x;
+    const uint32_t per_split = gridDim.x / nsplit, split = blockIdx.x / per_split;
+    const uint32_t L = blockIdx.x - split * per_split, k = L >> 3;
+    const uint32_t col_tile = (k / nct) * 8 + (L & 7), ct_tile = k % nct;  // (k_ks_tiled's XCD-aware mapping)
+    if (col_tile >= ncol) return;  // whole workgroup
+    const uint32_t c0 = col_tile * K40_CT;
+    const size_t t0 = (size_t)ct_tile * KT * CTS;
+    const bool bcol = col_tile == 0;
+    const uint32_t step_bytes = bks * K40_REC;
+    const uint32_t stage_bytes = G * step_bytes;
+    uint64_t* bb = reinterpret_cast<uint64_t*>(sm + 2 * stage_bytes);  // [2][G][baseKS] B entries
+    const uint32_t npieces = bks * K40_PIECES;                          // per step
+    // staging slots as in k_ks_tiled: everything lane-dependent fixed for the launch
+    const uint32_t lps = (npieces + KT - 1) / KT;
+    const uint64_t dmagic = ((1ull << 32) + dks - 1) / dks;
+    const uint32_t bd = bks * dks;
+    const size_t rec_step = (size_t)ncol * K40_REC;  // bytes per KSK row (all its tiles)
+    uint32_t st_of[MAXL], loff[MAXL], sto[MAXL];
+#pragma unroll
+    for (int l = 0; l < MAXL; ++l) {
+        const uint32_t st = (uint32_t)l / lps, r = ((uint32_t)l - st * lps) * KT + th;
+        const uint32_t rr = min(r, npieces - 1);
+        const uint32_t v = rr / K40_PIECES, pc = rr - v * K40_PIECES;
+        st_of[l] = min(st, (uint32_t)G - 1);
+        loff[l] = (uint32_t)(v * dks * rec_step) + col_tile * K40_REC + pc * 16;
+        sto[l] = (st < (uint32_t)G && r < npieces) ? st * step_bytes + v * K40_REC + pc * 16 : ~0u;
+    }
+    const uint32_t vb = min(th, bks - 1) * dks;
+    const uint32_t hmask = 0x01010101u * ((1u << hbits) - 1);
+    u32x4 stgX[MAXL], stgY[MAXL];
+    uint64_t bX[G], bY[G];
+    uint32_t dX[CTS], dY[CTS];
+    uint64_t acc[CTS][K40_CT];
+    uint32_t hs[CTS][K40_CT / 4];
+    uint64_t bsum[CTS];
+#pragma unroll
+    for (int c = 0; c < CTS; ++c) {
+        bsum[c] = 0;
+#pragma unroll
+        for (int kk = 0; kk < K40_CT; ++kk) acc[c][kk] = 0;
+#pragma unroll
+        for (int m = 0; m < K40_CT / 4; ++m) hs[c][m] = 0;
+    }
+#pragma unroll
+    for (int st = 0; st < G; ++st) bX[st] = bY[st] = 0;
+#define K40_LOAD(STG, BSTG, DGV, gg)                                                                \
+    do {                                                                                            \
+        _Pragma("unroll") for (int c = 0; c < CTS; ++c)                                             \
+            DGV[c] = dig[(size_t)((gg) * G / 4) * Bp + t0 + th + KT * c] >> (8 * (((gg) * G) % 4)); \
+        _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
+            const uint32_t s_ = (gg) * G + st_of[l];                                                \
+            const uint32_t i = (uint32_t)(((uint64_t)s_ * dmagic) >> 32), j = s_ - i * dks;         \
+            const unsigned char* pb = rec + ((size_t)i * bd + j) * rec_step;                        \
+            STG[l] = *reinterpret_cast<const u32x4*>(pb + loff[l]);                                 \
+        }                                                                                           \
+        if (bcol) {                                                                                 \
+            _Pragma("unroll") for (int st = 0; st < G; ++st) {                                      \
+                const uint32_t s_ = (gg) * G + st;                                                  \
+                const uint32_t i = (uint32_t)(((uint64_t)s_ * dmagic) >> 32), j = s_ - i * dks;     \
+                BSTG[st] = kskb[(size_t)i * bd + j + vb];                                           \
+            }                                                                                       \
+        }                                                                                           \
+    } while (0)
+#define K40_STORE(STG, BSTG, gg)                                                                    \
+    do {                                                                                            \
+        unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                          \
+        _Pragma("unroll") for (int l = 0; l < MAXL; ++l) {                                          \
+            if (sto[l] != ~0u) *reinterpret_cast<u32x4*>(b_ + sto[l]) = STG[l];                     \
+        }                                                                                           \
+        if (bcol && th < bks) {                                                                     \
+            _Pragma("unroll") for (int st = 0; st < G; ++st) bb[(((gg) & 1) * G + st) * bks + th] = BSTG[st]; \
+        }                                                                                           \
+    } while (0)
+#define K40_SUM(DGV, gg)                                                                            \
+    do {                                                                                            \
+        const unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                    \
+        _Pragma("unroll 1") for (int st = 0; st < G; ++st) {                                        \
+            _Pragma("unroll") for (int c = 0; c < CTS; ++c) {                                       \
+                const uint32_t d = (DGV[c] >> (8 * st)) & 0xff;                                     \
+                const unsigned char* r = b_ + st * step_bytes + d * K40_REC;                        \
+                _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                     \
+                    const u32x4 u = *reinterpret_cast<const u32x4*>(r + p * 16);                    \
+                    acc[c][4 * p + 0] = mad_u64_u32_1(u.x, acc[c][4 * p + 0]);                      \
+                    acc[c][4 * p + 1] = mad_u64_u32_1(u.y, acc[c][4 * p + 1]);                      \
+                    acc[c][4 * p + 2] = mad_u64_u32_1(u.z, acc[c][4 * p + 2]);                      \
+                    acc[c][4 * p + 3] = mad_u64_u32_1(u.w, acc[c][4 * p + 3]);                      \
+                }                                                                                   \
+                const u32x4 h = *reinterpret_cast<const u32x4*>(r + 64);                            \
+                hs[c][0] += h.x, hs[c][1] += h.y, hs[c][2] += h.z, hs[c][3] += h.w;                 \
+                if (bcol) bsum[c] += bb[(((gg) & 1) * G + st) * bks + d];                           \
+            }                                                                                       \
+        }                                                                                           \
+        _Pragma("unroll") for (int c = 0; c < CTS; ++c)                                             \
+            _Pragma("unroll") for (int m = 0; m < 4; ++m) hs[c][m] &= hmask;                        \
+    } while (0)
+    const uint32_t stages = P.N * dks / G;
+    const uint32_t s_len = stages / nsplit, s_lo = split * s_len, s_hi = s_lo + s_len;
+    K40_LOAD(stgX, bX, dX, s_lo);
+    K40_LOAD(stgY, bY, dY, s_lo + 1);
+    for (uint32_t g = s_lo; g < s_hi; g += 2) {
+        K40_STORE(stgX, bX, g);
+        uint32_t dXc[CTS];
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) dXc[c] = dX[c];
+        K40_LOAD(stgX, bX, dX, min(g + 2, s_hi - 2));
+        __syncthreads();
+        K40_SUM(dXc, g);
+        K40_STORE(stgY, bY, g + 1);
+        uint32_t dYc[CTS];
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) dYc[c] = dY[c];
+        K40_LOAD(stgY, bY, dY, min(g + 3, s_hi - 1));
+        __syncthreads();
+        K40_SUM(dYc, g + 1);
+    }
+#undef K40_LOAD
+#undef K40_STORE
+#undef K40_SUM
+    // column kk's sum, congruent mod qKS = 2^(32 + hbits)
+    auto colsum = [&](int c, int kk) -> uint64_t {
+        return acc[c][kk] + ((uint64_t)((hs[c][kk >> 2] >> (8 * (kk & 3))) & ((1u << hbits) - 1)) << 32);
+    };
+    if (nsplit > 1) {
+#pragma unroll
+        for (int c = 0; c < CTS; ++c) {
+            const size_t ct = t0 + th + KT * c;
+            if (ct >= B) continue;
+            uint64_t* o = part + ((size_t)split * B + ct) * (size_t)(n + 1);
+#pragma unroll
+            for (int kk = 0; kk < K40_CT; ++kk)
+                if (c0 + kk < n) o[c0 + kk] = colsum(c, kk);
+            if (bcol) o[n] = bsum[c];
+        }
+        return;
+    }
+    const uint64_t qks = P.qKS;
+#pragma unroll
+    for (int c = 0; c < CTS; ++c) {
+        const size_t ct = t0 + th + KT * c;
+        if (ct >= B) continue;
+        uint64_t* o = out + ct * (size_t)(n + 1);
+#pragma unroll
+        for (int kk = 0; kk < K40_CT; ++kk) {
+            const uint32_t col = c0 + kk;
+            if (col < n) {
+                const uint64_t r = colsum(c, kk) % qks;
+                o[col] = round_qQ(r == 0 ? 0 : qks - r, fmod, qks);  // 0 - sum
+            }
+        }
+        if (bcol) {
+            const uint64_t r = bsum[c] % qks, x = bq[ct];
+            o[n] = round_qQ(x >= r ? x - r : x + (qks - r), fmod, qks);  // b - sum
+        }
+    }
+}
+
 // sum of the splits' partial sums (u64; u32 partials that wrapped mod 2^32 only when qKS divides
 // 2^32, launch_ks_tiled), then the key switch's finish as in k_ks_tiled
 __global__ void __launch_bounds__(256) k_ks_combine(KSParams P, const uint64_t* __restrict__ part, uint32_t nsplit,
@@ -369,6 +565,38 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     return hipGetLastError();
 }
 
+uint32_t ks40_tiles(const KSParams& P) { return (P.n + K40_CT - 1) / K40_CT; }
+
+// the split-word form's width: qKS = 2^(32 + b) with 1 <= b <= 5 (0: not applicable)
+uint32_t ks40_hbits(const KSParams& P) {
+    if ((P.qKS & (P.qKS - 1)) != 0 || P.qKS <= (1ull << 32) || P.qKS > (1ull << 37)) return 0;
+    return (uint32_t)__builtin_ctzll(P.qKS) - 32;
+}
+
+template <int CTS, int G = 4>
+hipError_t launch_tiled40(const KSParams& P, const void* rec, const void* kskb, const uint32_t* dig, const uint64_t* bq,
+                          size_t B, size_t Bp, uint64_t fmod, uint64_t* out, uint64_t* part, hipStream_t s,
+                          const Knobs& kn, uint32_t hbits) {
+    const size_t lds = 2 * (size_t)G * P.baseKS * K40_REC + 2 * (size_t)G * P.baseKS * sizeof(uint64_t);
+    const size_t lpt = (size_t)G * ((P.baseKS * K40_PIECES + KT - 1) / KT);
+    if (lds > 80 * 1024 || lpt > 4) return hipErrorNotSupported;
+    auto k = k_ks_tiled40<CTS, 4, G>;
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
+    const uint32_t ncol = ks40_tiles(P);
+    const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
+    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, true);
+    hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const unsigned char*)rec, (const uint64_t*)kskb,
+                       dig, bq, B, Bp, nct, ncol, fmod, out, nsplit, part, hbits);
+    if (nsplit > 1) {
+        const size_t words = B * (P.n + 1);
+        hipLaunchKernelGGL(k_ks_combine, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, s, P, part, nsplit, bq,
+                           B, fmod, out);
+    }
+    return hipGetLastError();
+}
+
 constexpr size_t kTileMax = 4 * KT;  // the largest ciphertext tile of the builds below
 
 size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; }
@@ -385,6 +613,18 @@ size_t ks_tiled_scratch_bytes(const KSParams& P, size_t B) {
     return (size_t)P.N * P.dKS * Bp + Bp * sizeof(uint64_t) + ks_tiled_part_words(P, B) * sizeof(uint64_t);
 }
 
+size_t ks40_bytes(const KSParams& P) {
+    return ks40_hbits(P) ? (size_t)P.N * P.baseKS * P.dKS * ks40_tiles(P) * K40_REC : 0;
+}
+
+hipError_t launch_pack_ks40(const KSParams& P, const void* kska, void* out, hipStream_t s) {
+    if (!ks40_hbits(P)) return hipErrorNotSupported;
+    const size_t rows = (size_t)P.N * P.baseKS * P.dKS, threads = rows * ks40_tiles(P) * K40_CT;
+    hipLaunchKernelGGL(k_pack_ks40, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, (const uint64_t*)kska,
+                       rows, P.n, P.n_pad, ks40_tiles(P), (unsigned char*)out);
+    return hipGetLastError();
+}
+
 bool ks_tiled_supported(const KSParams& P) {
     // even stage count; step indices s < N dKS far below 2^32 / dKS (k_ks_tiled's magic-multiply s / dKS)
     return P.dKS >= 1 && P.dKS <= KS_MAX_DKS && P.baseKS <= 256 && (P.N * P.dKS) % (8 * GMAX) == 0 &&
@@ -392,7 +632,8 @@ bool ks_tiled_supported(const KSParams& P) {
 }
 
 hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, const void* kskb, const uint64_t* ext,
-                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn) {
+                           uint64_t fmod, uint64_t* out, size_t B, void* scratch, hipStream_t s, const Knobs& kn,
+                           const void* ksk40) {
     if (B == 0) return hipSuccess;
     if (!ks_tiled_supported(P)) return hipErrorNotSupported;
     const bool acc32 = (unsigned __int128)P.N * P.dKS * (P.qKS - 1) < ((unsigned __int128)1 << 32);
@@ -428,6 +669,12 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
             return cts == 2 ? launch_tiled<uint32_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
                             : launch_tiled<uint32_t, uint64_t, 32, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
         default:
+            // the split-word records (ks40 knob, default on; 0: the u64 form, A/B runs and tests)
+            if (ksk40 && kn.ks40 && ks40_hbits(P)) {
+                const hipError_t e40 = cts == 2 ? launch_tiled40<2>(P, ksk40, kskb, dig, bq, B, Bp, fmod, out, part, s, kn, ks40_hbits(P))
+                                                : launch_tiled40<1>(P, ksk40, kskb, dig, bq, B, Bp, fmod, out, part, s, kn, ks40_hbits(P));
+                if (e40 != hipErrorNotSupported) return e40;
+            }
             return cts == 2 ? launch_tiled<uint64_t, uint64_t, 16, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
                             : launch_tiled<uint64_t, uint64_t, 16, 1>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
     }

@@ -12,9 +12,9 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tfhe-gpu_a
 _ROOT = os.path.dirname(_PKG)
 _LIB = os.environ.get("TFHE_LIB", os.path.join(_PKG, "lib", "libtfhe_hip.so"))  # override: alternative builds
 HEADER = os.path.join(_ROOT, "include", "tfhe_hip.h")
-ABI_VERSION = 7  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays;
+ABI_VERSION = 8  # TFHE_HIP_ABI_VERSION of include/tfhe_hip.h (3: tfhe_info.replicate_*; 4: row-pointer host arrays;
                  # 5: device-resident EvalFunc / EvalFloor / EvalSign; 6: knobs.duo, info.duo_timeouts;
-                 # 7: knobs.split4)
+                 # 7: knobs.split4; 8: knobs.ks40, tfhe_rccl_selftest)
 
 # BINFHE_PARAMSET / BINGATE (binfhe-constants.h:46-101)
 PARAMSETS = {"TOY": 0, "MEDIUM": 1, "STD128_AP": 2, "STD128_APOPT": 3, "STD128": 4, "STD128_OPT": 5, "STD192": 6,
@@ -55,7 +55,7 @@ class Knobs(C.Structure):
     """tfhe_knobs: launch choices of a context (include/tfhe_hip.h), environment at setup, then tfhe_set_knobs."""
     _fields_ = [(k, C.c_int32) for k in ("ks_tiled_min", "ks_cts", "ks_split", "ks_pk", "host_parts", "wire",
                                          "acc_flags", "f64w", "sf2", "generic", "trace", "probe", "duo",
-                                         "sf2p", "split4")]
+                                         "sf2p", "split4", "ks40")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -159,7 +159,7 @@ def lib(path: str | None = None):
         # (tools/ab_lib.sh) may set TFHE_ABI_PREV=1 to admit ABI 6: its tfhe_knobs / tfhe_info are
         # prefixes of these, so reads and writes stay in bounds
         abi = L.tfhe_abi_version()
-        if abi != ABI_VERSION and not (abi == ABI_VERSION - 1 and os.environ.get("TFHE_ABI_PREV") == "1"):
+        if abi != ABI_VERSION and not (6 <= abi < ABI_VERSION and os.environ.get("TFHE_ABI_PREV") == "1"):
             raise TfheError(-1, "load", f"{path} has ABI {L.tfhe_abi_version()}, binding expects {ABI_VERSION}: "
                                         "rebuild (make -C tfhe-gpu_amd)")
         _libs[path] = L

@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="override the batch")
     ap.add_argument("--batches", default="", help="comma-separated batch sweep")
-    ap.add_argument("--splits", default="16", help="comma-separated ks_split caps for the tiled form")
+    ap.add_argument("--splits", default="32", help="comma-separated ks_split caps for the tiled form")
+    ap.add_argument("--ks40", default="0,1", help="ks40 knob values timed for the tiled form (8-byte keys: the u64 "
+                                                 "words = 0, the split-word records = 1; ignored elsewhere)")
     args = ap.parse_args()
     import torch
 
@@ -54,9 +56,11 @@ def main():
             ext = full[:B].contiguous()
             outs = {}
             res = {"config": name, "batch": B, "N": p.N, "n": p.n, "qKS": p.qKS, "baseKS": p.baseKS, "dKS": p.dKS}
-            modes = [("gather", 0, 16)] + [(f"tiled_split{z}", 1, int(z)) for z in args.splits.split(",")]
-            for mode, tmin, split in modes:
-                ctx.set_knobs(ks_tiled_min=tmin, ks_split=split)
+            k40 = [int(x) for x in args.ks40.split(",")] if p.qKS > (1 << 32) else [1]
+            modes = [("gather", 0, 16, 1)] + [(f"tiled_split{z}" + (f"_ks40{k}" if len(k40) > 1 else ""), 1, int(z), k)
+                                              for z in args.splits.split(",") for k in k40]
+            for mode, tmin, split, k in modes:
+                ctx.set_knobs(ks_tiled_min=tmin, ks_split=split, ks40=k)
                 out = torch.empty((B, p.n + 1), dtype=torch.int64, device="cuda")
                 call = lambda: capi.check(capi.lib().tfhe_mkm_switch_device(ctx.handle, B, ext.data_ptr(), p.q,
                                                                             out.data_ptr(), s.cuda_stream), "mkm")
@@ -70,7 +74,7 @@ def main():
                 s.synchronize()
                 outs[mode] = out.cpu().numpy()
                 res[f"{mode}_ms"] = round(e0.elapsed_time(e1) / args.reps, 3)
-            ctx.set_knobs(ks_tiled_min=-1, ks_split=16)
+            ctx.set_knobs(ks_tiled_min=-1, ks_split=32, ks40=1)
             res["equal"] = all(np.array_equal(outs["gather"], v) for v in outs.values())
             print(json.dumps(res), flush=True)
         ctx.GPUClean()
