@@ -494,9 +494,12 @@ def main():
     if rank == 0:
         bsk, ksk = synthetic_keys(p)
         ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath).GPUSetup(bsk, ksk)
-    # the host keys are not held through the timed run (C3's KSK alone is 4.8 GB); the oracle check and the
-    # port fallback regenerate them deterministically (synthetic_keys) after it
-    bsk = ksk = None
+        # large host keys are not held through the timed run (C3 / C5b: a 4.8 GB KSK); the oracle check and the
+        # port fallback regenerate them deterministically (synthetic_keys) after it
+        if bsk.nbytes + ksk.nbytes > (3 << 30):
+            bsk = ksk = None
+    else:
+        bsk = ksk = None
     if world > 1:
         # one RCCL broadcast of the packed device key image over xGMI (tfhe_amd/dist.py)
         img = None

@@ -206,7 +206,8 @@ void load_keys(Setup& s, const uint64_t* bsk_coeff, const uint64_t* ksk) {
 // ---- ciphertexts ------------------------------------------------------------------------
 size_t g_limit = 0;  // sizes= sweep: ciphertexts read from each input (0 = all)
 bool g_batch = false;      // batch= mode: several ops per process
-bool g_gpu_setup = false;  // batch= mode: GPUSetup done (once, by the first vector op)
+bool g_gpu_setup = false;  // batch= mode: GPUSetup done (by the first vector op, again when gpus= changes)
+int g_gpus = 0;
 
 std::vector<LWECiphertext> read_cts(const std::string& path, uint32_t n, uint64_t mod) {
     auto w = read_u64(path);
@@ -391,11 +392,14 @@ int run_op(Setup& s, or_rng& rng, std::ostringstream& js) {
 
     const std::string api = arg("api", "vector");
     const int reps = (int)arg_u64("reps", 1);
-    if (api == "vector" && !g_gpu_setup) {
+    const int gpus = (int)arg_u64("gpus", 0);
+    if (api == "vector" && (!g_gpu_setup || gpus != g_gpus)) {  // (a batch line with another gpus= sets up again)
+        if (g_gpu_setup) s.cc.GPUClean();
         double ts = now_s();
-        s.cc.GPUSetup((int)arg_u64("gpus", 0));
+        s.cc.GPUSetup(gpus);
         js << ",\"gpu_setup_s\":" << (now_s() - ts);
         g_gpu_setup = g_batch;  // a batch keeps it for its later ops
+        g_gpus = gpus;
     }
     std::vector<uint64_t> out;
     double best = 1e30, total = 0;

@@ -26,49 +26,47 @@ CASES = ["std128_NAND", "std128_AND", "std128_XOR", "std128_XNOR_FAST", "std128_
          "toy8192_sign"]
 
 
-def run_dropin(c, tmp, extra=(), gpus=1, env=None):
-    files = refvec.write_inputs(c, DATA["fixtures"], tmp)
-    args = [DROPIN, f"ctx={c['ctx']}", f"keys={c['keys']}", f"op={c['op']}", "api=vector", f"gpus={gpus}"]
-    args += [f"{k}={v}" for k, v in files.items()]
-    if c["mod"] is not None:
-        args.append(f"mod={c['mod']}")
-    args += [f"{k}={v}" for k, v in c["args"].items()] + list(extra)
-    r = subprocess.run(args, capture_output=True, text=True, timeout=600, env=dict(os.environ, **(env or {})))
-    assert r.returncode == 0, r.stderr[-2000:]
-    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
-
-
 _GROUPS = {}
 
 
-def run_group(name):
-    """The case's JSON line from one ref_dropin process per (ctx, keys) group of CASES (ref_driver batch=: one
-    context, one key load and one GPUSetup for every op of the group), run once per module."""
-    c = refvec.case(name, DATA)
-    key = (c["ctx"], c["keys"])
-    if key not in _GROUPS:
-        members = [m for m in CASES if (refvec.case(m, DATA)["ctx"], refvec.case(m, DATA)["keys"]) == key]
-        with tempfile.TemporaryDirectory() as tmp:
-            lines = []
+def run_batch(members, gpus=(1,), env=None):
+    """One ref_dropin process for cases sharing (ctx, keys) (ref_driver batch=: one context and one key load;
+    one GPUSetup per gpus value): {(case, gpus): JSON line}, and the process's stderr (the shim's timing lines)."""
+    key = (refvec.case(members[0], DATA)["ctx"], refvec.case(members[0], DATA)["keys"])
+    with tempfile.TemporaryDirectory() as tmp:
+        lines, tags = [], []
+        for g in gpus:
             for m in members:
                 cm = refvec.case(m, DATA)
-                d = os.path.join(tmp, m)
+                assert (cm["ctx"], cm["keys"]) == key
+                d = os.path.join(tmp, f"{m}_{g}")
                 os.makedirs(d)
-                toks = [f"op={cm['op']}"] + [f"{k}={v}" for k, v in refvec.write_inputs(cm, DATA["fixtures"], d).items()]
+                toks = [f"op={cm['op']}", f"gpus={g}"]
+                toks += [f"{k}={v}" for k, v in refvec.write_inputs(cm, DATA["fixtures"], d).items()]
                 if cm["mod"] is not None:
                     toks.append(f"mod={cm['mod']}")
                 toks += [f"{k}={v}" for k, v in cm["args"].items()]
                 lines.append(" ".join(toks))
-            bf = os.path.join(tmp, "batch")
-            with open(bf, "w") as f:
-                f.write("\n".join(lines) + "\n")
-            r = subprocess.run([DROPIN, f"ctx={key[0]}", f"keys={key[1]}", "api=vector", "gpus=1", f"batch={bf}"],
-                               capture_output=True, text=True, timeout=600, env=dict(os.environ))
-            assert r.returncode == 0, r.stderr[-2000:]
-            outs = [json.loads(x) for x in r.stdout.strip().splitlines()]
-        assert len(outs) == len(members), r.stdout[-2000:]
-        _GROUPS[key] = dict(zip(members, outs))
-    return _GROUPS[key][name]
+                tags.append((m, g))
+        bf = os.path.join(tmp, "batch")
+        with open(bf, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        r = subprocess.run([DROPIN, f"ctx={key[0]}", f"keys={key[1]}", "api=vector", f"batch={bf}"],
+                           capture_output=True, text=True, timeout=600, env=dict(os.environ, **(env or {})))
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert len(outs) == len(tags), r.stdout[-2000:]
+    return dict(zip(tags, outs)), r.stderr
+
+
+def run_group(name):
+    """The case's JSON line from one ref_dropin process per (ctx, keys) group of CASES, run once per module."""
+    c = refvec.case(name, DATA)
+    key = (c["ctx"], c["keys"])
+    if key not in _GROUPS:
+        members = [m for m in CASES if (refvec.case(m, DATA)["ctx"], refvec.case(m, DATA)["keys"]) == key]
+        _GROUPS[key] = run_batch(members)
+    return _GROUPS[key][0][(name, 1)]
 
 
 @pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/ref_dropin not built (make -C oracle -f Makefile.ref dropin)")
@@ -86,11 +84,13 @@ def test_reference_vector_api_on_mi355x(name):
 def test_shim_takes_the_test_vector_path():
     """EvalBinGate's accumulators reach the shim as sparse test vectors (tfhe_eval_acc_tv); an
     EvalAcc with dense accumulators takes the general path -- both give the reference's outputs."""
-    with tempfile.TemporaryDirectory() as tmp:
-        _, err = run_dropin(refvec.case("std128_NAND", DATA), tmp)
-        assert "marshal in (test vectors)" in err, err[-2000:]
-        _, err = run_dropin(refvec.case("std128_acc_amod1024", DATA), tmp)
-        assert "EvalAcc marshal in B=" in err, err[-2000:]
+    # the STD128 group's one process ran the gates (sparse test vectors) and the EvalAcc cases (dense)
+    c = refvec.case("std128_NAND", DATA)
+    assert run_group("std128_NAND")["fnv"] == c["vector"]["fnv"]
+    assert run_group("std128_acc_amod1024")["fnv"] == refvec.case("std128_acc_amod1024", DATA)["vector"]["fnv"]
+    err = _GROUPS[(c["ctx"], c["keys"])][1]
+    assert "marshal in (test vectors)" in err, err[-2000:]
+    assert "EvalAcc marshal in B=" in err, err[-2000:]
 
 
 @pytest.fixture(autouse=True)
@@ -99,6 +99,9 @@ def _shim_timing(monkeypatch):
 
 
 STUB = os.path.join(ROOT, "tests", "stub_rccl", "librccl_stub.so")
+
+
+_MULTI = {}
 
 
 @pytest.mark.skipif(not (os.path.exists(DROPIN) and os.path.exists(STUB)), reason="ref_dropin or the stub RCCL not built")
@@ -113,7 +116,10 @@ def test_reference_vector_api_over_several_devices(name, gpus):
     7 EvalFunc, 7 EvalSign on the C5a context)."""
     c = refvec.case(name, DATA)
     assert c["B"] >= 2 * gpus  # every device gets a shard (engine.hip run_shards)
-    with tempfile.TemporaryDirectory() as tmp:
-        js, err = run_dropin(c, tmp, gpus=gpus, env={"TFHE_LOGICAL_DEVICES": str(gpus), "TFHE_RCCL_LIB": STUB})
+    # one process per case: GPUSetup(2), then GPUSetup(3), on 3 logical devices (numGPUs = 2 uses two of them)
+    if name not in _MULTI:
+        _MULTI[name] = run_batch([name], gpus=(2, 3), env={"TFHE_LOGICAL_DEVICES": "3", "TFHE_RCCL_LIB": STUB})
+    outs, err = _MULTI[name]
+    js = outs[(name, gpus)]
     assert js["fnv"] == c["vector"]["fnv"], (name, gpus, js)
     assert f"[shim] GPUSetup devices={gpus} replicate_method=1" in err, err[-2000:]  # TFHE_REPLICATE_RCCL

@@ -122,11 +122,11 @@ def test_u16_keys_without_packed_sums(ks_ctx):
     assert np.array_equal(packed, plain) and np.array_equal(plain, gather)
 
 
-@pytest.mark.parametrize("B", [1, 128, 1029])
+@pytest.mark.parametrize("B", [2, 128, 1029])
 def test_split_word_keys_equal_u64_words(ks_ctx, B):
     """8-byte keys with qKS = 2^35 (ARB12 / the logQ contexts; TOY_N8192 takes the gather): the tiled key
     switch on the split-word records (ks40 = 1, the default: u32 low word + u8 high part, high parts summed
-    as byte fields mod 2^3) equals the u64-word form, the gather and the oracle -- at B = 1 and 128 through
+    as byte fields mod 2^3) equals the u64-word form, the gather and the oracle -- at B = 2 and 128 through
     the step split (partial sums + k_ks_combine), at 1029 without it; the rows of maximal entries (qKS - 1)
     put every byte field at its bound."""
     name, op, ctx, orc = ks_ctx

@@ -95,7 +95,7 @@ def std128(request, capi, oracle):
     if request.param == "generic":
         os.environ["TFHE_FORCE_GENERIC"] = "1"
     try:
-        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk, memo=("n1024", shape))
+        ctx, orc = make_pair(capi, oracle, op, cp, bsk, ksk)
     finally:
         os.environ.pop("TFHE_FORCE_GENERIC", None)
     yield dict(op=op, cp=cp, sk=sk, ctx=ctx, orc=orc, rng=rng, path=request.param)

@@ -23,8 +23,11 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 namespace tfhe {
 namespace {
@@ -298,6 +301,16 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
 // lo + (field mod 2^b) 2^32, congruent to the exact sum mod qKS.  Records are contiguous, so a row
 // segment is five 16-byte pieces and the staging of k_ks_tiled carries over unchanged.
 constexpr int K40_CT = 16, K40_REC = 80, K40_PIECES = K40_REC / 16;
+// steps of a stage unrolled in the sum loop (A/B builds: -DKS40_UNROLL=2 overlaps a step's LDS reads with the
+// previous step's sums at 204 instead of 196 VGPRs)
+#ifndef KS40_UNROLL
+#define KS40_UNROLL 1
+#endif
+#if KS40_UNROLL == 2
+#define K40_UNR _Pragma("unroll 2")
+#else
+#define K40_UNR _Pragma("unroll 1")
+#endif
 
 __global__ void k_pack_ks40(const uint64_t* __restrict__ ksk, size_t rows, uint32_t n, uint32_t npad64,
                             uint32_t ntiles, unsigned char* __restrict__ out) {
@@ -403,20 +416,26 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled40(KSParams P, const unsigned
 #define K40_SUM(DGV, gg)                                                                            \
     do {                                                                                            \
         const unsigned char* b_ = sm + ((gg) & 1) * stage_bytes;                                    \
-        _Pragma("unroll 1") for (int st = 0; st < G; ++st) {                                        \
+        K40_UNR for (int st = 0; st < G; ++st) {                                                       \
+            /* every row piece of the step for all CTS ciphertexts in flight before the first sum  \
+               (two waves per SIMD hide little LDS latency) */                                      \
+            u32x4 U[CTS][K40_PIECES];                                                               \
+            uint32_t dd[CTS];                                                                       \
             _Pragma("unroll") for (int c = 0; c < CTS; ++c) {                                       \
-                const uint32_t d = (DGV[c] >> (8 * st)) & 0xff;                                     \
-                const unsigned char* r = b_ + st * step_bytes + d * K40_REC;                        \
+                dd[c] = (DGV[c] >> (8 * st)) & 0xff;                                                \
+                const unsigned char* r = b_ + st * step_bytes + dd[c] * K40_REC;                    \
+                _Pragma("unroll") for (int p = 0; p < K40_PIECES; ++p)                              \
+                    U[c][p] = *reinterpret_cast<const u32x4*>(r + p * 16);                          \
+            }                                                                                       \
+            _Pragma("unroll") for (int c = 0; c < CTS; ++c) {                                       \
                 _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                     \
-                    const u32x4 u = *reinterpret_cast<const u32x4*>(r + p * 16);                    \
-                    acc[c][4 * p + 0] = mad_u64_u32_1(u.x, acc[c][4 * p + 0]);                      \
-                    acc[c][4 * p + 1] = mad_u64_u32_1(u.y, acc[c][4 * p + 1]);                      \
-                    acc[c][4 * p + 2] = mad_u64_u32_1(u.z, acc[c][4 * p + 2]);                      \
-                    acc[c][4 * p + 3] = mad_u64_u32_1(u.w, acc[c][4 * p + 3]);                      \
+                    acc[c][4 * p + 0] = mad_u64_u32_1(U[c][p].x, acc[c][4 * p + 0]);                \
+                    acc[c][4 * p + 1] = mad_u64_u32_1(U[c][p].y, acc[c][4 * p + 1]);                \
+                    acc[c][4 * p + 2] = mad_u64_u32_1(U[c][p].z, acc[c][4 * p + 2]);                \
+                    acc[c][4 * p + 3] = mad_u64_u32_1(U[c][p].w, acc[c][4 * p + 3]);                \
                 }                                                                                   \
-                const u32x4 h = *reinterpret_cast<const u32x4*>(r + 64);                            \
-                hs[c][0] += h.x, hs[c][1] += h.y, hs[c][2] += h.z, hs[c][3] += h.w;                 \
-                if (bcol) bsum[c] += bb[(((gg) & 1) * G + st) * bks + d];                           \
+                hs[c][0] += U[c][4].x, hs[c][1] += U[c][4].y, hs[c][2] += U[c][4].z, hs[c][3] += U[c][4].w; \
+                if (bcol) bsum[c] += bb[(((gg) & 1) * G + st) * bks + dd[c]];                       \
             }                                                                                       \
         }                                                                                           \
         _Pragma("unroll") for (int c = 0; c < CTS; ++c)                                             \
@@ -515,13 +534,43 @@ __global__ void __launch_bounds__(256) k_ks_combine(KSParams P, const uint64_t* 
 #define KS_BLOCK_TARGET 2048
 #endif
 constexpr uint32_t kMaxSplit = 32, kMaxSplitNarrow = 16, kSplitMaxB = 2048, kWideSplitMaxB = 512;
-uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B, const Knobs& kn, bool wide_keys) {
-    const uint32_t cap = std::min<uint32_t>((uint32_t)std::max(1, kn.ks_split),  // knob (TFHE_KS_SPLIT): 1 = no split
-                                            B <= kWideSplitMaxB ? (wide_keys ? kMaxSplit : kMaxSplitNarrow) : 4);
+// Round 6: the last wave's tail.  Every block of a launch sums the same number of steps, so a launch of `blocks`
+// blocks with `slots` resident at once takes ceil(blocks z / slots) / z block-lengths when the steps split z ways
+// (C3: 704 blocks at two per CU = 1.375 waves, i.e. two block-lengths with the second wave 37 % full).  Among
+// z, 2z, 4z, ... (within the knob's cap, kTailSplitMax, the stage pairs and the partial-sum buffer) the shortest
+// is taken; a candidate must beat the current one by 3 % (the partial sums and k_ks_combine cost a little).
+constexpr uint32_t kTailSplitMax = 8, kTailSplitMaxCts = 8 * 8192;  // partial-sum rows: z B <= kTailSplitMaxCts
+uint32_t ks_nsplit(const KSParams& P, size_t blocks, size_t B, const Knobs& kn, bool wide_keys, size_t slots) {
+    const uint32_t knob = (uint32_t)std::max(1, kn.ks_split);  // knob (TFHE_KS_SPLIT): 1 = no split
+    const uint32_t cap = std::min<uint32_t>(knob, B <= kWideSplitMaxB ? (wide_keys ? kMaxSplit : kMaxSplitNarrow) : 4);
     const uint32_t pairs = P.N * P.dKS / (2 * GMAX);
     uint32_t z = 1;
     while (2 * z <= cap && B <= kSplitMaxB && blocks * z < KS_BLOCK_TARGET && pairs % (2 * z) == 0) z *= 2;
-    return z;
+    if (slots == 0) return z;
+    auto cost = [&](uint32_t x) { return (double)((blocks * x + slots - 1) / slots) / x; };
+    uint32_t best = z;
+    for (uint32_t x = 2 * z; x <= std::min(knob, std::max(z, kTailSplitMax)) && pairs % (2 * x) == 0 &&
+                             (size_t)x * B <= kTailSplitMaxCts;
+         x *= 2)
+        if (cost(x) < 0.97 * cost(best)) best = x;
+    return best;
+}
+
+// resident blocks of kernel k at `lds` bytes of LDS per block, chip-wide (occupancy x CUs of the current device),
+// cached per (kernel, lds)
+size_t resident_blocks(const void* k, size_t lds) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<const void*, size_t>, size_t>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    for (auto& e : cache)
+        if (e.first.first == k && e.first.second == lds) return e.second;
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, KT, lds) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;  // unknown: the round-5 rule alone
+    const size_t r = (size_t)std::max(0, per_cu) * (size_t)std::max(0, cus);
+    cache.push_back({{k, lds}, r});
+    return r;
 }
 
 template <typename KW, typename ACC, int CT, int CTS, int G = 4, bool PK = false>
@@ -554,7 +603,10 @@ hipError_t launch_tiled(const KSParams& P, const void* kska, const void* kskb, c
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = (P.n_pad + CT - 1) / CT;
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
-    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, sizeof(KW) == 8);
+    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, sizeof(KW) == 8, resident_blocks((const void*)k, lds));
+    if (kn.trace)
+        std::fprintf(stderr, "[ks] B=%zu key bytes=%d blocks=%u resident=%zu nsplit=%u\n", B, (int)sizeof(KW), blocks,
+                     resident_blocks((const void*)k, lds), nsplit);
     hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const KW*)kska, (const KW*)kskb, dig, bq, B, Bp,
                        nct, ncol, fmod, out, nsplit, part);
     if (nsplit > 1) {
@@ -586,7 +638,10 @@ hipError_t launch_tiled40(const KSParams& P, const void* rec, const void* kskb, 
     const uint32_t nct = (uint32_t)((B + KT * CTS - 1) / (KT * CTS));
     const uint32_t ncol = ks40_tiles(P);
     const uint32_t blocks = nct * ((ncol + 7) / 8) * 8;
-    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, true);
+    const uint32_t nsplit = ks_nsplit(P, blocks, B, kn, true, resident_blocks((const void*)k, lds));
+    if (kn.trace)
+        std::fprintf(stderr, "[ks] B=%zu key bytes=%d blocks=%u resident=%zu nsplit=%u\n", B, 5, blocks,
+                     resident_blocks((const void*)k, lds), nsplit);
     hipLaunchKernelGGL(k, dim3(blocks * nsplit), dim3(KT), lds, s, P, (const unsigned char*)rec, (const uint64_t*)kskb,
                        dig, bq, B, Bp, nct, ncol, fmod, out, nsplit, part, hbits);
     if (nsplit > 1) {
@@ -604,7 +659,8 @@ size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; 
 }  // namespace
 
 size_t ks_tiled_part_words(const KSParams& P, size_t B) {  // split partial sums (ks_nsplit)
-    return std::max((size_t)kMaxSplit * std::min(B, (size_t)kWideSplitMaxB), (size_t)4 * std::min(B, (size_t)kSplitMaxB)) *
+    return std::max({(size_t)kMaxSplit * std::min(B, (size_t)kWideSplitMaxB), (size_t)4 * std::min(B, (size_t)kSplitMaxB),
+                     std::min((size_t)kTailSplitMax * B, (size_t)kTailSplitMaxCts)}) *
            (P.n + 1);
 }
 
