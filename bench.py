@@ -579,7 +579,8 @@ def main():
     rank_ms = tdist.gather_over_ranks(br_ms, dev) if world > 1 else [br_ms]
     info = ctx.info()
     balg, bsk_bytes = b_alg_per_bootstrap(p)
-    pmc_json = args.pmc_json or newest(os.path.join(ROOT, "profiles", f"r05_pmc_{name}.json"),
+    pmc_json = args.pmc_json or newest(os.path.join(ROOT, "profiles", f"r06_pmc_{name}.json"),
+                                       os.path.join(ROOT, "profiles", f"r05_pmc_{name}.json"),
                                        os.path.join(ROOT, "profiles", f"r04_pmc_{name}.json"),
                                        *([os.path.join(ROOT, "profiles", "r03_pmc_blind_rotate.json")]
                                          if name == "C2" else []))

@@ -295,16 +295,18 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled(KSParams P, const KW* __rest
 // (2^35 there), so every key word is below 2^(32+b).  k_pack_ks40 derives, once at setup, one 80-byte
 // record per (KSK row, 16-column tile): the 16 low words (u32, 64 B), then the 16 high parts (u8, 16 B) --
 // 80 B of LDS and L2 traffic per row segment against 128 B of u64 words.  The column sums only matter mod
-// qKS: the low words sum exactly in u64 (one v_mad_u64_u32 with a unit factor each, as the u64 form's add);
+// qKS: the low words sum exactly in u64 (one v_mad_u64_u32 with a unit factor each, as the u64 form's add;
+// K40_SDWA below: two u32 sums of 16-bit halves instead, measured slower);
 // the high parts sum as byte fields of u32 words, four columns per add, reduced mod 2^b after every stage
 // of four steps (a field stays below 5 * 2^b <= 160, no carry into its neighbour); a column's sum is
 // lo + (field mod 2^b) 2^32, congruent to the exact sum mod qKS.  Records are contiguous, so a row
 // segment is five 16-byte pieces and the staging of k_ks_tiled carries over unchanged.
 constexpr int K40_CT = 16, K40_REC = 80, K40_PIECES = K40_REC / 16;
-// steps of a stage unrolled in the sum loop (A/B builds: -DKS40_UNROLL=2 overlaps a step's LDS reads with the
-// previous step's sums at 204 instead of 196 VGPRs)
+// steps of a stage unrolled in the sum loop: 2 overlaps a step's LDS reads with the previous step's sums (same box,
+// ARB12 at 128 / 1024 / 4096 ciphertexts: 1.32 / 2.75 / 8.74 ms unrolled once, 1.31 / 2.68 / 8.56 twice; round 5's
+// u64 form 1.455 / 3.46 / 12.07; profiles/r06h)
 #ifndef KS40_UNROLL
-#define KS40_UNROLL 1
+#define KS40_UNROLL 2
 #endif
 #if KS40_UNROLL == 2
 #define K40_UNR _Pragma("unroll 2")
@@ -325,6 +327,12 @@ __global__ void k_pack_ks40(const uint64_t* __restrict__ ksk, size_t rows, uint3
     rec[64 + col] = (unsigned char)(w >> 32);
 }
 
+// K40_SDWA (A/B builds): 1 sums the low words as two u32 sums of their 16-bit halves (two SDWA adds per word),
+// 0 (default) as u64 sums (one v_mad_u64_u32 with a unit factor per word): the SDWA form measured 4-5 % slower
+// unrolled once and 1.7x slower unrolled twice (246 VGPRs; profiles/r06h)
+#ifndef K40_SDWA
+#define K40_SDWA 0
+#endif
 __device__ __forceinline__ uint64_t mad_u64_u32_1(uint32_t x, uint64_t acc) {  // acc + x in one VALU
     uint64_t r, junk;  // (the carry-out lane mask is never read)
     asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(junk) : "v"(x), "v"(acc));
@@ -372,14 +380,18 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled40(KSParams P, const unsigned
     u32x4 stgX[MAXL], stgY[MAXL];
     uint64_t bX[G], bY[G];
     uint32_t dX[CTS], dY[CTS];
-    uint64_t acc[CTS][K40_CT];
+    uint32_t a0[CTS][K40_SDWA ? K40_CT : 1], a1[CTS][K40_SDWA ? K40_CT : 1];  // sums of the low words' 16-bit halves
+    uint64_t al[CTS][K40_SDWA ? 1 : K40_CT];                                   // (each < 2^30: exact), or u64 sums
     uint32_t hs[CTS][K40_CT / 4];
     uint64_t bsum[CTS];
 #pragma unroll
     for (int c = 0; c < CTS; ++c) {
         bsum[c] = 0;
 #pragma unroll
-        for (int kk = 0; kk < K40_CT; ++kk) acc[c][kk] = 0;
+        for (int kk = 0; kk < K40_CT; ++kk) {
+            if constexpr (K40_SDWA) a0[c][kk] = a1[c][kk] = 0;
+            else al[c][kk] = 0;
+        }
 #pragma unroll
         for (int m = 0; m < K40_CT / 4; ++m) hs[c][m] = 0;
     }
@@ -428,12 +440,16 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled40(KSParams P, const unsigned
                     U[c][p] = *reinterpret_cast<const u32x4*>(r + p * 16);                          \
             }                                                                                       \
             _Pragma("unroll") for (int c = 0; c < CTS; ++c) {                                       \
-                _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                     \
-                    acc[c][4 * p + 0] = mad_u64_u32_1(U[c][p].x, acc[c][4 * p + 0]);                \
-                    acc[c][4 * p + 1] = mad_u64_u32_1(U[c][p].y, acc[c][4 * p + 1]);                \
-                    acc[c][4 * p + 2] = mad_u64_u32_1(U[c][p].z, acc[c][4 * p + 2]);                \
-                    acc[c][4 * p + 3] = mad_u64_u32_1(U[c][p].w, acc[c][4 * p + 3]);                \
-                }                                                                                   \
+                _Pragma("unroll") for (int p = 0; p < 4; ++p)                                       \
+                    _Pragma("unroll") for (int v = 0; v < 4; ++v) {                                 \
+                        const uint32_t w = v == 0 ? U[c][p].x : v == 1 ? U[c][p].y : v == 2 ? U[c][p].z : U[c][p].w; \
+                        if constexpr (K40_SDWA) {                                                   \
+                            a0[c][4 * p + v] += w & 0xffff;  /* two SDWA adds */                    \
+                            a1[c][4 * p + v] += w >> 16;                                            \
+                        } else {                                                                    \
+                            al[c][4 * p + v] = mad_u64_u32_1(w, al[c][4 * p + v]);                  \
+                        }                                                                           \
+                    }                                                                               \
                 hs[c][0] += U[c][4].x, hs[c][1] += U[c][4].y, hs[c][2] += U[c][4].z, hs[c][3] += U[c][4].w; \
                 if (bcol) bsum[c] += bb[(((gg) & 1) * G + st) * bks + dd[c]];                       \
             }                                                                                       \
@@ -466,7 +482,8 @@ __global__ void __launch_bounds__(KT, 2) k_ks_tiled40(KSParams P, const unsigned
 #undef K40_SUM
     // column kk's sum, congruent mod qKS = 2^(32 + hbits)
     auto colsum = [&](int c, int kk) -> uint64_t {
-        return acc[c][kk] + ((uint64_t)((hs[c][kk >> 2] >> (8 * (kk & 3))) & ((1u << hbits) - 1)) << 32);
+        const uint64_t lo = K40_SDWA ? (uint64_t)a0[c][kk] + ((uint64_t)a1[c][kk] << 16) : al[c][K40_SDWA ? 0 : kk];
+        return lo + ((uint64_t)((hs[c][kk >> 2] >> (8 * (kk & 3))) & ((1u << hbits) - 1)) << 32);
     };
     if (nsplit > 1) {
 #pragma unroll
