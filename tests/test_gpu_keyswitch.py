@@ -122,6 +122,7 @@ def test_u16_keys_without_packed_sums(ks_ctx):
     assert np.array_equal(packed, plain) and np.array_equal(plain, gather)
 
 
+@pytest.mark.parametrize("ks_ctx", ["ARB12"], indirect=True)
 @pytest.mark.parametrize("B", [2, 128, 1029])
 def test_split_word_keys_equal_u64_words(ks_ctx, B):
     """8-byte keys with qKS = 2^35 (ARB12 / the logQ contexts; TOY_N8192 takes the gather): the tiled key
@@ -130,9 +131,7 @@ def test_split_word_keys_equal_u64_words(ks_ctx, B):
     the step split (partial sums + k_ks_combine), at 1029 without it; the rows of maximal entries (qKS - 1)
     put every byte field at its bound."""
     name, op, ctx, orc = ks_ctx
-    if op.qKS != (1 << 35) or name == "TOY_N8192":
-        pytest.skip("split-word records: qKS = 2^35 with the tiled form")
-    assert ctx.knobs()["ks40"] == 1
+    assert op.qKS == (1 << 35) and ctx.knobs()["ks40"] == 1
     ext = _ext(op, B, 40 + B)
     split40 = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
     with ctx.knobs_set(ks40=0):
