@@ -3,6 +3,8 @@ are reproducible from the raw files committed beside them, and physically plausi
 are at most the part's 2.4 GHz, and the roofline fractions they imply are at most 1."""
 import json
 import os
+
+import pytest
 import subprocess
 import sys
 
@@ -107,10 +109,11 @@ def test_r04_bench_lines_reproduce_their_roofline():
         assert line["value"] > 100 * cb["value"], cfg
 
 
-# ---- round 5: the final per-configuration records (profiles/r05x, profiles/r05_pmc_*.json) ----
-def test_r05_pmc_records_are_consistent():
+# ---- rounds 5 and 6: the final per-configuration records (profiles/rNNx, profiles/rNN_pmc_*.json) ----
+@pytest.mark.parametrize("rnd", ["r05", "r06"])
+def test_final_pmc_records_are_consistent(rnd):
     for cfg, (units, *_rest) in R04_CONFIGS.items():
-        pmc = json.load(open(os.path.join(ROOT, "profiles", f"r05_pmc_{cfg}.json")))
+        pmc = json.load(open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_{cfg}.json")))
         assert pmc["units_per_launch"] == units, cfg
         t = pmc["gui_pass_kernel_ns_per_launch"] * 1e-9
         held = pmc["grbm_gui_active_per_launch"] / 8 / t / 1e9
@@ -120,17 +123,18 @@ def test_r05_pmc_records_are_consistent():
         assert pmc["hbm_bytes_per_launch"] / t < 8e12, cfg
 
 
-def test_r05_bench_lines_reproduce_their_roofline_and_checked_their_outputs():
+@pytest.mark.parametrize("rnd", ["r05", "r06"])
+def test_final_bench_lines_reproduce_their_roofline_and_checked_their_outputs(rnd):
     peaks = json.load(open(os.path.join(ROOT, "profiles", "r04_valu_peak.json")))["peaks"]
     for cfg, (units, n, N, dG2, fam) in R04_CONFIGS.items():
-        line = json.load(open(os.path.join(ROOT, "profiles", "r05x", f"bench_{cfg}.json")))
+        line = json.load(open(os.path.join(ROOT, "profiles", f"{rnd}x", f"bench_{cfg}.json")))
         r = line["roofline"]
         assert r["units_per_launch"] == units and r["peak_family"] == fam, cfg
         assert r["alg_modmul_per_unit"] == _alg_modmul(n, N, dG2), cfg
         achieved = r["alg_modmul_per_unit"] * units / (r["kernel_ms"] * 1e-3)
         assert abs(achieved / 1e12 - r["achieved"]) < 0.01, cfg
         assert abs(r["frac"] - achieved / peaks[fam]["modmul_per_s"]) < 0.002 and 0 < r["frac"] <= 1, cfg
-        assert r["traffic"] is not None, cfg  # read from the r05 PMC record of the same build
+        assert r["traffic"] is not None, cfg  # read from the PMC record of the same build
         assert line["parity_ok"] is True and line["parity_failed"] == [], cfg
         assert line["oracle_sample"]["ranks_passed"] == line["oracle_sample"]["ranks_checked"] == 1, cfg
         cb = line["cpu_baseline"]
@@ -139,7 +143,7 @@ def test_r05_bench_lines_reproduce_their_roofline_and_checked_their_outputs():
         assert line["value"] > 100 * cb["value"], cfg
         # the event-timed blind rotation agrees with rocprof's average for the same kernel (+-5 %)
         import csv
-        rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r05x", f"kernel_stats_{cfg}.csv"))))
+        rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", f"{rnd}x", f"kernel_stats_{cfg}.csv"))))
         br = [row for row in rows if "k_blind_rotate" in row["Name"]]
         top = max(br, key=lambda row: float(row["TotalDurationNs"]))
         assert abs(float(top["AverageNs"]) * 1e-6 / r["kernel_ms"] - 1) < 0.05, cfg
