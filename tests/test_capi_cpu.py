@@ -205,7 +205,10 @@ def test_environment_knobs_are_validated(env, why):
 
 
 @pytest.mark.parametrize("kernel,product,probes", [("k_blind_rotate_sf2duo", ["0"], ["0", "1"]),
-                                                    ("k_blind_rotate_f64wduo", ["0"], ["0", "1", "2", "3", "4"]),
+                                                    ("k_blind_rotate_f64wduo", ["0, false, false, 2", "0, true, true, 1"],
+                                                     ["0, false, false, 2", "0, true, true, 1", "1, false, false, 2",
+                                                      "1, true, true, 1", "2, true, true, 1", "3, true, true, 1",
+                                                      "4, true, true, 1"]),
                                                     ("k_blind_rotate_sf2p", ["2, 0"], ["2, 0", "2, 1"])])
 def test_product_library_has_no_duo_probe(capi, kernel, product, probes):
     """The duo probes (1: a partner that never arrives; f64wduo 2: no hand-off, 3: broadcast factor rows,
@@ -216,7 +219,7 @@ def test_product_library_has_no_duo_probe(capi, kernel, product, probes):
 
     def duo(path):
         out = subprocess.run(["nm", "-C", path], capture_output=True, text=True, check=True).stdout
-        return sorted(set(re.findall(kernel + r"<([\d, ]+)>", out)))
+        return sorted(set(re.findall(kernel + r"<([\w, ]+)>", out)))
 
     assert duo(capi.library_path()) == product
     assert duo(capi.capi.TEST_LIB) == probes

@@ -103,10 +103,12 @@ def test_tiled_keyswitch_ciphertexts_per_thread(ks_ctx, cts):
     batch) equal the gather form."""
     name, op, ctx, orc = ks_ctx
     ext = _ext(op, 1029, 13)
-    with ctx.knobs_set(ks_cts=int(cts)):
-        tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
     gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
-    assert np.array_equal(tiled, gather)
+    # 8-byte keys: both the split-word records (ks40 = 1, the default) and the u64 words at both depths
+    for k40 in ((1, 0) if op.qKS > (1 << 32) else (1,)):
+        with ctx.knobs_set(ks_cts=int(cts), ks40=k40):
+            tiled = _with_min(ctx, "1", lambda: ctx.MKMSwitch(ext, op.q))
+        assert np.array_equal(tiled, gather), k40
 
 
 def test_u16_keys_without_packed_sums(ks_ctx):

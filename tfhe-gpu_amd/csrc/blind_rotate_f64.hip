@@ -750,7 +750,10 @@ __device__ __forceinline__ uint32_t fsw(uint32_t e) { return F64D_FSW ? e ^ ((e 
 // (value + round tag in one 8-byte word, no flag or barriers) polling the four words one after another 8.03
 // against 7.71, the same with all four loads in flight per poll 7.56-7.71 against 7.51-7.66 (a tie), one flag
 // per wavefront with no workgroup barrier 8.8-9.2 against 7.5-7.6 (profiles/r05g, r05h, r05i).
-template <int PROBE = 0>
+// Round 6: templated on f64w's shape as well -- <RED, WRAP, LD> = <true, true, 1> for the STD128Q class (above)
+// and <false, false, 2> for the STD192 class (Q < 2^40, no reductions, two transformed digits whose outputs and
+// C' are exchanged between the column's waves through three LDS buffers; 132 KiB of LDS), as f64w's two instances.
+template <int PROBE = 0, bool RED = true, bool WRAP = true, int LD = 1>
 __global__ void __launch_bounds__(512, 2)
 k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, const uint64_t* __restrict__ a,
                        uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X, uint32_t pairs) {
@@ -763,9 +766,10 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     double* bf = lds_d + 2 * N;  // forward buffer [2][H]
     double* bi = bf + 2 * H;     // inverse buffer [2][H]
     double* cx = bi + 2 * H;     // this round's C' (+ the WRAP correction) [2][H], slot positions
+    double* dx = cx + 2 * H;     // LD = 2: digit 0's values for the other column's waves [2][H] (digit 1: bf)
     // F64D_MFULL: the whole 2N-entry factor table psi^e - 1 (32 KiB; one workgroup per CU leaves the LDS for
     // it), one lookup per factor; otherwise the two 64-entry tables, two lookups and a product per factor
-    double* mt = cx + 2 * H;     // monomial tables
+    double* mt = dx + (LD > 1 ? 2 * H : 0);  // monomial tables
     uint32_t* ex = reinterpret_cast<uint32_t*>(mt + (F64D_MFULL ? 2 * N : 128));  // rotation exponents [n]
     __shared__ int wflag[2];
     __shared__ uint32_t duo_ok;
@@ -812,30 +816,37 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
     double Cn[4];  // N^-1 NTT(acc_j) at the lane's slots
     {
         double d[4];
-        f64d_fwd<true>(bf, acc, d, h, psi, K);
+        f64d_fwd<RED>(bf, acc, d, h, psi, K);
 #pragma unroll
         for (int s = 0; s < 4; ++s) Cn[s] = fmodmul(d[s], K.Ninv, K);
     }
     __syncthreads();  // the prologue's wave-local passes vs round 0's pass A (f64w's round-2 race)
-    double sl[2], kl[2];  // digit 0 and the WRAP residual (f64w<..., LD = 1>)
+    // digit l of c: low logG bits (signed) of (c + Kd_l) >> (l logG); WRAP: residual (c + KdL) >> (L logG) (f64w's)
+    double sl[LD + 1], kl[LD + 1];
     {
-        const uint32_t shift = P.digits * logG;
-        int64_t Kx = Bh;
-        for (uint32_t z = 1; z < P.digits; ++z) Kx = (Kx << logG) + Bh;
-        sl[0] = 1.0, kl[0] = 0.0;
-        sl[1] = __builtin_ldexp(1.0, -(int)shift);
-        kl[1] = __dmul_rn((double)Kx, sl[1]);
+        int64_t Kd = 0;
+        for (uint32_t l = 0; l <= (uint32_t)LD; ++l) {
+            const uint32_t shift = (l == (uint32_t)LD ? P.digits : l) * logG;
+            int64_t Kx = Kd;
+            if (l == (uint32_t)LD)
+                for (uint32_t z = l; z < P.digits; ++z) Kx = (Kx << logG) + Bh;
+            sl[l] = __builtin_ldexp(1.0, -(int)shift);
+            kl[l] = __dmul_rn((double)Kx, sl[l]);
+            Kd = (Kd << logG) + Bh;
+        }
     }
     uint32_t* myflag = X.flags + (pair * 2 + h) * 32;
     const uint32_t* peerflag = X.flags + (pair * 2 + (1 - h)) * 32;
     for (uint32_t i = 0; i < P.n; ++i) {
         const uint32_t ai = ex[i];
         const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: launcher)
-        double D[4], dum[4];
-        // products of column j: group gi = (key kk, row rr): rr 0 own digit, 1 the other's, 2 own C', 3 the other's
-        auto krow = [j](uint32_t rr) -> uint32_t { return rr == 0 ? j : rr == 1 ? 1 - j : rr == 2 ? 2 + j : 3 - j; };
+        double D[LD][4], dum[4];
+        // products of column j: group gi = (key kk, row rr): rr = 2l (own digit l), 2l + 1 (the other column's
+        // digit l), 2LD (own C'), 2LD + 1 (the other's); key row 2l + polynomial, 2LD + polynomial
+        constexpr int RW = 2 * LD + 2, NG = 2 * RW;
+        auto krow = [j](uint32_t rr) -> uint32_t { return (rr & ~1u) + ((rr & 1) ? 1 - j : j); };
         auto kload = [&](int gi, double (&kv)[4]) {
-            const uint32_t kk = gi >> 2, r = krow(gi & 3);
+            const uint32_t kk = gi / RW, r = krow(gi % RW);
             const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
             const v2d lo = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8), (int)o, 0));
             const v2d hi = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rk, (int)(u4 * 8 + 16), (int)o, 0));
@@ -845,61 +856,69 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
         // latency overlaps the transform instead of opening the products (two waves per SIMD hide little)
         // (F64D_KPRE = d groups in flight: the first d requested here, group g + d at product group g, a ring
         // of d + 1; 0: the round-4 form, group 0 requested at the products)
-        constexpr int KD = F64D_KPRE > 0 ? F64D_KPRE : 1, KR = KD + 1 < 8 ? KD + 1 : 8;
+        constexpr int KD = F64D_KPRE > 0 ? F64D_KPRE : 1, KR = KD + 1 < NG ? KD + 1 : NG;
         double kv[KR][4];
 #pragma unroll
         for (int g = 0; g < (F64D_KPRE > 0 ? KD : 0); ++g) kload(g, kv[g]);
-        auto digit = [&](bool corr, double (&d)[4]) {
+        auto digit = [&](uint32_t l, bool corr, double (&d)[4]) {
             double v[8];
             bool wv = false;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const double c = acc[k];
-                const double res = __builtin_floor(__fma_rn(c, sl[1], kl[1]));
-                if (corr) {
+                const double res = WRAP ? __builtin_floor(__fma_rn(c, sl[LD], kl[LD])) : 0.0;
+                if (WRAP && corr) {
                     v[k] = __dmul_rn(res, -K.wfac);
                 } else {
-                    v[k] = __fma_rn(-Bg, __builtin_floor(__fma_rn(c, Bginv, 0.5)), c);
-                    wv |= res != 0.0;
+                    const double f = l == 0 ? c : __builtin_floor(__fma_rn(c, sl[l], kl[l]));
+                    v[k] = __fma_rn(-Bg, __builtin_floor(__fma_rn(f, Bginv, 0.5)), f);
+                    if (WRAP) wv |= res != 0.0;
                 }
             }
-            if (!corr) {
+            if (WRAP && !corr && l == 0) {
                 if (t == 0) wflag[(i + 1) & 1] = 0;
                 if (wv) wflag[i & 1] = 1;
             }
-            f64d_fwd<true>(bf, v, d, h, psi, K);
+            if (l > 0 && !corr) __syncthreads();  // other waves may still read their blocks of digit l - 1
+            f64d_fwd<RED>(bf, v, d, h, psi, K);
         };
-        digit(false, D);
+#pragma unroll
+        for (int l = 0; l < LD; ++l) digit(l, false, D[l]);
         double Cx[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) Cx[s] = Cn[s];
-        if (wflag[i & 1]) {  // (uniform: published by the forward's barrier; about 2^-14 of rounds)
+        if (WRAP && wflag[i & 1]) {  // (uniform: published by the forward's barrier; about 2^-14 of rounds)
             __syncthreads();  // other waves may still read their blocks
-            digit(true, dum);
+            digit(LD, true, dum);
 #pragma unroll
             for (int s = 0; s < 4; ++s) Cx[s] = fred(__dadd_rn(Cx[s], dum[s]), K);
         }
-        // this lane's digit and C' values for the other column's waves
+        // this lane's digit and C' values for the other column's waves (each wave writes only its own block of
+        // every buffer; bf: the last digit, dx: digit 0 when LD = 2)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            bf[sp + dswz(4 * l + s)] = D[s];
+            bf[sp + dswz(4 * l + s)] = D[LD - 1][s];
+            if constexpr (LD > 1) dx[sp + dswz(4 * l + s)] = D[0][s];
             cx[sp + dswz(4 * l + s)] = Cx[s];
         }
         if constexpr (PROBE != 4) __syncthreads();  // (PROBE 4, timing only: no exchange barrier, results invalid)
-        double Do[4], Co[4];  // the other polynomial's at the same slots
+        double Do[LD][4], Co[4];  // the other polynomial's at the same slots
         const uint32_t so = (1 - j) * H + 256 * (w & 3);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) Do[s] = bf[so + dswz(4 * l + s)], Co[s] = cx[so + dswz(4 * l + s)];
+        for (int s = 0; s < 4; ++s) {
+            Do[LD - 1][s] = bf[so + dswz(4 * l + s)], Co[s] = cx[so + dswz(4 * l + s)];
+            if constexpr (LD > 1) Do[0][s] = dx[so + dswz(4 * l + s)];
+        }
         double A[2][4];
         if constexpr (F64D_KPRE == 0) kload(0, kv[0]);
 #pragma unroll
-        for (int gi = 0; gi < 8; ++gi) {
-            if (gi + KD < 8) kload(gi + KD, kv[(gi + KD) % KR]);
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gi + KD < NG) kload(gi + KD, kv[(gi + KD) % KR]);
             __builtin_amdgcn_sched_barrier(0);
-            const int kk = gi >> 2, rr = gi & 3;
+            const int kk = gi / RW, rr = gi % RW;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const double dv = rr == 0 ? D[s] : rr == 1 ? Do[s] : rr == 2 ? Cx[s] : Co[s];
+                const double dv = rr < 2 * LD ? ((rr & 1) ? Do[rr >> 1][s] : D[rr >> 1][s]) : (rr & 1) ? Co[s] : Cx[s];
                 const double pr = fmodmul(dv, kv[gi % KR][s], K);
                 A[kk][s] = rr == 0 ? pr : __dadd_rn(A[kk][s], pr);
             }
@@ -919,7 +938,7 @@ k_blind_rotate_f64wduo(BRParams P, F64Const K, const double* __restrict__ tabs, 
             Cn[s] = fred(__dadd_rn(Cn[s], S[s]), K);
         }
         double o[4];
-        f64d_inv<true>(bi, S, o, h, ipsi, K);
+        f64d_inv<RED>(bi, S, o, h, ipsi, K);
         // hand-off: this half's stage-1 values of both columns to the partner (thread t's 4 at k' 512 + t)
         double* mine = reinterpret_cast<double*>(X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N);
         const double* theirs = reinterpret_cast<const double*>(X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N);
@@ -1116,7 +1135,9 @@ hipError_t launch_pack_bsk_f64(const BRParams& P, const DevTables& T, const void
 }
 
 bool f64_duo_form(const BRParams& P, bool fold) {
-    return f64_path_supported(P, 64) && fold && P.Q >= (1ull << 40) && !fold_exact(P) && P.digits == 2;
+    if (!f64_path_supported(P, 64) || !fold) return false;
+    return (P.Q >= (1ull << 40) && !fold_exact(P) && P.digits == 2) ||  // STD128Q class: <RED, WRAP, 1>
+           (P.Q < (1ull << 40) && fold_exact(P) && P.digits == 3);      // STD192 class (round 6): <-, -, 2>
 }
 
 hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const void* keys, bool fold,
@@ -1157,20 +1178,25 @@ hipError_t launch_blind_rotate_f64(const BRParams& P, const DevTables& T, const 
             return hipGetLastError();
         }
 #endif
-        if (red && wrap && ld == 1 && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs && B <= kDuoMaxPairs) {
+        const bool duo_shape = (red && wrap && ld == 1) || (!red && !wrap && ld == 2);
+        if (duo_shape && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs && B <= kDuoMaxPairs) {
             // two workgroups per ciphertext (f64wduo), then the rescue of timed-out pairs
             const DuoBuf X = duo_layout(*duo);
-            const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + (F64D_MFULL ? 2 * P.N : 128)) * sizeof(double) +
-                                rot_exponent_bytes(P.n);
-            auto dk = k_blind_rotate_f64wduo<0>;
+            const size_t ldsd = ((size_t)2 * P.N + 3 * P.N + (ld > 1 ? P.N : 0) + (F64D_MFULL ? 2 * P.N : 128)) *
+                                    sizeof(double) + rot_exponent_bytes(P.n);
+            auto dk = red ? k_blind_rotate_f64wduo<0, true, true, 1> : k_blind_rotate_f64wduo<0, false, false, 2>;
+            auto rk = red ? k_blind_rotate_f64w<true, true, 1, 0, true> : k_blind_rotate_f64w<false, false, 2, 0, true>;
 #ifdef TFHE_TEST_PROBES
-            if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
-            if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
-            if (kn.probe == 9) dk = k_blind_rotate_f64wduo<3>;  // timing only: broadcast factor-table reads
-            if (kn.probe == 11) dk = k_blind_rotate_f64wduo<4>;  // timing only: no D / C' exchange barrier
+            if (red) {  // (the STD128Q instance's probes)
+                if (kn.probe == 5) dk = k_blind_rotate_f64wduo<1>;  // test library only: a partner that never arrives
+                if (kn.probe == 7) dk = k_blind_rotate_f64wduo<2>;  // timing only: no hand-off (results invalid)
+                if (kn.probe == 9) dk = k_blind_rotate_f64wduo<3>;  // timing only: broadcast factor-table reads
+                if (kn.probe == 11) dk = k_blind_rotate_f64wduo<4>;  // timing only: no D / C' exchange barrier
+            } else if (kn.probe == 5) {
+                dk = k_blind_rotate_f64wduo<1, false, false, 2>;  // test library only: a partner that never arrives
+            }
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
-            auto rk = k_blind_rotate_f64w<true, true, 1, 0, true>;
             (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             return duo_serialised(*duo, s, [&]() -> hipError_t {
                 if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;
