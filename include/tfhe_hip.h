@@ -61,7 +61,7 @@ extern "C" {
                                    7: tfhe_knobs.split4 (two-group STD128 form); the duo forms cover
                                       STD128Q (f64wduo) and timed-out pairs are recomputed;
                                    8: tfhe_knobs.ks40 (split-word key-switch records for 8-byte keys);
-                                      tfhe_rccl_selftest */
+                                      tfhe_rccl_selftest; the duo form covers the STD192 classes */
 
 typedef enum tfhe_status {
     TFHE_OK = 0,
@@ -112,7 +112,7 @@ typedef struct tfhe_info {
     int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
     double replicate_ms;       /* wall time of that replication (0 for one device) */
     uint32_t duo_timeouts;     /* workgroups of the two-workgroup forms (sf2duo: two-digit special-form
-                                  contexts; f64wduo: STD128Q class) that timed out waiting for their partner
+                                  contexts; f64wduo: STD128Q and STD192 classes) that timed out waiting for their partner
                                   (10 ms of wall clock in one round) since setup, summed over devices
                                   (synchronises them); the ciphertexts of such a pair are recomputed from
                                   their saved inputs by the one-workgroup kernel (sf2 / f64w) queued behind
@@ -282,7 +282,7 @@ typedef struct tfhe_knobs {
     int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
     int32_t trace;        /* host-array runner timeline on stderr */
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
-    int32_t duo;          /* two-digit special-form contexts (sf2duo) and STD128Q-class FP64 contexts (f64wduo):
+    int32_t duo;          /* two-digit special-form contexts (sf2duo) and STD128Q- / STD192-class FP64 contexts (f64wduo):
                              batches up to this size (default 128, at most 256) run each ciphertext on two
                              workgroups, and only while the device holds every pair co-resident (a duo workgroup
                              takes one CU: at most half the CU count, 128 on MI355X); 0: never */
