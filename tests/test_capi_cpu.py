@@ -204,16 +204,18 @@ def test_environment_knobs_are_validated(env, why):
     assert "ERR" in r.stdout and "launch knob from the environment" in r.stdout and why in r.stdout, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("kernel,product,probes", [("k_blind_rotate_sf2duo", ["0"], ["0", "1"]),
+@pytest.mark.parametrize("kernel,product,probes", [("k_blind_rotate_sf2duo", [], ["0"]),
                                                     ("k_blind_rotate_f64wduo", ["0, false, false, 2", "0, true, true, 1"],
                                                      ["0, false, false, 2", "0, true, true, 1", "1, false, false, 2",
                                                       "1, true, true, 1", "2, true, true, 1", "3, true, true, 1",
                                                       "4, true, true, 1"]),
-                                                    ("k_blind_rotate_sf2p", ["2, 0"], ["2, 0", "2, 1"])])
+                                                    ("k_blind_rotate_sf2p", ["2, 0"], ["2, 0", "2, 1"]),
+                                                    ("k_blind_rotate_sfduo", ["1, 0", "2, 0"],
+                                                     ["1, 0", "1, 1", "1, 2", "2, 0", "2, 1", "2, 2"])])
 def test_product_library_has_no_duo_probe(capi, kernel, product, probes):
     """The duo probes (1: a partner that never arrives; f64wduo 2: no hand-off, 3: broadcast factor rows,
-    4: no D / C' exchange barrier; sf2p<2, 1>: broadcast factor rows -- all timing only) are test-library
-    instances only."""
+    4: no D / C' exchange barrier; sf2p<2, 1>: broadcast factor rows; sfduo 2: no hand-off -- all timing only;
+    sf2duo: the polynomial-split A/B form of the two-digit duo) are test-library instances only."""
     import re
     import subprocess
 

@@ -1,4 +1,6 @@
-"""GPU: the two-workgroup special-form blind rotation (k_blind_rotate_sf2duo, blind_rotate_generic.hip).
+"""GPU: the two-workgroup two-digit special-form blind rotation (k_blind_rotate_sfduo<2>, blind_rotate_generic.hip;
+round 6: split by NTT half -- the round-4/5 form split by accumulator polynomial, k_blind_rotate_sf2duo, is the test
+library's A/B form and is checked against it below).
 
 Two-digit special-form contexts (C5b: STD128 logQ = 23, throw = 1) run batches of at most
 `tfhe_knobs.duo` (default 128, at most 256) ciphertexts with each ciphertext's round split over two workgroups
@@ -139,6 +141,32 @@ def test_duo_partner_timeout_is_recomputed(oracle):
         assert ctx.info().duo_timeouts == 2
         assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)  # the failed word is cleared per launch
         assert ctx.info().duo_timeouts == 2
+    finally:
+        ctx.GPUClean()
+        orc.close()
+
+
+def test_polynomial_split_form_equals_default(oracle):
+    """The test library's probe 13 runs the round-4/5 two-digit duo (k_blind_rotate_sf2duo, split by accumulator
+    polynomial; 1.5-2.4 % slower than sfduo<2> at 128, profiles/r06m): the same outputs as the default form, the
+    one-workgroup form and the oracle."""
+    import tfhe_amd
+
+    op, cp = _ctx_params(oracle), _ctx_params(tfhe_amd)
+    bsk, ksk = oracle.kat_keys(op, oracle.Rng(79))
+    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
+    orc = oracle.Oracle(op, bsk, ksk)
+    del bsk, ksk
+    try:
+        a, acc = _inputs(op, 128, 450)
+        dflt = ctx.EvalAcc(a, 2 * op.N, acc)
+        with ctx.knobs_set(probe=13):
+            poly = ctx.EvalAcc(a, 2 * op.N, acc)
+        with ctx.knobs_set(duo=0):
+            one = ctx.EvalAcc(a, 2 * op.N, acc)
+        assert np.array_equal(dflt, poly) and np.array_equal(dflt, one)
+        assert np.array_equal(dflt[[5]].reshape(1, -1), orc.eval_acc(a[[5]], 2 * op.N, acc[[5]]).reshape(1, -1))
+        assert ctx.info().duo_timeouts == 0
     finally:
         ctx.GPUClean()
         orc.close()

@@ -544,16 +544,7 @@ k_blind_rotate_f64w(BRParams P, F64Const K, const double* __restrict__ tabs, con
 // stage 5, inverse after stages 9 (sums), 6 and 3), so every value obeys f64w's bounds
 // (tools/bounds_f64.py).  A member that times out sets the pair's failed word and the rescue launch
 // (k_blind_rotate_f64w<..., RESCUE>) recomputes that ciphertext from its saved input.
-// Buffer index of element x of a half polynomial (block x >> 8, y = x & 255): y's low five bits are
-// XORed with f(y[7:5]) so that every pass's 64-bit accesses are conflict-free per 32 lanes
-// (tools/lds_layouts_duo.py checks every pass).
-__device__ __forceinline__ uint32_t dswz(uint32_t x) {
-    // bit 5 -> bits 1, 3; bit 6 -> bit 4; bit 4 -> bits 0, 2: every b64 read conflict-free per 32-lane group
-    // (64 banks) AND every b64 write per 16-lane group (32 banks; MI355X_MICROARCH.md "LDS"), for every
-    // pass, the D / C' exchange and the units (tools/lds_layouts_duo.py; the round-5 first form, bits 5-7
-    // into bits 0-4 only, left the writes of passes (7,8), (10,9), (8,7) and the exchange 2-way)
-    return x ^ (((x >> 5) & 1) * 10u) ^ (((x >> 6) & 1) << 4) ^ (((x >> 4) & 1) * 5u);
-}
+// Buffer index of element x of a half polynomial: dswz (device_math.hpp, shared with sfduo).
 
 // forward: v = coefficients tau + 256k of polynomial t >> 8 (all N) -> d = the NTT values of half h at this
 // lane's slots 4u .. 4u+3, u = 64 (w & 3) + l of half h, polynomial w >> 2 (also left in the buffer)

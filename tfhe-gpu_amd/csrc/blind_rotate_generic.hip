@@ -1681,6 +1681,374 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
     }
 }
 
+// ---------------------------------------------------------------------------
+// sfduo: the special-form round on TWO workgroups per ciphertext, split by NTT half -- f64wduo's design
+// (blind_rotate_f64.hip) in sf arithmetic.  sf2duo splits by accumulator polynomial, which needs two digits
+// per polynomial to keep its 512 threads busy; the one-digit contexts (C3's arbFunc logQ 12 class: sf2<1>)
+// ran one workgroup per ciphertext at every batch (verdict r5 "missing" 2).  The negacyclic transform's
+// stage 0 pairs x and x + N/2; after it the two halves of the slots are independent rings until the
+// inverse's stage 0.  Member h of a pair (blocks b and b + 8, as sf2duo) holds the whole accumulator (both
+// polynomials, pass-A layout: thread t has coefficients tau + 256k of polynomial t >> 8) and per round:
+//   * extracts every coefficient's digits (sf2's closed form, inputs r + 28Q: the offset-free forward);
+//   * forward of each digit polynomial: stage 0 for its half's outputs only, stages 1-2 on the thread's 4
+//     values (one barrier), stages 3-10 wave-local (wave w: 256-block w & 3 of half h of polynomial w >> 2,
+//     radix-4 passes (3,4) (5,6) (7,8) (9,10)), so the lane ends with 4 slots of one polynomial;
+//   * products for column w >> 2 of its half's slots: its own polynomial's digits from registers, the other
+//     polynomial's through LDS (one barrier), 2 keys x 2 DIG rows; one table product per monomial factor
+//     (the whole 2N-row factor table in LDS, sf2p's layout);
+//   * inverse stages 10-3 wave-local, stages 2-1 across waves (one barrier), with sf2's folds (the sums of
+//     stages 9, 6 and 3), then hands its 4 stage-1 values per thread (16 KiB) to the partner and takes the
+//     partner's (the sf2duo hand-off, bounded wait), and both finish stage 0 and the accumulator update for
+//     all coefficients.
+// Every element goes through sf2's butterflies in sf2's order with the same folds, so sf2's bounds hold
+// unchanged (tools/bounds_sf.py); the buffers use f64wduo's swizzle (dswz, 8-byte words as there).  Per lane
+// and round: 24 forward products per digit against sf2's 44, 8 x DIG key products against 16 x DIG, 8 factor
+// products against 16, 24 inverse against 44.  A member that times out sets the pair's failed word and the
+// rescue launch (k_blind_rotate_sf2<DIG, true>) recomputes the ciphertext from its saved input.
+// LDS: forward twiddles (W0, W1) 32 KiB, forward / inverse buffers 2 x 16 KiB, two digits a third buffer,
+// factor table 64 KiB, exponents: 132 / 148 KiB, one workgroup per CU.
+template <class TW>
+__device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], uint64_t (&d)[4], uint32_t h,
+                                        const TW& T, const SfC& K) {
+    constexpr uint32_t H = G3_N / 2;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    {
+        const uint32_t tau = g3_tau();
+        uint64_t* p = bf + (t >> 8) * H + dswz(tau);
+        const uint64_t w0 = tw0(T, 1), w1 = tw1(T, 1);
+        uint64_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // stage 0, this half's outputs (x - v >= 0: inputs carry 28Q)
+            const uint64_t x = sf_mul(v[k + 4], w0, w1, K.c2);
+            o[k] = h ? v[k] - x : v[k] + x;
+        }
+        sf_ct(o[0], o[2], T, 2 + h, K), sf_ct(o[1], o[3], T, 2 + h, K);
+        sf_ct(o[0], o[1], T, 4 + 2 * h, K), sf_ct(o[2], o[3], T, 5 + 2 * h, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[256 * k] = o[k];
+    }
+    __syncthreads();
+    const uint32_t B = 4 * h + (w & 3);  // 256-block of the whole polynomial
+    uint64_t* q = bf + (w >> 2) * H + 256 * (w & 3);
+    uint64_t x[4];
+    {  // stages 3, 4
+        uint32_t y = l;
+        asm volatile("" : "+v"(y));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
+        sf_ct(x[0], x[2], T, 8 + B, K), sf_ct(x[1], x[3], T, 8 + B, K);
+        sf_ct(x[0], x[1], T, 16 + 2 * B, K), sf_ct(x[2], x[3], T, 17 + 2 * B, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 5, 6
+        const uint32_t c = l >> 4, y = 64 * c + (l & 15);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
+        sf_ct(x[0], x[2], T, 32 + 4 * B + c, K), sf_ct(x[1], x[3], T, 32 + 4 * B + c, K);
+        sf_ct(x[0], x[1], T, 64 + 8 * B + 2 * c, K), sf_ct(x[2], x[3], T, 65 + 8 * B + 2 * c, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 7, 8
+        const uint32_t c = l >> 2, y = 16 * c + (l & 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
+        sf_ct(x[0], x[2], T, 128 + 16 * B + c, K), sf_ct(x[1], x[3], T, 128 + 16 * B + c, K);
+        sf_ct(x[0], x[1], T, 256 + 32 * B + 2 * c, K), sf_ct(x[2], x[3], T, 257 + 32 * B + 2 * c, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 9, 10: slots 4u .. 4u+3, u = 64 B + l (sf2's units)
+        const uint32_t y = 4 * l;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + k)];
+        sf_ct(x[0], x[2], T, 512 + 64 * B + l, K), sf_ct(x[1], x[3], T, 512 + 64 * B + l, K);
+        sf_ct(x[0], x[1], T, 1024 + 128 * B + 2 * l, K), sf_ct(x[2], x[3], T, 1025 + 128 * B + 2 * l, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = x[k];
+    }
+}
+
+// inverse: s = column w >> 2's NTT-domain increment at the lane's slots -> after stages 10..1 o = elements
+// tau + 256k' (k' < 4) of half h of column t >> 8 (stage-1 outputs; stage 0 follows the hand-off)
+template <class TW>
+__device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], uint64_t (&o)[4], uint32_t h,
+                                        const TW& T, const SfC& K) {
+    constexpr uint32_t H = G3_N / 2;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    const uint32_t B = 4 * h + (w & 3);
+    uint64_t* q = bi + (w >> 2) * H + 256 * (w & 3);
+    uint64_t x[4] = {s[0], s[1], s[2], s[3]};
+    {  // stages 10, 9 (stage 9's sums folded, as sf2's units)
+        const uint32_t y = 4 * l;
+        sf_gs(x[0], x[1], T, 1024 + 128 * B + 2 * l, K), sf_gs(x[2], x[3], T, 1025 + 128 * B + 2 * l, K);
+        sf_gs<true>(x[0], x[2], T, 512 + 64 * B + l, K), sf_gs<true>(x[1], x[3], T, 512 + 64 * B + l, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 8, 7
+        const uint32_t c = l >> 2, y = 16 * c + (l & 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
+        sf_gs(x[0], x[1], T, 256 + 32 * B + 2 * c, K), sf_gs(x[2], x[3], T, 257 + 32 * B + 2 * c, K);
+        sf_gs(x[0], x[2], T, 128 + 16 * B + c, K), sf_gs(x[1], x[3], T, 128 + 16 * B + c, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 6, 5 (stage 6's sums folded, as the end of sf2's pass C)
+        const uint32_t c = l >> 4, y = 64 * c + (l & 15);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
+        sf_gs<true>(x[0], x[1], T, 64 + 8 * B + 2 * c, K), sf_gs<true>(x[2], x[3], T, 65 + 8 * B + 2 * c, K);
+        sf_gs(x[0], x[2], T, 32 + 4 * B + c, K), sf_gs(x[1], x[3], T, 32 + 4 * B + c, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
+    }
+    wl_sync();
+    {  // stages 4, 3 (stage 3's sums folded, as the end of sf2's pass B)
+        uint32_t y = l;
+        asm volatile("" : "+v"(y));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
+        sf_gs(x[0], x[1], T, 16 + 2 * B, K), sf_gs(x[2], x[3], T, 17 + 2 * B, K);
+        sf_gs<true>(x[0], x[2], T, 8 + B, K), sf_gs<true>(x[1], x[3], T, 8 + B, K);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = x[k];
+    }
+    __syncthreads();
+    {  // stages 2, 1 of half h (no fold, as sf2's pass A)
+        const uint32_t tau = g3_tau();
+        const uint64_t* p = bi + (t >> 8) * H + dswz(tau);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = p[256 * k];
+        sf_gs(o[0], o[1], T, 4 + 2 * h, K), sf_gs(o[2], o[3], T, 5 + 2 * h, K);
+        sf_gs(o[0], o[2], T, 2 + h, K), sf_gs(o[1], o[3], T, 2 + h, K);
+    }
+}
+
+#ifndef SFD_KPRE
+#define SFD_KPRE 2
+#endif
+// PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a partner
+// that never arrives would, and the wait is a 64th of the 10 ms bound.  PROBE 2 (timing only, results invalid):
+// no hand-off -- each member takes its own stage-1 values for its partner's.
+// The hand-off's hardware assumptions are f64wduo's (blind_rotate_f64.hip): relaxed agent-scope stores drained
+// by vmcnt(0) and the barrier before the flag; pairing b, b + 8 for latency only; both members co-resident
+// (the launcher's cap), a partner missing after 10 ms of wall clock fails the pair.
+template <int DIG, int PROBE = 0>
+__global__ void __launch_bounds__(G3_TH, 2)
+k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const uint64_t* __restrict__ psi1,
+                     const uint64_t* __restrict__ ipsi, const uint64_t* __restrict__ ipsi1,
+                     const uint64_t* __restrict__ mono, const uint64_t* __restrict__ mono1,
+                     const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ bsk1,
+                     const uint64_t* __restrict__ a, uint64_t amod, uint64_t* __restrict__ acc_io, DuoBuf X,
+                     uint32_t pairs) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    constexpr uint32_t N = G3_N, H = N / 2, TH = G3_TH;
+    const uint32_t b = blockIdx.x, pair = (b >> 4) * 8 + (b & 7), h = (b >> 3) & 1;
+    if (pair >= pairs) return;  // both members of a pair take this branch together
+    __shared__ uint32_t duo_ok;
+    uint64_t* tf0 = reinterpret_cast<uint64_t*>(smem);  // forward twiddles W0 [N], W1 [N]
+    uint64_t* tf1 = tf0 + N;
+    uint64_t* bf = tf1 + N;                  // forward buffer [2][H]
+    uint64_t* bi = bf + N;                   // inverse buffer [2][H]
+    uint64_t* dx = bi + N;                   // DIG = 2: digit 0's values for the other column's waves [2][H]
+    uint64_t* mt = dx + (DIG > 1 ? N : 0);   // factor table: row e = (psi^e - 1, its W1) [2N][2]
+    uint32_t* ex = reinterpret_cast<uint32_t*>(mt + 4 * N);  // rotation exponents [n]
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6, twoN = 2 * N, logG = P.logG;
+    const uint32_t j = __builtin_amdgcn_readfirstlane(w >> 2);  // this wave's polynomial / column
+    const uint32_t u4 = 4 * (256 * h + 64 * (w & 3) + l);       // this lane's slots u4 .. u4+3 (whole ring)
+    const uint32_t sp = j * H + 256 * (w & 3);                  // their buffer block
+    const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
+    const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
+    const uint32_t sh = 64 - logG;
+    for (uint32_t k = t; k < N; k += TH) tf0[k] = psi[k], tf1[k] = psi1[k];
+    for (uint32_t k = t; k < twoN; k += TH) {
+        mt[2 * sf_mrow(k)] = mono[k] % Q;  // psi^k - 1
+        mt[2 * sf_mrow(k) + 1] = mono1[k];
+    }
+    const SfTw TF{tf0, tf1};
+    const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
+                   __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
+    uint64_t* g = acc_io + (size_t)pair * twoN;
+    const uint64_t* ap = a + (size_t)pair * P.n;
+    stage_rot_exponents<TH>(ex, ap, P.n, amod, twoN);
+    const size_t round_words = (size_t)4 * P.dG2 * N;
+    const uint32_t tau = t & 255, pp = t >> 8;  // pass-A role: coefficients tau + 256k of polynomial pp
+
+    uint64_t acc[8];  // canonical [0, Q), all N coefficients of polynomial pp (both members)
+    uint64_t* sv = X.save + (size_t)pair * twoN;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint64_t v = g[pp * N + tau + 256 * k];
+        if (pp == h) sv[pp * N + tau + 256 * k] = v;  // the rescue's input if the pair times out
+        acc[k] = v >= Q ? v % Q : v;
+    }
+    __syncthreads();  // twiddles, factor table, exponents in LDS
+
+    const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
+    int64_t Kdl[DIG];  // sf2's closed-form digit offsets
+#pragma unroll
+    for (int d = 0; d < DIG; ++d) {
+        int64_t Kd = 0;
+        for (uint32_t z = 0; z < d + P.thr; ++z) Kd = (Kd << logG) + Bh;
+        Kdl[d] = Kd;
+    }
+    uint32_t* myflag = X.flags + (pair * 2 + h) * 32;
+    const uint32_t* peerflag = X.flags + (pair * 2 + (1 - h)) * 32;
+    for (uint32_t i = 0; i < P.n; ++i) {
+        const uint32_t ai = ex[i];
+        const uint32_t round_off = i * (uint32_t)round_words * 8;  // bytes (< 2^32: checked at launch)
+        // products of column j: group gi = (key kk, row rr): rr = 2d (own polynomial's digit d), 2d + 1 (the
+        // other polynomial's); key row 2d + polynomial
+        constexpr int RW = 2 * DIG, NG = 2 * RW;
+        auto krow = [j](uint32_t rr) -> uint32_t { return (rr & ~1u) + ((rr & 1) ? 1 - j : j); };
+        auto kload = [&](int gi, uint64_t (&kw)[8]) {
+            const uint32_t kk = gi / RW, r = krow(gi % RW);
+            const uint32_t o = round_off + ((kk * P.dG2 + r) * 2 + j) * N * 8;
+            const v4u a0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8), (int)o, 0));
+            const v4u a1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk0, (int)(u4 * 8 + 16), (int)o, 0));
+            const v4u b0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8), (int)o, 0));
+            const v4u b1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rk1, (int)(u4 * 8 + 16), (int)o, 0));
+            kw[0] = a0.x | ((uint64_t)a0.y << 32), kw[1] = a0.z | ((uint64_t)a0.w << 32);
+            kw[2] = a1.x | ((uint64_t)a1.y << 32), kw[3] = a1.z | ((uint64_t)a1.w << 32);
+            kw[4] = b0.x | ((uint64_t)b0.y << 32), kw[5] = b0.z | ((uint64_t)b0.w << 32);
+            kw[6] = b1.x | ((uint64_t)b1.y << 32), kw[7] = b1.z | ((uint64_t)b1.w << 32);
+        };
+        // SFD_KPRE key groups requested before the forward transform (a ring of SFD_KPRE + 1), as sf2duo
+        constexpr int KD = SFD_KPRE > 0 ? SFD_KPRE : 1, KR = KD + 1 < NG ? KD + 1 : NG;
+        uint64_t kw[KR][8];
+#pragma unroll
+        for (int gq = 0; gq < (SFD_KPRE > 0 ? KD : 0); ++gq) kload(gq, kw[gq]);
+        uint64_t D[DIG][4];
+#pragma unroll
+        for (int d = 0; d < DIG; ++d) {
+            const uint32_t shift = (d + P.thr) * logG;
+            const int64_t Klo = Kdl[d], Khi = Kdl[d] - Qs;
+            uint64_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t xv = acc[k];
+                const int64_t dd = ((int64_t)xv + (xv < Qhalf ? Klo : Khi)) >> shift;
+                const int64_t r = (int64_t)((uint64_t)dd << sh) >> sh;
+                v[k] = (uint64_t)r + K.Qf;  // r mod Q + 28Q (the offset-free forward's inputs)
+            }
+            if (d > 0) __syncthreads();  // other waves may still read their blocks of digit d - 1
+            sfd_fwd(bf, v, D[d], h, TF, K);
+        }
+        // this lane's digits for the other column's waves (each wave writes only its own block: bf the last
+        // digit, dx digit 0 when DIG = 2)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            bf[sp + dswz(4 * l + s)] = D[DIG - 1][s];
+            if constexpr (DIG > 1) dx[sp + dswz(4 * l + s)] = D[0][s];
+        }
+        __syncthreads();
+        uint64_t Do[DIG][4];  // the other polynomial's digits at the same slots
+        const uint32_t so = (1 - j) * H + 256 * (w & 3);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            Do[DIG - 1][s] = bf[so + dswz(4 * l + s)];
+            if constexpr (DIG > 1) Do[0][s] = dx[so + dswz(4 * l + s)];
+        }
+        uint64_t A[2][4];
+        if constexpr (SFD_KPRE == 0) kload(0, kw[0]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+            if (gi + KD < NG) kload(gi + KD, kw[(gi + KD) % KR]);
+            __builtin_amdgcn_sched_barrier(0);
+            const int kk = gi / RW, rr = gi % RW;
+            const uint64_t(&c)[8] = kw[gi % KR];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint64_t dv = (rr & 1) ? Do[rr >> 1][s] : D[rr >> 1][s];
+                const uint64_t prod = sf_mul(dv, c[s], c[4 + s], K.c2);
+                A[kk][s] = rr == 0 ? prod : A[kk][s] + prod;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t uo = u4;
+        asm volatile("" : "+v"(uo));
+        uint64_t S[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {  // one table product per factor (row e holds psi^e - 1), as sf2p
+            const uint32_t ip = ((2 * (__builtin_bitreverse32(uo + s) >> 21) + 1) * ai) & (twoN - 1);
+            const uint64_t* fp = mt + 2 * sf_mrow(ip);
+            const uint64_t* fm = mt + 2 * sf_mrow((twoN - ip) & (twoN - 1));
+            S[s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
+        }
+        uint64_t o[4];
+        sfd_inv(bi, S, o, h, TI, K);
+        // hand-off: this half's stage-1 values of both columns to the partner (thread t's 4 at k' 512 + t)
+        uint64_t* mine = X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N;
+        const uint64_t* theirs = X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N;
+        if constexpr (PROBE != 2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) duo_store(mine + 512 * k + t, o[k]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's stores drained; every read of the buffers done
+        if (PROBE != 2 && t == 0) {
+            const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
+            if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool ok = !gone;
+            uint64_t t_end = 0;
+            uint32_t k = 0;
+            while (ok && __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1) {
+                if ((++k & 7) == 0) {  // the clock every 8th poll, the deadline set at the first read
+                    const uint64_t now = wall_clock64();
+                    if (t_end == 0) t_end = now + (PROBE ? X.wait_ticks >> 6 : X.wait_ticks);
+                    else if (now > t_end) ok = false;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            duo_ok = ok;
+            if (!ok) {
+                __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if constexpr (PROBE != 2) {
+            __syncthreads();
+            if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
+        }
+        const uint64_t iw0 = tw0(TI, 1), iw1 = tw1(TI, 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // stage 0 for all coefficients (sf2's pass A end), then sf2's update
+            const uint64_t pv = PROBE == 2 ? o[k] : duo_load(theirs + 512 * k + t);
+            const uint64_t lo = h ? pv : o[k], hi = h ? o[k] : pv;
+            const uint64_t r[2] = {lo + hi, sf_mul(lo + (K.Q10 - hi), iw0, iw1, K.c2)};  // < 18.1 Q
+#pragma unroll
+            for (int z = 0; z < 2; ++z) {
+                const uint64_t y = sf_fold(acc[k + 4 * z] + r[z], K.c);  // < 2Q
+                acc[k + 4 * z] = y >= Q ? y - Q : y;
+            }
+        }
+    }
+    __syncthreads();
+    // member h writes polynomial h (acc0 transposed, poly.cpp:762-770) through the forward buffer (N words)
+    if (pp == h) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) bf[tau + 256 * k] = acc[k];
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < N; k += TH) {
+        if (h == 0) {
+            const uint64_t v = bf[k == 0 ? 0 : N - k];
+            g[k] = k == 0 ? v : (v == 0 ? 0 : Q - v);
+        } else {
+            g[N + k] = bf[k];
+        }
+    }
+}
+
 // W1 = w 2^32 mod Q for w < Q: w 2^32 = (w >> 22) 2^54 + (w mod 2^22) 2^32  (< 2^54 + 2^32 c < 2Q)
 __global__ void k_pack_sf(uint64_t Q, uint32_t c, const uint64_t* __restrict__ in, size_t words,
                           uint64_t* __restrict__ out) {
@@ -1808,17 +2176,26 @@ hipError_t launch_blind_rotate_sf(const BRParams& P, const DevTables& T, const v
                                (const uint64_t*)bsk, w1 + 4 * P.N, a, amod, acc, (const uint32_t*)nullptr,
                                (const uint64_t*)nullptr);
         };
-        if (P.digits == 2 && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs && B <= kDuoMaxPairs) {
+        if ((P.digits == 1 || P.digits == 2) && duo && B <= (size_t)kn.duo && B <= duo->resident_pairs &&
+            B <= kDuoMaxPairs) {
             const DuoBuf X = duo_layout(*duo);
-            const size_t ldsd = ((size_t)4 * G3_N + SF2D_MT) * 8 + rot_exponent_bytes(P.n);
-            auto dk = k_blind_rotate_sf2duo<0>;
+            // sfduo<DIG> (split by NTT half).  Two digits: sf2duo (split by accumulator polynomial, rounds 4-5) measured
+            // 1.5-2.4 % slower at C5b's 128 (profiles/r06m, two alternations on one box), kept as the test
+            // library's A/B form (probe 13)
+            auto dk = P.digits == 1 ? k_blind_rotate_sfduo<1> : k_blind_rotate_sfduo<2>;
+            size_t ldsd = (size_t)(P.digits == 1 ? 8 : 9) * G3_N * 8 + rot_exponent_bytes(P.n);
 #ifdef TFHE_TEST_PROBES
-            if (kn.probe == 5) dk = k_blind_rotate_sf2duo<1>;  // test library only: a partner that never arrives
+            if (kn.probe == 5) dk = P.digits == 1 ? k_blind_rotate_sfduo<1, 1> : k_blind_rotate_sfduo<2, 1>;  // a partner that never arrives
+            if (kn.probe == 7) dk = P.digits == 1 ? k_blind_rotate_sfduo<1, 2> : k_blind_rotate_sfduo<2, 2>;  // timing only: no hand-off
+            if (kn.probe == 13 && P.digits == 2) {  // the polynomial split (A/B)
+                dk = k_blind_rotate_sf2duo<0>;
+                ldsd = ((size_t)4 * G3_N + SF2D_MT) * 8 + rot_exponent_bytes(P.n);
+            }
 #endif
             (void)hipFuncSetAttribute((const void*)dk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsd);
             // the rescue: one-workgroup sf2 for the ciphertexts of timed-out pairs, from their saved inputs
             // (every other workgroup reads one word and exits: a few microseconds per launch)
-            auto rk = k_blind_rotate_sf2<2, true>;
+            auto rk = P.digits == 1 ? k_blind_rotate_sf2<1, true> : k_blind_rotate_sf2<2, true>;
             (void)hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             return duo_serialised(*duo, s, [&]() -> hipError_t {
                 if (hipError_t e = hipMemsetAsync(X.flags, 0, (size_t)B * 2 * 128, s); e != hipSuccess) return e;

@@ -122,4 +122,15 @@ __device__ __forceinline__ void stage_rot_exponents(uint32_t* ex, const uint64_t
 }
 __host__ __device__ constexpr size_t rot_exponent_bytes(uint32_t n) { return ((size_t)n * 4 + 15) & ~(size_t)15; }
 
+// The NTT-half duo kernels (f64wduo, blind_rotate_f64.hip; sfduo, blind_rotate_generic.hip): buffer index of
+// element x of a half polynomial (block x >> 8, y = x & 255).  y's low five bits are XORed with f(y[7:5]):
+// bit 5 -> bits 1, 3; bit 6 -> bit 4; bit 4 -> bits 0, 2, so that every b64 read is conflict-free per 32-lane
+// group (64 banks) AND every b64 write per 16-lane group (32 banks; MI355X_MICROARCH.md "LDS"), for every pass,
+// the cross-wave digit exchange and the units (tools/lds_layouts_duo.py; the round-5 first form, bits 5-7 into
+// bits 0-4 only, left the writes of passes (7,8), (10,9), (8,7) and the exchange 2-way).  Both kernels hold
+// 8-byte words, so the analysis covers both.
+__device__ __forceinline__ uint32_t dswz(uint32_t x) {
+    return x ^ (((x >> 5) & 1) * 10u) ^ (((x >> 6) & 1) << 4) ^ (((x >> 4) & 1) * 5u);
+}
+
 }  // namespace tfhe

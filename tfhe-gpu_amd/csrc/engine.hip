@@ -425,7 +425,7 @@ tfhe_status finish_device(tfhe_ctx* c, Device& d) {
     if (c->use_sf) {
         HCHECK(hipMalloc(&d.keys_sf, sf_bytes(c->br)));
         HCHECK(launch_pack_sf(c->br, d.tables, d.arena + c->layout.bsk, d.keys_sf, d.stream));
-        if (c->br.digits == 2) SCHECK(alloc_duo(d));
+        if (c->br.digits == 1 || c->br.digits == 2) SCHECK(alloc_duo(d));  // sfduo<1> / sf2duo
         HCHECK(hipStreamSynchronize(d.stream));
     }
     return TFHE_OK;

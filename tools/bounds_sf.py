@@ -148,13 +148,15 @@ def model(rows, sf2=True, form="sf2"):
     """form: "sf2" / gen3sf (two-level LDS factor tables), "sf2p" (one product per factor with a row of
     the 2N-entry table, no offset: S = fold(sf(A0, F+) + sf(A1, F-))), "duo" (sf2duo: a member sums its own
     polynomial's rows only -- `rows` digits x 1 polynomial -- and its accumulator update adds its own
-    column's inverse output and the partner's: acc + own + partner, one fold, one conditional subtraction)."""
+    column's inverse output and the partner's: acc + own + partner, one fold, one conditional subtraction),
+    "sfduo" (round 6, split by NTT half: sf2's offset-free forward on r + 28Q and sf2's inverse folds, element by
+    element in sf2's order, with sf2p's one product per factor; the update adds one inverse output, as sf2)."""
     Q = A.Q
     # sf2: digits r + 28Q, r in [-B/2, B/2), |r| <= Q/2 for any base the path admits; gen3sf: r mod Q + 28Q;
     # sf2p, sf2duo: r + Q with the offset in the difference (ct_ofs)
     global CT
     CT = ct_ofs if form in ("sf2p", "duo") else ct
-    mfull = form == "sf2p" or (form == "duo" and DUO_MFULL)
+    mfull = form in ("sf2p", "sfduo") or (form == "duo" and DUO_MFULL)
     x = (FWD_OFF * Q - Q // 2, FWD_OFF * Q + Q // 2) if sf2 else (FWD_OFF * Q, (FWD_OFF + 1) * Q)
     if form in ("sf2p", "duo"):
         x = (0, 2 * Q)
@@ -236,7 +238,9 @@ def main():
                                         ("sf2, C5b (two digits)", 2, True, "sf2"),
                                         ("sf2, CHES EvalFunc context (three digits)", 3, True, "sf2"),
                                         ("sf2p, C5b from 512 ciphertexts (two digits)", 2, True, "sf2p"),
-                                        ("sf2duo, C5b up to 128 ciphertexts (two digits)", 2, True, "duo"),
+                                        ("sf2duo, C5b up to 128 ciphertexts (two digits; test-library A/B form)", 2, True, "duo"),
+                                        ("sfduo<1>, C3 up to 128 ciphertexts (one digit)", 1, True, "sfduo"),
+                                        ("sfduo<2>, C5b up to 128 ciphertexts (two digits)", 2, True, "sfduo"),
                                         ("gen3sf, 3 digits (TOY logQ 23)", 3, False, "sf2"),
                                         ("gen3sf, 8 digits (the most any context has)", 8, False, "sf2")):
             print(f"c = {c}, {name}")

@@ -14,8 +14,11 @@
   func   CHES-experiments.cpp:64-126: EvalFunc(x^3 mod p) in GenerateBinFHEContext(STD128, true,
          12, 0, GINX, false, 1 << 18) at B = 1, 8, 64, 256, 512 (host-array, device-resident, and
          the drop-in through ref_dropin sizes=...).
+  arb    C3's context (arbFunc logQ 12, one transformed digit): EvalFunc(m^3 mod 8) and the blind rotation
+         at B = 64 .. 4096, the two-workgroup sfduo<1> against the one-workgroup sf2<1> at the duo batches.
+  duo2   C5b's context at 128: sf2duo against sfduo<2> (test library, probe 13) and one workgroup.
 
-    python3 tools/small_batch.py [sign] [and] [func] [--reps 5]
+    python3 tools/small_batch.py [sign] [and] [func] [split] [arb] [duo2] [--reps 5]
 
 One JSON line per measurement.
 """
@@ -288,14 +291,139 @@ def run_func(reps):
     emit(res)
 
 
+def run_arb(reps):
+    """C3's context (arbFunc logQ 12, one transformed digit) at small batches: EvalFunc(m^3 mod 8) device-resident
+    and the blind rotation alone at B = 64 .. 4096; at the duo batches also the one-workgroup sf2<1> (duo = 0) on
+    the same box, alternating, and the first 4 outputs against the oracle."""
+    import torch
+
+    import pyoracle
+    import tfhe_amd
+    from bench import cube_lut, synthetic_keys
+
+    spec = ("STD128", True, 12, 0, 0, 1)
+    p, po = tfhe_amd.params_from_logq(*spec), pyoracle.params_from_logq(*spec)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(s)
+    sp = s.cuda_stream
+    sync = lambda: torch.cuda.synchronize(dev)
+    progress("C3: keys")
+    bsk, ksk = synthetic_keys(p)
+    ctx = tfhe_amd.BinFHEContextHIP(p).GPUSetup(bsk, ksk)
+    progress("C3: oracle")
+    orc = pyoracle.Oracle(po, bsk, ksk)
+    del bsk, ksk
+    lut = cube_lut(int(p.q))
+    dl = torch.from_numpy(lut.astype(np.int64)).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    full = torch.randint(0, int(p.q), (4096, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    lib = tfhe_amd.lib()
+    rows = []
+    for B in (64, 128, 256, 512, 1024, 4096):
+        progress(f"C3: B={B}")
+        ct = full[:B].contiguous()
+        out = torch.empty_like(ct)
+        call = lambda: ctx.EvalFuncDevice(B, ct.data_ptr(), dl.data_ptr(), out.data_ptr(), stream=sp)
+        a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
+        acc = torch.zeros((B, 2, p.N), dtype=torch.int64, device=dev)
+        br_call = lambda: tfhe_amd.capi.check(
+            lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp), "eval_acc")
+        b0 = ctx.info().bootstraps
+        call()
+        sync()
+        per = (ctx.info().bootstraps - b0) // B
+        forms = [("", {})] + ([("one_workgroup_", {"duo": 0})] if B <= ctx.knobs()["duo"] else [])
+        res = {k: [[], []] for k, _ in forms}
+        for _ in range(2):  # two alternating reps of every form
+            for k, kn in forms:
+                with ctx.knobs_set(**kn):
+                    res[k][0].append(timed(call, reps, sync)[0])
+                    res[k][1].append(timed(br_call, reps, sync)[0])
+        call()
+        sync()
+        h = ct[:4].cpu().numpy().astype(np.uint64)
+        exact = bool(np.array_equal(out[:4].cpu().numpy().astype(np.uint64), orc.eval_func(h, lut)))
+        best = min(res[""][0])
+        row = {"B": B, "ms_per_call": round(best * 1e3, 3), "bootstraps_per_ct": per,
+               "bootstraps_per_s": round(B * per / best, 1), "blind_rotation_ms": round(min(res[""][1]) * 1e3, 3),
+               "parity_4": exact}
+        if len(forms) > 1:
+            row.update(one_workgroup_ms_per_call=round(min(res["one_workgroup_"][0]) * 1e3, 3),
+                       one_workgroup_blind_rotation_ms=round(min(res["one_workgroup_"][1]) * 1e3, 3))
+        rows.append(row)
+    ref = rows[-1]["bootstraps_per_s"]
+    for r in rows:
+        r["rate_vs_4096"] = round(r["bootstraps_per_s"] / ref, 3)
+    emit({"what": "C3 arbFunc logQ 12 EvalFunc(m^3 mod 8) device-resident batch sweep",
+          "kernel": int(ctx.info().br_kernel), "duo_timeouts": int(ctx.info().duo_timeouts), "rows": rows})
+    orc.close()
+    ctx.GPUClean()
+
+
+def run_duo2(reps, libpath=None):
+    """C5b's context (two transformed digits) at the 8-GPU shard (128): the blind rotation and EvalSign on
+    sf2duo (split by accumulator polynomial, the default), on sfduo<2> (split by NTT half; test library,
+    probe 13) and on one workgroup per ciphertext, alternating on one box; outputs compared."""
+    import torch
+
+    import tfhe_amd
+    from bench import SIGN_MOD, synthetic_keys
+
+    p = tfhe_amd.params_from_logq("STD128", False, 23, 0, 0, 1)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(s)
+    sp = s.cuda_stream
+    sync = lambda: torch.cuda.synchronize(dev)
+    progress("C5b: keys")
+    bsk, ksk = synthetic_keys(p)
+    ctx = tfhe_amd.BinFHEContextHIP(p, library=libpath or tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
+    del bsk, ksk
+    lib = ctx._L  # the test library the context was set up on
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    B = 128
+    ct = torch.randint(0, SIGN_MOD, (B, p.n + 1), dtype=torch.int64, device=dev, generator=g)
+    out = torch.empty_like(ct)
+    a = torch.randint(0, int(p.q), (B, p.n), dtype=torch.int64, device=dev, generator=g)
+    acc0 = torch.randint(0, int(p.Q), (B, 2, p.N), dtype=torch.int64, device=dev, generator=g)
+    acc = acc0.clone()
+    sign = lambda: ctx.EvalSignDevice(B, ct.data_ptr(), SIGN_MOD, out.data_ptr(), stream=sp)
+    br = lambda: tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp),
+                                     "eval_acc")
+    forms = [("sf2duo", {}), ("sfduo2", {"probe": 13}), ("one_workgroup", {"duo": 0})]
+    res = {k: {"sign_ms": [], "br_ms": []} for k, _ in forms}
+    outs = {}
+    for _ in range(3):
+        for k, kn in forms:
+            with ctx.knobs_set(**kn):
+                progress(f"C5b 128: {k}")
+                res[k]["sign_ms"].append(round(timed(sign, reps, sync)[0] * 1e3, 3))
+                res[k]["br_ms"].append(round(timed(br, reps, sync)[0] * 1e3, 3))
+                acc.copy_(acc0)
+                br()
+                sign()
+                sync()
+                outs[k] = (acc.cpu().numpy(), out.cpu().numpy())
+    same = all(np.array_equal(outs[k][0], outs["one_workgroup"][0]) and np.array_equal(outs[k][1], outs["one_workgroup"][1])
+               for k in outs)
+    emit({"what": "C5b at 128: sf2duo vs sfduo<2> vs one workgroup (alternating, one box)", "B": B, "lib": libpath,
+          "forms": res, "outputs_equal": same, "duo_timeouts": int(ctx.info().duo_timeouts)})
+    ctx.GPUClean()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("what", nargs="*", default=["sign", "and", "func"])
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="duo2: a test-library build (default lib/libtfhe_hip_test.so)")
     args = ap.parse_args()
     for w in args.what:
         {"sign": lambda: run_sign(args.reps), "and": lambda: run_and(), "func": lambda: run_func(args.reps),
-         "split": lambda: run_split(args.reps)}[w]()
+         "split": lambda: run_split(args.reps), "arb": lambda: run_arb(args.reps),
+         "duo2": lambda: run_duo2(args.reps, args.lib)}[w]()
 
 
 if __name__ == "__main__":
