@@ -1705,9 +1705,17 @@ k_blind_rotate_sf2duo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const
 // and round: 24 forward products per digit against sf2's 44, 8 x DIG key products against 16 x DIG, 8 factor
 // products against 16, 24 inverse against 44.  A member that times out sets the pair's failed word and the
 // rescue launch (k_blind_rotate_sf2<DIG, true>) recomputes the ciphertext from its saved input.
-// LDS: forward twiddles (W0, W1) 32 KiB, forward / inverse buffers 2 x 16 KiB, two digits a third buffer,
-// factor table 64 KiB, exponents: 132 / 148 KiB, one workgroup per CU.
-template <class TW>
+// LDS: twiddles 32 KiB (both directions' compact half tables, SFD_TWL), forward / inverse buffers 2 x 16 KiB, two
+// digits a third buffer, factor table 64 KiB, exponents: 132 / 148 KiB, one workgroup per CU.
+// Twiddle index of stage s (full table: 2^s + j).  CMP: the member's compact half table -- a member of an
+// NTT-half pair uses only the entries of its half at every stage s >= 1 (j in [h 2^(s-1), (h + 1) 2^(s-1))),
+// so entry 2^s + j moves to 2^(s-1) + (j - h 2^(s-1)), and stage 0's entry 1 to 0: N / 2 entries per table,
+// which lets both directions' twiddles sit in LDS (sfduo, SFD_TWL)
+template <bool CMP>
+__device__ __forceinline__ uint32_t twi(uint32_t idx, int s, uint32_t h) {
+    return !CMP ? idx : s == 0 ? 0u : idx - (1u << (s - 1)) * (1 + h);
+}
+template <bool CMP, class TW>
 __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], uint64_t (&d)[4], uint32_t h,
                                         const TW& T, const SfC& K) {
     constexpr uint32_t H = G3_N / 2;
@@ -1715,15 +1723,15 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
     {
         const uint32_t tau = g3_tau();
         uint64_t* p = bf + (t >> 8) * H + dswz(tau);
-        const uint64_t w0 = tw0(T, 1), w1 = tw1(T, 1);
+        const uint64_t w0 = tw0(T, twi<CMP>(1, 0, h)), w1 = tw1(T, twi<CMP>(1, 0, h));
         uint64_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // stage 0, this half's outputs (x - v >= 0: inputs carry 28Q)
             const uint64_t x = sf_mul(v[k + 4], w0, w1, K.c2);
             o[k] = h ? v[k] - x : v[k] + x;
         }
-        sf_ct(o[0], o[2], T, 2 + h, K), sf_ct(o[1], o[3], T, 2 + h, K);
-        sf_ct(o[0], o[1], T, 4 + 2 * h, K), sf_ct(o[2], o[3], T, 5 + 2 * h, K);
+        sf_ct(o[0], o[2], T, twi<CMP>(2 + h, 1, h), K), sf_ct(o[1], o[3], T, twi<CMP>(2 + h, 1, h), K);
+        sf_ct(o[0], o[1], T, twi<CMP>(4 + 2 * h, 2, h), K), sf_ct(o[2], o[3], T, twi<CMP>(5 + 2 * h, 2, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) p[256 * k] = o[k];
     }
@@ -1736,8 +1744,8 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
         asm volatile("" : "+v"(y));
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
-        sf_ct(x[0], x[2], T, 8 + B, K), sf_ct(x[1], x[3], T, 8 + B, K);
-        sf_ct(x[0], x[1], T, 16 + 2 * B, K), sf_ct(x[2], x[3], T, 17 + 2 * B, K);
+        sf_ct(x[0], x[2], T, twi<CMP>(8 + B, 3, h), K), sf_ct(x[1], x[3], T, twi<CMP>(8 + B, 3, h), K);
+        sf_ct(x[0], x[1], T, twi<CMP>(16 + 2 * B, 4, h), K), sf_ct(x[2], x[3], T, twi<CMP>(17 + 2 * B, 4, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = x[k];
     }
@@ -1746,8 +1754,8 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
         const uint32_t c = l >> 4, y = 64 * c + (l & 15);
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
-        sf_ct(x[0], x[2], T, 32 + 4 * B + c, K), sf_ct(x[1], x[3], T, 32 + 4 * B + c, K);
-        sf_ct(x[0], x[1], T, 64 + 8 * B + 2 * c, K), sf_ct(x[2], x[3], T, 65 + 8 * B + 2 * c, K);
+        sf_ct(x[0], x[2], T, twi<CMP>(32 + 4 * B + c, 5, h), K), sf_ct(x[1], x[3], T, twi<CMP>(32 + 4 * B + c, 5, h), K);
+        sf_ct(x[0], x[1], T, twi<CMP>(64 + 8 * B + 2 * c, 6, h), K), sf_ct(x[2], x[3], T, twi<CMP>(65 + 8 * B + 2 * c, 6, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
     }
@@ -1756,8 +1764,8 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
         const uint32_t c = l >> 2, y = 16 * c + (l & 3);
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
-        sf_ct(x[0], x[2], T, 128 + 16 * B + c, K), sf_ct(x[1], x[3], T, 128 + 16 * B + c, K);
-        sf_ct(x[0], x[1], T, 256 + 32 * B + 2 * c, K), sf_ct(x[2], x[3], T, 257 + 32 * B + 2 * c, K);
+        sf_ct(x[0], x[2], T, twi<CMP>(128 + 16 * B + c, 7, h), K), sf_ct(x[1], x[3], T, twi<CMP>(128 + 16 * B + c, 7, h), K);
+        sf_ct(x[0], x[1], T, twi<CMP>(256 + 32 * B + 2 * c, 8, h), K), sf_ct(x[2], x[3], T, twi<CMP>(257 + 32 * B + 2 * c, 8, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
     }
@@ -1766,8 +1774,8 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
         const uint32_t y = 4 * l;
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + k)];
-        sf_ct(x[0], x[2], T, 512 + 64 * B + l, K), sf_ct(x[1], x[3], T, 512 + 64 * B + l, K);
-        sf_ct(x[0], x[1], T, 1024 + 128 * B + 2 * l, K), sf_ct(x[2], x[3], T, 1025 + 128 * B + 2 * l, K);
+        sf_ct(x[0], x[2], T, twi<CMP>(512 + 64 * B + l, 9, h), K), sf_ct(x[1], x[3], T, twi<CMP>(512 + 64 * B + l, 9, h), K);
+        sf_ct(x[0], x[1], T, twi<CMP>(1024 + 128 * B + 2 * l, 10, h), K), sf_ct(x[2], x[3], T, twi<CMP>(1025 + 128 * B + 2 * l, 10, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) d[k] = x[k];
     }
@@ -1775,7 +1783,7 @@ __device__ __forceinline__ void sfd_fwd(uint64_t* bf, const uint64_t (&v)[8], ui
 
 // inverse: s = column w >> 2's NTT-domain increment at the lane's slots -> after stages 10..1 o = elements
 // tau + 256k' (k' < 4) of half h of column t >> 8 (stage-1 outputs; stage 0 follows the hand-off)
-template <class TW>
+template <bool CMP, class TW>
 __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], uint64_t (&o)[4], uint32_t h,
                                         const TW& T, const SfC& K) {
     constexpr uint32_t H = G3_N / 2;
@@ -1785,8 +1793,8 @@ __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], ui
     uint64_t x[4] = {s[0], s[1], s[2], s[3]};
     {  // stages 10, 9 (stage 9's sums folded, as sf2's units)
         const uint32_t y = 4 * l;
-        sf_gs(x[0], x[1], T, 1024 + 128 * B + 2 * l, K), sf_gs(x[2], x[3], T, 1025 + 128 * B + 2 * l, K);
-        sf_gs<true>(x[0], x[2], T, 512 + 64 * B + l, K), sf_gs<true>(x[1], x[3], T, 512 + 64 * B + l, K);
+        sf_gs(x[0], x[1], T, twi<CMP>(1024 + 128 * B + 2 * l, 10, h), K), sf_gs(x[2], x[3], T, twi<CMP>(1025 + 128 * B + 2 * l, 10, h), K);
+        sf_gs<true>(x[0], x[2], T, twi<CMP>(512 + 64 * B + l, 9, h), K), sf_gs<true>(x[1], x[3], T, twi<CMP>(512 + 64 * B + l, 9, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + k)] = x[k];
     }
@@ -1795,8 +1803,8 @@ __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], ui
         const uint32_t c = l >> 2, y = 16 * c + (l & 3);
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 4 * k)];
-        sf_gs(x[0], x[1], T, 256 + 32 * B + 2 * c, K), sf_gs(x[2], x[3], T, 257 + 32 * B + 2 * c, K);
-        sf_gs(x[0], x[2], T, 128 + 16 * B + c, K), sf_gs(x[1], x[3], T, 128 + 16 * B + c, K);
+        sf_gs(x[0], x[1], T, twi<CMP>(256 + 32 * B + 2 * c, 8, h), K), sf_gs(x[2], x[3], T, twi<CMP>(257 + 32 * B + 2 * c, 8, h), K);
+        sf_gs(x[0], x[2], T, twi<CMP>(128 + 16 * B + c, 7, h), K), sf_gs(x[1], x[3], T, twi<CMP>(128 + 16 * B + c, 7, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 4 * k)] = x[k];
     }
@@ -1805,8 +1813,8 @@ __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], ui
         const uint32_t c = l >> 4, y = 64 * c + (l & 15);
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 16 * k)];
-        sf_gs<true>(x[0], x[1], T, 64 + 8 * B + 2 * c, K), sf_gs<true>(x[2], x[3], T, 65 + 8 * B + 2 * c, K);
-        sf_gs(x[0], x[2], T, 32 + 4 * B + c, K), sf_gs(x[1], x[3], T, 32 + 4 * B + c, K);
+        sf_gs<true>(x[0], x[1], T, twi<CMP>(64 + 8 * B + 2 * c, 6, h), K), sf_gs<true>(x[2], x[3], T, twi<CMP>(65 + 8 * B + 2 * c, 6, h), K);
+        sf_gs(x[0], x[2], T, twi<CMP>(32 + 4 * B + c, 5, h), K), sf_gs(x[1], x[3], T, twi<CMP>(32 + 4 * B + c, 5, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 16 * k)] = x[k];
     }
@@ -1816,8 +1824,8 @@ __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], ui
         asm volatile("" : "+v"(y));
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = q[dswz(y + 64 * k)];
-        sf_gs(x[0], x[1], T, 16 + 2 * B, K), sf_gs(x[2], x[3], T, 17 + 2 * B, K);
-        sf_gs<true>(x[0], x[2], T, 8 + B, K), sf_gs<true>(x[1], x[3], T, 8 + B, K);
+        sf_gs(x[0], x[1], T, twi<CMP>(16 + 2 * B, 4, h), K), sf_gs(x[2], x[3], T, twi<CMP>(17 + 2 * B, 4, h), K);
+        sf_gs<true>(x[0], x[2], T, twi<CMP>(8 + B, 3, h), K), sf_gs<true>(x[1], x[3], T, twi<CMP>(8 + B, 3, h), K);
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[dswz(y + 64 * k)] = x[k];
     }
@@ -1827,14 +1835,20 @@ __device__ __forceinline__ void sfd_inv(uint64_t* bi, const uint64_t (&s)[4], ui
         const uint64_t* p = bi + (t >> 8) * H + dswz(tau);
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = p[256 * k];
-        sf_gs(o[0], o[1], T, 4 + 2 * h, K), sf_gs(o[2], o[3], T, 5 + 2 * h, K);
-        sf_gs(o[0], o[2], T, 2 + h, K), sf_gs(o[1], o[3], T, 2 + h, K);
+        sf_gs(o[0], o[1], T, twi<CMP>(4 + 2 * h, 2, h), K), sf_gs(o[2], o[3], T, twi<CMP>(5 + 2 * h, 2, h), K);
+        sf_gs(o[0], o[2], T, twi<CMP>(2 + h, 1, h), K), sf_gs(o[1], o[3], T, twi<CMP>(2 + h, 1, h), K);
     }
 }
 
 #ifndef SFD_KPRE
 #define SFD_KPRE 2
 #endif
+// SFD_TWL: both directions' twiddles in LDS as the member's compact half tables (twi), instead of the forward
+// table whole in LDS and the inverse one read from memory at every stage (the same 32 KiB of LDS)
+#ifndef SFD_TWL
+#define SFD_TWL 1
+#endif
+
 // PROBE 1 (test library only, TFHE_TEST_PROBES): member 1 of pair 0 stops publishing at round 2, as a partner
 // that never arrives would, and the wait is a 64th of the 10 ms bound.  PROBE 2 (timing only, results invalid):
 // no hand-off -- each member takes its own stage-1 values for its partner's.
@@ -1853,10 +1867,12 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
     constexpr uint32_t N = G3_N, H = N / 2, TH = G3_TH;
     const uint32_t b = blockIdx.x, pair = (b >> 4) * 8 + (b & 7), h = (b >> 3) & 1;
     if (pair >= pairs) return;  // both members of a pair take this branch together
-    __shared__ uint32_t duo_ok;
-    uint64_t* tf0 = reinterpret_cast<uint64_t*>(smem);  // forward twiddles W0 [N], W1 [N]
-    uint64_t* tf1 = tf0 + N;
-    uint64_t* bf = tf1 + N;                  // forward buffer [2][H]
+    __shared__ uint32_t duo_ok, duo_fail;
+    uint64_t* tf0 = reinterpret_cast<uint64_t*>(smem);  // SFD_TWL: forward and inverse W0, W1 [4][H] (compact);
+    uint64_t* tf1 = tf0 + (SFD_TWL ? H : N);            // else forward W0 [N], W1 [N]
+    uint64_t* ti0 = tf1 + H;
+    uint64_t* ti1 = ti0 + H;
+    uint64_t* bf = tf0 + 2 * N;              // forward buffer [2][H]
     uint64_t* bi = bf + N;                   // inverse buffer [2][H]
     uint64_t* dx = bi + N;                   // DIG = 2: digit 0's values for the other column's waves [2][H]
     uint64_t* mt = dx + (DIG > 1 ? N : 0);   // factor table: row e = (psi^e - 1, its W1) [2N][2]
@@ -1868,12 +1884,20 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
     const uint64_t Q = K.Q, Qhalf = P.Q >> 1;
     const int64_t Qs = (int64_t)P.Q, Bh = (int64_t)1 << (logG - 1);
     const uint32_t sh = 64 - logG;
-    for (uint32_t k = t; k < N; k += TH) tf0[k] = psi[k], tf1[k] = psi1[k];
+    if constexpr (SFD_TWL) {
+        for (uint32_t k = t; k < H; k += TH) {  // compact entry k of half h: full index k + 2^(s-1) (1 + h)
+            const uint32_t e = k == 0 ? 1 : k + (1u << (31 - __builtin_clz(k))) * (1 + h);
+            tf0[k] = psi[e], tf1[k] = psi1[e], ti0[k] = ipsi[e], ti1[k] = ipsi1[e];
+        }
+    } else {
+        for (uint32_t k = t; k < N; k += TH) tf0[k] = psi[k], tf1[k] = psi1[k];
+    }
     for (uint32_t k = t; k < twoN; k += TH) {
         mt[2 * sf_mrow(k)] = mono[k] % Q;  // psi^k - 1
         mt[2 * sf_mrow(k) + 1] = mono1[k];
     }
     const SfTw TF{tf0, tf1};
+    const SfTw TIL{ti0, ti1};
     const SfTwB TI{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi), 0, (int)(N * 8), 0x00020000),
                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(ipsi1), 0, (int)(N * 8), 0x00020000)};
     uint64_t* g = acc_io + (size_t)pair * twoN;
@@ -1882,6 +1906,7 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
     const size_t round_words = (size_t)4 * P.dG2 * N;
     const uint32_t tau = t & 255, pp = t >> 8;  // pass-A role: coefficients tau + 256k of polynomial pp
 
+    if (t == 0) duo_fail = 0;
     uint64_t acc[8];  // canonical [0, Q), all N coefficients of polynomial pp (both members)
     uint64_t* sv = X.save + (size_t)pair * twoN;
 #pragma unroll
@@ -1891,6 +1916,8 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
         acc[k] = v >= Q ? v % Q : v;
     }
     __syncthreads();  // twiddles, factor table, exponents in LDS
+    // the inverse's stage-0 twiddle, once (its load sat behind the hand-off of every round)
+    const uint64_t iw0 = SFD_TWL ? ti0[0] : tw0(TI, 1), iw1 = SFD_TWL ? ti1[0] : tw1(TI, 1);
 
     const __amdgpu_buffer_rsrc_t rk0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk), 0, -1, 0x00020000);
     const __amdgpu_buffer_rsrc_t rk1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bsk1), 0, -1, 0x00020000);
@@ -1941,7 +1968,7 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
                 v[k] = (uint64_t)r + K.Qf;  // r mod Q + 28Q (the offset-free forward's inputs)
             }
             if (d > 0) __syncthreads();  // other waves may still read their blocks of digit d - 1
-            sfd_fwd(bf, v, D[d], h, TF, K);
+            sfd_fwd<SFD_TWL>(bf, v, D[d], h, TF, K);
         }
         // this lane's digits for the other column's waves (each wave writes only its own block: bf the last
         // digit, dx digit 0 when DIG = 2)
@@ -1985,45 +2012,49 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
             S[s] = sf_fold(sf_mul(A[0][s], fp[0], fp[1], K.c2) + sf_mul(A[1][s], fm[0], fm[1], K.c2), K.c);
         }
         uint64_t o[4];
-        sfd_inv(bi, S, o, h, TI, K);
+        if constexpr (SFD_TWL) sfd_inv<true>(bi, S, o, h, TIL, K);
+        else sfd_inv<false>(bi, S, o, h, TI, K);
         // hand-off: this half's stage-1 values of both columns to the partner (thread t's 4 at k' 512 + t)
         uint64_t* mine = X.xbuf + (((size_t)pair * 2 + h) * 2 + (i & 1)) * N;
         const uint64_t* theirs = X.xbuf + (((size_t)pair * 2 + (1 - h)) * 2 + (i & 1)) * N;
-        if constexpr (PROBE != 2) {
+        // (measured against a data-tagged form -- the round's tag in each word's bits 58-63, per-thread polls, no flag
+        // or barrier: a tie at 128 in C3's and C5b's contexts, profiles/r06o; the hand-off costs 1.8 us of a 7.6-us
+        // round either way)
+        uint64_t pv[4];
+        {
+            if constexpr (PROBE != 2) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) duo_store(mine + 512 * k + t, o[k]);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // every wave's stores drained; every read of the buffers done
-        if (PROBE != 2 && t == 0) {
-            const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
-            if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool ok = !gone;
-            uint64_t t_end = 0;
-            uint32_t k = 0;
-            while (ok && __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1) {
-                if ((++k & 7) == 0) {  // the clock every 8th poll, the deadline set at the first read
-                    const uint64_t now = wall_clock64();
-                    if (t_end == 0) t_end = now + (PROBE ? X.wait_ticks >> 6 : X.wait_ticks);
-                    else if (now > t_end) ok = false;
+                for (int k = 0; k < 4; ++k) duo_store(mine + 512 * k + t, o[k]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // every wave's stores drained; every read of the buffers done
+            if (PROBE != 2 && t == 0) {
+                const bool gone = PROBE == 1 && pair == 0 && h == 1 && i >= 2;
+                if (!gone) __hip_atomic_store(myflag, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bool ok = !gone;
+                uint64_t t_end = 0;
+                uint32_t k = 0;
+                while (ok && __hip_atomic_load(const_cast<uint32_t*>(peerflag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i + 1) {
+                    if ((++k & 7) == 0) {  // the clock every 8th poll, the deadline set at the first read
+                        const uint64_t now = wall_clock64();
+                        if (t_end == 0) t_end = now + (PROBE ? X.wait_ticks >> 6 : X.wait_ticks);
+                        else if (now > t_end) ok = false;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                duo_ok = ok;
+                if (!ok) duo_fail = 1;
             }
-            duo_ok = ok;
-            if (!ok) {
-                __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (PROBE != 2) {
+                __syncthreads();
+                if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) pv[k] = PROBE == 2 ? o[k] : duo_load(theirs + 512 * k + t);
         }
-        if constexpr (PROBE != 2) {
-            __syncthreads();
-            if (!duo_ok) break;  // uniform: the partner never arrived (the rescue launch recomputes the pair)
-        }
-        const uint64_t iw0 = tw0(TI, 1), iw1 = tw1(TI, 1);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // stage 0 for all coefficients (sf2's pass A end), then sf2's update
-            const uint64_t pv = PROBE == 2 ? o[k] : duo_load(theirs + 512 * k + t);
-            const uint64_t lo = h ? pv : o[k], hi = h ? o[k] : pv;
+            const uint64_t lo = h ? pv[k] : o[k], hi = h ? o[k] : pv[k];
             const uint64_t r[2] = {lo + hi, sf_mul(lo + (K.Q10 - hi), iw0, iw1, K.c2)};  // < 18.1 Q
 #pragma unroll
             for (int z = 0; z < 2; ++z) {
@@ -2033,6 +2064,10 @@ k_blind_rotate_sfduo(BRParams P, SfC K, const uint64_t* __restrict__ psi, const 
         }
     }
     __syncthreads();
+    if (duo_fail && t == 0) {  // this member timed out: fail the pair (the rescue launch recomputes it)
+        __hip_atomic_store(X.flags + pair * 2 * 32 + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(X.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // member h writes polynomial h (acc0 transposed, poly.cpp:762-770) through the forward buffer (N words)
     if (pp == h) {
 #pragma unroll

@@ -65,9 +65,13 @@ def main():
                                         "eval_acc")
                     torch.cuda.synchronize(dev)
                     ts.append(time.perf_counter() - t0)
+            finals = row.setdefault("_finals", {})
+            finals[tag] = acc.cpu()
             row[f"{tag}_ms"] = round(min(ts[1:]) * 1e3, 3)
             row[f"{tag}_us_per_round"] = round(min(ts[1:]) * 1e6 / p.n, 2)
         row["handoff_us_per_round"] = round(row["duo_us_per_round"] - row["free_us_per_round"], 2)
+        finals = row.pop("_finals")
+        row["duo_equals_one"] = bool(torch.equal(finals["duo"], finals["one"]))  # same inputs, same number of runs
         rows.append(row)
     kern = "f64wduo" if args.ctx == "STD128Q" else "sfduo<1>"
     print(json.dumps({"what": f"{kern} hand-off price ({args.ctx} blind rotation, device-resident)", "lib": libpath,

@@ -16,7 +16,7 @@
          the drop-in through ref_dropin sizes=...).
   arb    C3's context (arbFunc logQ 12, one transformed digit): EvalFunc(m^3 mod 8) and the blind rotation
          at B = 64 .. 4096, the two-workgroup sfduo<1> against the one-workgroup sf2<1> at the duo batches.
-  duo2   C5b's context at 128: sf2duo against sfduo<2> (test library, probe 13) and one workgroup.
+  duo2   C5b's context at 128: sfduo<2> (the default) against sf2duo (test library, probe 13) and one workgroup.
 
     python3 tools/small_batch.py [sign] [and] [func] [split] [arb] [duo2] [--reps 5]
 
@@ -364,8 +364,10 @@ def run_arb(reps):
 
 def run_duo2(reps, libpath=None):
     """C5b's context (two transformed digits) at the 8-GPU shard (128): the blind rotation and EvalSign on
-    sf2duo (split by accumulator polynomial, the default), on sfduo<2> (split by NTT half; test library,
-    probe 13) and on one workgroup per ciphertext, alternating on one box; outputs compared."""
+    sfduo<2> (split by NTT half, the default since round 6), on sf2duo (split by accumulator polynomial; test
+    library, probe 13) and on one workgroup per ciphertext, alternating on one box; outputs compared.
+    (profiles/r06l, r06m: run before the default changed, so their "sf2duo" key is the default form of then,
+    sf2duo, and "sfduo2" is probe 13 of then, sfduo<2>.)"""
     import torch
 
     import tfhe_amd
@@ -393,7 +395,7 @@ def run_duo2(reps, libpath=None):
     sign = lambda: ctx.EvalSignDevice(B, ct.data_ptr(), SIGN_MOD, out.data_ptr(), stream=sp)
     br = lambda: tfhe_amd.capi.check(lib.tfhe_eval_acc_device(ctx.handle, B, a.data_ptr(), int(p.q), acc.data_ptr(), sp),
                                      "eval_acc")
-    forms = [("sf2duo", {}), ("sfduo2", {"probe": 13}), ("one_workgroup", {"duo": 0})]
+    forms = [("sfduo2", {}), ("sf2duo", {"probe": 13}), ("one_workgroup", {"duo": 0})]
     res = {k: {"sign_ms": [], "br_ms": []} for k, _ in forms}
     outs = {}
     for _ in range(3):
