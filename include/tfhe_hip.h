@@ -111,7 +111,7 @@ typedef struct tfhe_info {
     int br_kernel;             /* blind rotation for power-of-two a-moduli: TFHE_BR_* */
     int replicate_method;      /* how setup replicated the key image to devices 1..: TFHE_REPLICATE_* */
     double replicate_ms;       /* wall time of that replication (0 for one device) */
-    uint32_t duo_timeouts;     /* workgroups of the two-workgroup forms (sf2duo: two-digit special-form
+    uint32_t duo_timeouts;     /* workgroups of the two-workgroup forms (sfduo: one- and two-digit special-form
                                   contexts; f64wduo: STD128Q and STD192 classes) that timed out waiting for their partner
                                   (10 ms of wall clock in one round) since setup, summed over devices
                                   (synchronises them); the ciphertexts of such a pair are recomputed from
@@ -282,7 +282,7 @@ typedef struct tfhe_knobs {
     int32_t generic;      /* generic kernel form: 0 by N; 1 v1 (digits in LDS); 2 v2 also at N = 2048 */
     int32_t trace;        /* host-array runner timeline on stderr */
     int32_t probe;        /* test library only (lib/libtfhe_hip_test.so): fault-probe / timing builds */
-    int32_t duo;          /* two-digit special-form contexts (sf2duo) and STD128Q- / STD192-class FP64 contexts (f64wduo):
+    int32_t duo;          /* one- and two-digit special-form contexts (sfduo) and STD128Q- / STD192-class FP64 contexts (f64wduo):
                              batches up to this size (default 128, at most 256) run each ciphertext on two
                              workgroups, and only while the device holds every pair co-resident (a duo workgroup
                              takes one CU: at most half the CU count, 128 on MI355X); 0: never */
