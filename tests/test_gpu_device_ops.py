@@ -13,21 +13,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module", params=["STD128", "arb12"])
-def env(request, oracle):
-    import tfhe_amd
-
-    if request.param == "STD128":
-        op, cp = oracle.params_from_set("STD128"), tfhe_amd.params_from_set("STD128")
-    else:
-        op = oracle.params_from_logq("STD128", True, 12, 0, 0, 1)
-        cp = tfhe_amd.params_from_logq("STD128", True, 12, 0, 0, 1)
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(3))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield op, ctx, orc
-    ctx.GPUClean()
-    orc.close()
+def env(request, shared_kat):
+    s = shared_kat("STD128" if request.param == "STD128" else "ARB12")  # the session's shared contexts
+    return s["op"], s["ctx"], s["orc"]
 
 
 def _dev(x):

@@ -26,20 +26,13 @@ def _ctx_params(mod):
 
 
 @pytest.fixture(scope="module")
-def duo(oracle):
-    import tfhe_amd
-
-    op, cp = _ctx_params(oracle), _ctx_params(tfhe_amd)
-    assert (cp.digitsG - cp.numDigitsToThrow) == 2 and cp.N == 2048  # the sf2<2> / sf2duo shape
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(77))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+def duo(shared_kat):
+    s = shared_kat("LOGQ23")
+    cp, ctx = s["cp"], s["ctx"]
+    assert (cp.digitsG - cp.numDigitsToThrow) == 2 and cp.N == 2048  # the sf2<2> / sfduo<2> shape
     assert ctx.knobs()["duo"] == 128
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield dict(op=op, ctx=ctx, orc=orc)
+    yield s
     assert ctx.info().duo_timeouts == 0
-    ctx.GPUClean()
-    orc.close()
 
 
 def _inputs(op, B, seed):
@@ -118,55 +111,39 @@ def test_duo_evalsign_shard_decrypts(oracle):
         orc.close()
 
 
-def test_duo_partner_timeout_is_recomputed(oracle):
+def test_duo_partner_timeout_is_recomputed(shared_kat):
     """A partner that never arrives: the test library's probe 5 makes member 1 of pair 0 stop
     publishing at round 2.  Both members time out, the pair's failed word is set, and the rescue launch
     behind the duo kernel recomputes that ciphertext from its saved input with the one-workgroup kernel:
     every output stays bit-exact and tfhe_info.duo_timeouts counts the two timed-out workgroups."""
-    import tfhe_amd
-
-    op, cp = _ctx_params(oracle), _ctx_params(tfhe_amd)
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(78))
-    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    try:
-        a, acc = _inputs(op, 9, 400)
-        want = orc.eval_acc(a, 2 * op.N, acc)
-        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
-        assert ctx.info().duo_timeouts == 0
-        with ctx.knobs_set(probe=5):
-            got = ctx.EvalAcc(a, 2 * op.N, acc)
-        assert np.array_equal(got, want)
-        assert ctx.info().duo_timeouts == 2
-        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)  # the failed word is cleared per launch
-        assert ctx.info().duo_timeouts == 2
-    finally:
-        ctx.GPUClean()
-        orc.close()
+    s = shared_kat("LOGQ23", test_lib=True)
+    op, ctx, orc = s["op"], s["ctx"], s["orc"]
+    a, acc = _inputs(op, 9, 400)
+    want = orc.eval_acc(a, 2 * op.N, acc)
+    t0 = ctx.info().duo_timeouts
+    assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+    assert ctx.info().duo_timeouts == t0
+    with ctx.knobs_set(probe=5):
+        got = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(got, want)
+    assert ctx.info().duo_timeouts == t0 + 2
+    assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)  # the failed word is cleared per launch
+    assert ctx.info().duo_timeouts == t0 + 2
 
 
-def test_polynomial_split_form_equals_default(oracle):
+def test_polynomial_split_form_equals_default(shared_kat):
     """The test library's probe 13 runs the round-4/5 two-digit duo (k_blind_rotate_sf2duo, split by accumulator
     polynomial; 1.5-2.4 % slower than sfduo<2> at 128, profiles/r06m): the same outputs as the default form, the
     one-workgroup form and the oracle."""
-    import tfhe_amd
-
-    op, cp = _ctx_params(oracle), _ctx_params(tfhe_amd)
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(79))
-    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    try:
-        a, acc = _inputs(op, 128, 450)
-        dflt = ctx.EvalAcc(a, 2 * op.N, acc)
-        with ctx.knobs_set(probe=13):
-            poly = ctx.EvalAcc(a, 2 * op.N, acc)
-        with ctx.knobs_set(duo=0):
-            one = ctx.EvalAcc(a, 2 * op.N, acc)
-        assert np.array_equal(dflt, poly) and np.array_equal(dflt, one)
-        assert np.array_equal(dflt[[5]].reshape(1, -1), orc.eval_acc(a[[5]], 2 * op.N, acc[[5]]).reshape(1, -1))
-        assert ctx.info().duo_timeouts == 0
-    finally:
-        ctx.GPUClean()
-        orc.close()
+    s = shared_kat("LOGQ23", test_lib=True)
+    op, ctx, orc = s["op"], s["ctx"], s["orc"]
+    a, acc = _inputs(op, 128, 450)
+    t0 = ctx.info().duo_timeouts
+    dflt = ctx.EvalAcc(a, 2 * op.N, acc)
+    with ctx.knobs_set(probe=13):
+        poly = ctx.EvalAcc(a, 2 * op.N, acc)
+    with ctx.knobs_set(duo=0):
+        one = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(dflt, poly) and np.array_equal(dflt, one)
+    assert np.array_equal(dflt[[5]].reshape(1, -1), orc.eval_acc(a[[5]], 2 * op.N, acc[[5]]).reshape(1, -1))
+    assert ctx.info().duo_timeouts == t0

@@ -21,19 +21,12 @@ QIN = 1 << 23
 
 
 @pytest.fixture(scope="module")
-def f64duo(oracle):
-    import tfhe_amd
-
-    op, cp = oracle.params_from_set("STD128Q"), tfhe_amd.params_from_set("STD128Q")
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(91))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+def f64duo(shared_kat):
+    s = shared_kat("STD128Q")  # the session's shared context
+    ctx = s["ctx"]
     assert ctx.info().br_kernel == 3 and ctx.knobs()["duo"] == 128  # f64w with the WRAP fold
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield dict(op=op, ctx=ctx, orc=orc)
+    yield s
     assert ctx.info().duo_timeouts == 0
-    ctx.GPUClean()
-    orc.close()
 
 
 def _inputs(op, B, seed, amod=None):
@@ -196,19 +189,12 @@ def test_f64duo_two_streams_and_two_contexts(oracle):
 # ---- round 6: the STD192 class (k_blind_rotate_f64wduo<0, false, false, 2>: Q < 2^40, no reductions, two
 # transformed digits + C', the top digit eliminated exactly) -- "What's missing" 2 of the round-5 verdict ----
 @pytest.fixture(scope="module")
-def f64duo192(oracle):
-    import tfhe_amd
-
-    op, cp = oracle.params_from_set("STD192"), tfhe_amd.params_from_set("STD192")
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(94))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
+def f64duo192(shared_kat):
+    s = shared_kat("STD192")  # the session's shared context
+    ctx = s["ctx"]
     assert ctx.info().br_kernel == 3 and ctx.knobs()["duo"] == 128
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield dict(op=op, ctx=ctx, orc=orc)
+    yield s
     assert ctx.info().duo_timeouts == 0
-    ctx.GPUClean()
-    orc.close()
 
 
 @pytest.mark.parametrize("B", [1, 9])

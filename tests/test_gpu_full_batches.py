@@ -14,45 +14,26 @@ from helpers import cube_lut, random_cts
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(oracle, spec):
-    import tfhe_amd
-
-    if spec[0] == "set":
-        op, cp = oracle.params_from_set(spec[1]), tfhe_amd.params_from_set(spec[1])
-    else:
-        op, cp = oracle.params_from_logq(*spec[1:]), tfhe_amd.params_from_logq(*spec[1:])
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(5))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    return op, cp, ctx, orc
-
-
-def test_c3_evalfunc_full_batch(oracle):
-    op, cp, ctx, orc = _ctx(oracle, ("logq", "STD128", True, 12, 0, 0, 1))
-    try:
-        assert ctx.info().br_kernel == 5  # special form
-        rs = np.random.default_rng(3)
-        B = 4096
-        ct = random_cts(rs, B, cp.n, cp.q)
-        lut = cube_lut(cp.q)
-        out = ctx.EvalFunc(ct, lut)
-        idx = [0, 1, 2047, 4094, 4095]
-        assert np.array_equal(out[idx], orc.eval_func(ct[idx], lut, cp.q))
-    finally:
-        ctx.GPUClean()
-        orc.close()
+def test_c3_evalfunc_full_batch(shared_kat):
+    s = shared_kat("ARB12")  # the session's shared context
+    cp, ctx, orc = s["cp"], s["ctx"], s["orc"]
+    assert ctx.info().br_kernel == 5  # special form
+    rs = np.random.default_rng(3)
+    B = 4096
+    ct = random_cts(rs, B, cp.n, cp.q)
+    lut = cube_lut(cp.q)
+    out = ctx.EvalFunc(ct, lut)
+    idx = [0, 1, 2047, 4094, 4095]
+    assert np.array_equal(out[idx], orc.eval_func(ct[idx], lut, cp.q))
 
 
-def test_c4_std192_across_the_chunk_boundary(oracle):
-    op, cp, ctx, orc = _ctx(oracle, ("set", "STD192"))
-    try:
-        rs = np.random.default_rng(4)
-        B = 65536 + 3
-        c1 = random_cts(rs, B, cp.n, cp.q)
-        c2 = random_cts(rs, B, cp.n, cp.q)
-        out = ctx.EvalBinGate("NAND", c1, c2)
-        idx = [0, 65535, 65536, B - 1]
-        assert np.array_equal(out[idx], orc.eval_bin_gate("NAND", c1[idx], c2[idx]))
-    finally:
-        ctx.GPUClean()
-        orc.close()
+def test_c4_std192_across_the_chunk_boundary(shared_kat):
+    s = shared_kat("STD192")  # the session's shared context
+    cp, ctx, orc = s["cp"], s["ctx"], s["orc"]
+    rs = np.random.default_rng(4)
+    B = 65536 + 3
+    c1 = random_cts(rs, B, cp.n, cp.q)
+    c2 = random_cts(rs, B, cp.n, cp.q)
+    out = ctx.EvalBinGate("NAND", c1, c2)
+    idx = [0, 65535, 65536, B - 1]
+    assert np.array_equal(out[idx], orc.eval_bin_gate("NAND", c1[idx], c2[idx]))

@@ -5,35 +5,28 @@ workgroup with the whole monomial table in their shared LDS -- the default above
 GenerateBinFHEContext(STD128, true, 12, 0, GINX, false, 1 << 18) -- baseG 2^18, no thrown digit),
 gen3sf takes more (TOY logQ 29: 4, tests/test_gpu_unittest_func.py) and is the cross-check of all
 (knob sf2 = 0).  Per context: EvalAcc on 5 ciphertexts bit-exact against the oracle, and 64
-ciphertexts equal on sf2 and gen3sf.  Keys: Appendix B splitmix64 keys.
+ciphertexts equal on sf2 and gen3sf.  Keys: Appendix B splitmix64 keys (the session's shared contexts).
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-CONTEXTS = {  # name: params_from_logq args, transformed digits
-    "C3_arb_logQ12_thr1": (("STD128", True, 12, 0, 0, 1), 1),
-    "C5b_logQ23_thr1": (("STD128", False, 23, 0, 0, 1), 2),
-    "CHES_func_baseG18": (("STD128", True, 12, 0, 1 << 18, 0), 3),
+CONTEXTS = {  # name: the shared context (conftest.SHARED_SPECS), transformed digits
+    "C3_arb_logQ12_thr1": ("ARB12", 1),
+    "C5b_logQ23_thr1": ("LOGQ23", 2),
+    "CHES_func_baseG18": ("CHES18", 3),
 }
 
 
 @pytest.fixture(scope="module", params=list(CONTEXTS))
-def sfctx(request, oracle):
-    import tfhe_amd
-
-    spec, digits = CONTEXTS[request.param]
-    op, cp = oracle.params_from_logq(*spec), tfhe_amd.params_from_logq(*spec)
+def sfctx(request, shared_kat):
+    name, digits = CONTEXTS[request.param]
+    s = shared_kat(name)
+    op, cp, ctx = s["op"], s["cp"], s["ctx"]
     assert cp.digitsG - cp.numDigitsToThrow == digits and cp.Q == (1 << 54) - 77823
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(91))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
     assert ctx.info().br_kernel == 5  # TFHE_BR_SF
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield op, ctx, orc
-    ctx.GPUClean()
-    orc.close()
+    return op, ctx, s["orc"]
 
 
 def _inputs(op, B, seed):

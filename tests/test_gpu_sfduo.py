@@ -14,8 +14,8 @@ through memory.  Checked through the C-ABI:
   * a partner that never arrives (test library, probe 5): both members time out, the rescue launch recomputes
     the ciphertext, every output stays exact;
   * no partner times out otherwise (tfhe_info.duo_timeouts).
-Keys: the Appendix B splitmix64 keys (parity does not need valid keys); the EvalFunc case uses the oracle's
-keygen.
+Keys: the Appendix B splitmix64 keys (parity does not need valid keys; the session's shared contexts); the
+EvalFunc case uses the oracle's keygen.
 """
 import numpy as np
 import pytest
@@ -27,20 +27,13 @@ SPEC = ("STD128", True, 12, 0, 0, 1)
 
 
 @pytest.fixture(scope="module")
-def sfd(oracle):
-    import tfhe_amd
-
-    op, cp = oracle.params_from_logq(*SPEC), tfhe_amd.params_from_logq(*SPEC)
+def sfd(shared_kat):
+    s = shared_kat("ARB12")
+    cp, ctx = s["cp"], s["ctx"]
     assert cp.digitsG - cp.numDigitsToThrow == 1 and cp.N == 2048 and cp.Q == (1 << 54) - 77823
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(93))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
     assert ctx.info().br_kernel == 5 and ctx.knobs()["duo"] == 128  # TFHE_BR_SF
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield dict(op=op, ctx=ctx, orc=orc)
+    yield s
     assert ctx.info().duo_timeouts == 0
-    ctx.GPUClean()
-    orc.close()
 
 
 def _inputs(op, B, seed):
@@ -119,28 +112,20 @@ def test_sfduo_evalfunc_decrypts(oracle):
         orc.close()
 
 
-def test_sfduo_partner_timeout_is_recomputed(oracle):
+def test_sfduo_partner_timeout_is_recomputed(shared_kat):
     """The test library's probe 5 makes member 1 of pair 0 stop publishing at round 2: both members time out,
     the pair's failed word is set, and the rescue (k_blind_rotate_sf2<1, true>) recomputes that ciphertext from
     its saved input -- every output stays bit-exact and tfhe_info.duo_timeouts counts the two workgroups."""
-    import tfhe_amd
-
-    op, cp = oracle.params_from_logq(*SPEC), tfhe_amd.params_from_logq(*SPEC)
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(94))
-    ctx = tfhe_amd.BinFHEContextHIP(cp, library=tfhe_amd.capi.TEST_LIB).GPUSetup(bsk, ksk)
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    try:
-        a, acc = _inputs(op, 9, 800)
-        want = orc.eval_acc(a, 2 * op.N, acc)
-        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
-        assert ctx.info().duo_timeouts == 0
-        with ctx.knobs_set(probe=5):
-            got = ctx.EvalAcc(a, 2 * op.N, acc)
-        assert np.array_equal(got, want)
-        assert ctx.info().duo_timeouts == 2
-        assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
-        assert ctx.info().duo_timeouts == 2
-    finally:
-        ctx.GPUClean()
-        orc.close()
+    s = shared_kat("ARB12", test_lib=True)
+    op, ctx, orc = s["op"], s["ctx"], s["orc"]
+    a, acc = _inputs(op, 9, 800)
+    want = orc.eval_acc(a, 2 * op.N, acc)
+    t0 = ctx.info().duo_timeouts
+    assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+    assert ctx.info().duo_timeouts == t0
+    with ctx.knobs_set(probe=5):
+        got = ctx.EvalAcc(a, 2 * op.N, acc)
+    assert np.array_equal(got, want)
+    assert ctx.info().duo_timeouts == t0 + 2
+    assert np.array_equal(ctx.EvalAcc(a, 2 * op.N, acc), want)
+    assert ctx.info().duo_timeouts == t0 + 2

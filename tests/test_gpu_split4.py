@@ -14,18 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def std128(oracle):
-    import tfhe_amd
-
-    op, cp = oracle.params_from_set("STD128"), tfhe_amd.params_from_set("STD128")
-    bsk, ksk = oracle.kat_keys(op, oracle.Rng(41))
-    ctx = tfhe_amd.BinFHEContextHIP(cp).GPUSetup(bsk, ksk)
-    assert ctx.info().br_kernel == 1 and ctx.knobs()["split4"] == 384
-    orc = oracle.Oracle(op, bsk, ksk)
-    del bsk, ksk
-    yield dict(op=op, ctx=ctx, orc=orc)
-    ctx.GPUClean()
-    orc.close()
+def std128(shared_kat):
+    s = shared_kat("STD128")  # the session's shared context
+    assert s["ctx"].info().br_kernel == 1 and s["ctx"].knobs()["split4"] == 384
+    return s
 
 
 def _inputs(op, B, seed, amod):
