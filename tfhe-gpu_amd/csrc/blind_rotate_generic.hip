@@ -1449,7 +1449,8 @@ k_blind_rotate_sf2p(BRParams P, SfC K, const uint64_t* __restrict__ psi, const u
 // ---------------------------------------------------------------------------
 // sf2duo: the two-digit sf2 round split over TWO workgroups per ciphertext, for batches too small
 // to fill the chip (round 4: C5b's 128-ciphertext shard of an 8-GPU node ran one workgroup per CU
-// on half the CUs).  Workgroup x of a pair owns accumulator polynomial x: it decomposes acc_x into
+// on half the CUs).  Since round 6 the test library's A/B form only (probe 13): sfduo<2> below, split by NTT
+// half, measured 1.5-3 % faster and is the default.  Workgroup x of a pair owns accumulator polynomial x: it decomposes acc_x into
 // its two digits (threads 0-255 digit 0, 256-511 digit 1: the forward transform of sf2 with the
 // digits in place of the polynomials), multiplies them by key rows 2l + x of both keys and both
 // columns, applies the monomial factors to its partial sums of both columns and inverts both
