@@ -53,8 +53,8 @@ def test_duo_eval_acc_matches_oracle(duo, B):
 
 @pytest.mark.parametrize("B", [64, 128, 129])
 def test_duo_equals_one_workgroup_form(duo, B):
-    """duo = 256 (the knob's maximum): 64 and 128 run sf2duo; 129 is past the device's co-resident pairs (one
-    135-KiB duo workgroup per CU: half of MI355X's 256 CUs), so it runs the one-workgroup kernel (a
+    """duo = 256 (the knob's maximum): 64 and 128 run sfduo<2>; 129 is past the device's co-resident pairs (one
+    148-KiB duo workgroup per CU: half of MI355X's 256 CUs), so it runs the one-workgroup kernel (a
     pair must never wait behind its own launch's pairs); every form equals duo = 0 and the oracle."""
     op, ctx = duo["op"], duo["ctx"]
     a, acc = _inputs(op, B, 200 + B)
