@@ -271,7 +271,8 @@ tfhe_status tfhe_rccl_selftest(int device, size_t bytes, const char* lib, int* v
  * without a lock, as OpenFHE's BinFHEContext is not safe to reconfigure mid-call either). ---- */
 typedef struct tfhe_knobs {
     int32_t ks_tiled_min; /* smallest batch on the batch-tiled key switch; -1: the default (1); 0: never */
-    int32_t ks_cts;       /* ciphertexts per thread in the tiled key switch: 0 (by key width / batch), 1, 2 */
+    int32_t ks_cts;       /* ciphertexts per thread in the tiled key switch: 0 (by key width / batch), 1, 2, 4 (4: the packed
+                             u16 form only -- STD128's keys, its default from 2048 ciphertexts; other widths take 2) */
     int32_t ks_split;     /* most block groups the key-switch steps split over at small batches (1: none) */
     int32_t ks_pk;        /* 0: 32-bit column sums for u16 keys instead of packed u16 pairs */
     int32_t host_parts;   /* sub-batches per device in the host-array runner (>= 1) */

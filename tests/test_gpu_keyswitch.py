@@ -97,11 +97,13 @@ def test_default_threshold_routes_small_batches_to_gather(ks_ctx):
     assert np.array_equal(one, orc.mkm_switch(np.ascontiguousarray(ext[:1]), op.q))
 
 
-@pytest.mark.parametrize("cts", ["1", "2"])
+@pytest.mark.parametrize("cts", ["1", "2", "4"])
 def test_tiled_keyswitch_ciphertexts_per_thread(ks_ctx, cts):
-    """Both tile depths (one or two ciphertexts per thread; the default picks by key width and
-    batch) equal the gather form."""
+    """Every tile depth (one, two or -- the packed u16 form only, STD128's default from 2048 ciphertexts -- four
+    ciphertexts per thread; the default picks by key width and batch) equals the gather form."""
     name, op, ctx, orc = ks_ctx
+    if cts == "4" and not (op.qKS <= (1 << 16) and op.qKS & (op.qKS - 1) == 0):  # u16 keys, packed sums
+        pytest.skip("four per thread: the packed u16 form only (other widths take two)")
     ext = _ext(op, 1029, 13)
     gather = _with_min(ctx, "0", lambda: ctx.MKMSwitch(ext, op.q))
     # 8-byte keys: both the split-word records (ks40 = 1, the default) and the u64 words at both depths

@@ -199,7 +199,7 @@ namespace {
 // The range every knob must lie in (tfhe_set_knobs and the environment alike); nullptr when valid.
 const char* knob_out_of_range(const Knobs& k) {
     if (k.ks_tiled_min < -1) return "ks_tiled_min (TFHE_KS_TILED_MIN) < -1";
-    if (k.ks_cts < 0 || k.ks_cts > 2) return "ks_cts (TFHE_KS_CTS) not in 0..2";
+    if (k.ks_cts < 0 || k.ks_cts > 4 || k.ks_cts == 3) return "ks_cts (TFHE_KS_CTS) not 0, 1, 2 or 4";
     if (k.ks_split < 1) return "ks_split (TFHE_KS_SPLIT) < 1";
     if (k.host_parts < 1) return "host_parts (TFHE_HOST_PARTS) < 1";
     if (k.generic < 0 || k.generic > 2) return "generic (TFHE_GENERIC) not in 0..2";

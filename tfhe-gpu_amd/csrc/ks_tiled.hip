@@ -670,6 +670,8 @@ hipError_t launch_tiled40(const KSParams& P, const void* rec, const void* kskb, 
 }
 
 constexpr size_t kTileMax = 4 * KT;  // the largest ciphertext tile of the builds below
+// (the packed-u16 form's column tile: 16 columns 1.51 ms, 64 columns / four steps per stage exceed the staging
+// builds, against 0.93 ms for 32 columns and two steps at 8192; profiles/r06ks)
 
 size_t ks_tiled_bp(size_t B) { return (B + kTileMax - 1) / kTileMax * kTileMax; }
 
@@ -727,12 +729,21 @@ hipError_t launch_ks_tiled(const KSParams& P, int ksk_bits, const void* kska, co
     // (ARB12 B = 4096 13.8 -> 12.5 ms, logQ = 23 B = 1024 4.06 -> 3.66) and for u32 keys at large
     // batches (STD192 8192 5.81 -> 5.24), not for STD128Q at 1024 (1.26 -> 1.40) or the packed u16
     // form (profiles/r03ks, r03ks2, r03z).  The ks_cts knob (TFHE_KS_CTS) overrides (A/B runs and tests).
-    const int cts = kn.ks_cts ? kn.ks_cts : (ksk_bits == 64 || (ksk_bits == 32 && B >= 4096)) ? 2 : 1;
+    // (ks_cts 4 builds only for the packed u16 form; the other widths take 2 for it)
+    const int cts = kn.ks_cts ? std::min(kn.ks_cts, 2) : (ksk_bits == 64 || (ksk_bits == 32 && B >= 4096)) ? 2 : 1;
+    // the packed u16 form (STD128): four ciphertexts per thread from 2048 ciphertexts -- the KSK (256.5 MiB, at the
+    // Infinity Cache's size) is streamed once per ciphertext tile, so 8192 / 1024 tiles instead of 8192 / 256
+    // (same box, two alternations: 8192 0.927 -> 0.641-0.646 ms, 4096 0.552-0.556 -> 0.372-0.375, 2048 0.33 ->
+    // 0.265-0.276; two per thread 0.79 / 0.47 / 0.28; at 1024 two per thread were slower, 0.217 -> 0.234:
+    // profiles/r06ks2, r06ks3)
+    const int cts16 = kn.ks_cts ? kn.ks_cts : B >= 2048 ? 4 : 1;
     switch (ksk_bits) {
         case 16:  // baseKS = 128 rows per step: two steps per stage keep the LDS at 40 KiB
             // qKS a power of two <= 2^16 (STD128: 2^14): packed u16 sums (ks_pk knob 0: u32 sums, A/B runs)
             if ((P.qKS & (P.qKS - 1)) == 0 && P.qKS <= (1u << 16) && kn.ks_pk)
-                return launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
+                return cts16 == 4   ? launch_tiled<uint16_t, uint32_t, 32, 4, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
+                       : cts16 == 2 ? launch_tiled<uint16_t, uint32_t, 32, 2, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn)
+                                    : launch_tiled<uint16_t, uint32_t, 32, 1, 2, true>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
             return launch_tiled<uint16_t, uint32_t, 32, 1, 2>(P, kska, kskb, dig, bq, B, Bp, fmod, out, part, s, kn);
         case 32:
             // u32 sums also when they wrap mod 2^32 harmlessly: qKS a power of two (STD128Q: 2^25)

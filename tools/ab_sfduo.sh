@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of sfduo builds (tools/alt_generic.sh variants): the blind rotation at 64 / 128 in C3's context
+# Same-box A/B of sfduo builds (tools/alt_build.sh variants): the blind rotation at 64 / 128 in C3's context
 # (tools/duo_probe.py --ctx ARB12: one / duo / no-hand-off rows) and C5b's 128 (tools/small_batch.py duo2),
 # alternating the builds `rounds` times.  GPU box, repo root:  tools/ab_sfduo.sh TAG "LIB_A LIB_B ..." [rounds]
 set -u

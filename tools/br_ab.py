@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Blind rotation alone, device-resident, for same-box A/B of library builds (tools/alt_generic.sh variants):
+"""Blind rotation alone, device-resident, for same-box A/B of library builds (tools/alt_build.sh variants):
 
     python3 tools/br_ab.py --ctx LOGQ23 --batches 1024 [--lib altlib/X/libtfhe_hip_test.so] [--knob k=v ...]
 
