@@ -1,3 +1,6 @@
+#!/bin/bash
+# Same-box A/B of library builds on the key switch alone (tools/ks_bench.py, default split), two alternations:
+#   TAG=r06ks CFGS="STD128" BATCHES=1024,8192 LIBS="lib/a.so altlib/x/libtfhe_hip_test.so" tools/ks16_ab.sh
 set -u
 O=gpurun_out/${TAG:-r06ks}; mkdir -p $O
 for r in 1 2; do
